@@ -1,0 +1,200 @@
+"""Benchmark: batched quadrotor env-steps/s on MI355X (BASELINE.json configs[1]).
+
+Workload (N=1 GPU): 65,536 DroneGymEnv-equivalent envs per GPU, synthetic
+random policy (actions i.i.d. U[0, 7.3575)^4 f32 from Philox, pre-generated
+and resident in HBM before the timed region), DummyVecEnv auto-reset inside
+the step, f64 state (the reference's precision).  One "step" = one
+dr_step over the whole batch.  The K timed steps are captured in one
+hipGraph and replayed (launch-bound loop), bracketed by barrier +
+synchronize on both sides; the max over ranks is taken.
+
+Multi-GPU: one process per GPU (torchrun), independent env shards (global
+env ids rank*N+i), no data-path collective -> "scaling": "weak".
+
+The JSON line also carries
+  roofline      dominant kernel (env_step_kernel): algorithmic bytes per
+                launch (N x 305 B in f64 mode, 197 B in f32) over
+                its average per-launch GPU time from HIP events on the
+                launch stream across the timed region;
+  cpu_baseline  rank 0, N=1: the SubprocVecEnv-equivalent process pool over
+                the fixture-pinned numpy port (oracle/cpu_baseline.py),
+                run BEFORE the GPU is touched;
+  ppo           PPO updates/s for configs[2] (65,536 envs, 2x256 tanh MLP,
+                GAE lambda 0.95), when --ppo-updates > 0.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+BYTES_PER_ENV_STEP = {"f64": 305, "f32": 197}
+HBM_PEAK_GBS = 8000.0      # MI355X HBM3E spec (MI355X_MICROARCH.md)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=1000)
+    ap.add_argument("--warmup", type=int, default=100)
+    ap.add_argument("--envs", type=int, default=65536, help="envs per GPU")
+    ap.add_argument("--state-dtype", choices=["f64", "f32"], default="f64")
+    ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=1.5)
+    ap.add_argument("--ppo-updates", type=int, default=0)
+    ap.add_argument("--extra", action="store_true",
+                    help="also time the f32-state mode and the 4M-env size")
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"))
+    return ap.parse_args()
+
+
+def cpu_baseline(seconds):
+    from oracle.cpu_baseline import cpu_model, run_pool
+    procs = max(1, min(16, len(os.sched_getaffinity(0))))
+    r = run_pool(procs, 64, seconds)
+    return {"value": round(r["value"], 1), "unit": "env-steps/s", "cores": procs,
+            "kind": "port",
+            "sample": (f"{procs} worker processes x 64 numpy-port envs (oracle/drone_np, "
+                       f"bit-exact vs reference), random U[0,7.3575)^4 actions, DummyVecEnv "
+                       f"auto-reset, {r['elapsed']:.2f} s wall each ({r['steps']} env-steps); "
+                       f"SubprocVecEnv-equivalent without pipe IPC; CPU: {cpu_model()}")}
+
+
+def time_env(args, dtype_name, n_envs, rank, world, device, steps, warmup):
+    import torch
+    import torch.distributed as dist
+
+    from drone_rl_amd import DroneBatch, random_actions
+    dtype = torch.float64 if dtype_name == "f64" else torch.float32
+    b = DroneBatch(n_envs, "gym", dtype=dtype, device=device, seed=2025,
+                   env_id_offset=rank * n_envs, auto_reset=True)
+    b.reset()
+    total = warmup + steps
+    # inputs resident in HBM before the timed region
+    acts = torch.empty(total, n_envs, 4, dtype=torch.float32, device=device)
+    for t in range(total):
+        random_actions(n_envs, seed=7, step=t, env_id_offset=rank * n_envs, out=acts[t])
+    for t in range(warmup):
+        b.step(acts[t])
+    stream = torch.cuda.current_stream(device)
+    graph = None
+    if not args.no_graph:
+        s = torch.cuda.Stream(device)
+        s.wait_stream(stream)
+        with torch.cuda.stream(s):
+            graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(graph, stream=s):
+                for t in range(warmup, total):
+                    b.step(acts[t])
+        stream.wait_stream(s)
+    torch.cuda.synchronize(device)
+    ev0 = torch.cuda.Event(enable_timing=True)
+    ev1 = torch.cuda.Event(enable_timing=True)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(device)
+    t0 = time.perf_counter()
+    ev0.record(stream)
+    if graph is not None:
+        graph.replay()
+    else:
+        for t in range(warmup, total):
+            b.step(acts[t])
+    ev1.record(stream)
+    torch.cuda.synchronize(device)
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    gpu_ms = ev0.elapsed_time(ev1)
+    if world > 1:
+        t = torch.tensor([elapsed, gpu_ms], dtype=torch.float64, device=device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed, gpu_ms = float(t[0]), float(t[1])
+    # sanity: the env is alive (episodes end and reset under a random policy)
+    ep = b.get("ep_num").float().mean().item()
+    b.close()
+    del graph
+    return elapsed, gpu_ms, ep
+
+
+def main():
+    args = parse()
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(args.cpu_seconds)      # before any GPU work
+
+    import torch
+    import torch.distributed as dist
+    torch.cuda.set_device(local)
+    device = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=device)
+
+    elapsed, gpu_ms, ep = time_env(args, args.state_dtype, args.envs, rank, world, device,
+                                   args.steps, args.warmup)
+    K, N = args.steps, args.envs
+    value = N * world * K / elapsed
+    per_launch_s = gpu_ms / 1e3 / K
+    bpe = BYTES_PER_ENV_STEP[args.state_dtype]
+    achieved = N * bpe / per_launch_s / 1e9
+    traffic = None
+    try:
+        tj = json.load(open(args.traffic_json))
+        key = f"{args.state_dtype}_{N}"
+        if key in tj:
+            traffic = tj[key]["hbm_bytes_per_launch"]
+    except (OSError, ValueError, KeyError):
+        pass
+    out = {
+        "metric": "env-steps/s (whole node) + PPO updates/s, 65 536 envs/GPU, 2x256 MLP",
+        "value": round(value, 1),
+        "unit": "env-steps/s",
+        "n_gpus": world,
+        "steps": K,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed / K * 1e3, 6),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": args.state_dtype,
+        "data": "synthetic (random policy U[0,7.3575)^4 f32 actions, Philox; "
+                "reset draws Philox)",
+        "config": {"workload": "configs[1]: 65,536 batched DroneGymEnv envs per GPU, "
+                               "random policy, dynamics-kernel throughput (auto-reset in step)",
+                   "envs_per_gpu": N, "global_envs": N * world,
+                   "state_dtype": args.state_dtype, "hipgraph": not args.no_graph,
+                   "parallelism": f"dp{world} (independent env shards)"},
+        "roofline": {"bound": "hbm", "achieved": round(achieved, 1),
+                     "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                     "kernel": "env_step_kernel", "bytes_per_env_step": bpe,
+                     "avg_launch_us": round(per_launch_s * 1e6, 3)},
+        "mean_ep_num": round(ep, 2),
+    }
+    if cpu is not None:
+        out["cpu_baseline"] = cpu
+    if args.extra and world == 1:
+        ex = {}
+        for dn, n in (("f32", N), ("f64", 1 << 22), ("f32", 1 << 22)):
+            k = 200 if n > N else args.steps
+            el, gm, _ = time_env(args, dn, n, 0, 1, device, k, 20)
+            pl = gm / 1e3 / k
+            ex[f"{dn}_{n}"] = {"env_steps_per_s": round(n * k / el, 1),
+                              "avg_launch_us": round(pl * 1e6, 3),
+                              "achieved_GBs": round(n * BYTES_PER_ENV_STEP[dn] / pl / 1e9, 1)}
+        out["extra"] = ex
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

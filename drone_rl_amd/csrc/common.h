@@ -1,0 +1,97 @@
+// Shared helpers for libdronerl.so (gfx950): error plumbing, Philox4x32-10,
+// launch geometry.  Internal header; the public ABI is include/dronerl.h.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <string>
+
+#include "../../include/dronerl.h"
+
+namespace dr {
+
+// ----------------------------------------------------------------------------
+// Errors: a per-thread message for handle-less calls, a per-handle one else.
+// ----------------------------------------------------------------------------
+void set_global_error(const std::string &msg);
+const char *global_error();
+
+#define DR_HIP_CHECK_RET(expr, errsink)                                       \
+    do {                                                                      \
+        hipError_t e__ = (expr);                                              \
+        if (e__ != hipSuccess) {                                              \
+            errsink(std::string(#expr) + ": " + hipGetErrorString(e__));      \
+            return DR_ERR_HIP;                                                \
+        }                                                                     \
+    } while (0)
+
+// RAII device switch: entry points run on the handle's device and restore
+// the caller's current device on exit.
+struct DeviceGuard {
+    int prev = -1;
+    bool switched = false;
+    explicit DeviceGuard(int dev) {
+        if (hipGetDevice(&prev) == hipSuccess && prev != dev) {
+            switched = (hipSetDevice(dev) == hipSuccess);
+        }
+    }
+    ~DeviceGuard() {
+        if (switched) (void)hipSetDevice(prev);
+    }
+};
+
+// ----------------------------------------------------------------------------
+// Philox4x32-10 (Salmon et al., SC'11), counter-based: every (key, counter)
+// pair gives an independent 128-bit block, so env i's draws never depend on
+// how many other envs reset or in which order.
+// ----------------------------------------------------------------------------
+struct u32x4 {
+    uint32_t x, y, z, w;
+};
+
+__host__ __device__ inline u32x4 philox4x32_10(u32x4 c, uint32_t k0,
+                                               uint32_t k1) {
+    constexpr uint32_t M0 = 0xD2511F53u, M1 = 0xCD9E8D57u;
+    constexpr uint32_t W0 = 0x9E3779B9u, W1 = 0xBB67AE85u;
+#pragma unroll
+    for (int r = 0; r < 10; ++r) {
+        const uint64_t p0 = (uint64_t)M0 * c.x;
+        const uint64_t p1 = (uint64_t)M1 * c.z;
+        const uint32_t hi0 = (uint32_t)(p0 >> 32), lo0 = (uint32_t)p0;
+        const uint32_t hi1 = (uint32_t)(p1 >> 32), lo1 = (uint32_t)p1;
+        c = u32x4{hi1 ^ c.y ^ k0, lo1, hi0 ^ c.w ^ k1, lo0};
+        k0 += W0;
+        k1 += W1;
+    }
+    return c;
+}
+
+// 53-bit uniform double in [0,1) from two words (numpy's construction:
+// (a >> 5) * 2^26 + (b >> 6), scaled by 2^-53).
+__host__ __device__ inline double u01_f64(uint32_t a, uint32_t b) {
+    return ((double)(a >> 5) * 67108864.0 + (double)(b >> 6)) *
+           (1.0 / 9007199254740992.0);
+}
+
+// 24-bit uniform float in [0,1).
+__host__ __device__ inline float u01_f32(uint32_t a) {
+    return (float)(a >> 8) * (1.0f / 16777216.0f);
+}
+
+// Stream tags (counter word w) so that different consumers of one key never
+// share a counter.
+enum : uint32_t {
+    TAG_RESET = 0x52000000u,    // env reset uniforms, block index in low bits
+    TAG_ACTION = 0x41000000u,   // synthetic random policy
+    TAG_NORMAL = 0x4E000000u,   // Gaussian policy noise
+    TAG_PERM = 0x50000000u      // minibatch permutation keys
+};
+
+constexpr int kBlock = 256;   // 4 waves of 64
+
+inline unsigned grid_for(int64_t n, int per_block = kBlock) {
+    return (unsigned)((n + per_block - 1) / per_block);
+}
+
+}  // namespace dr

@@ -1,0 +1,738 @@
+// Batched quadrotor environment for MI355X (gfx950).
+//
+// One HIP thread owns one env for the whole step: the state lives in HBM as a
+// struct of arrays (15 arrays of N: pos xyz, vel xyz, euler xyz, omega xyz,
+// target xyz, then step / ep_num / eps / monitor counters), so every state
+// load and store of a wave is one contiguous 512 B (f64) or 256 B (f32)
+// transaction.  Actions arrive as (N,4) f32 (one 16 B load per lane).  The
+// (N,15) f32 observation rows (60 B, not 16 B aligned per env) are staged
+// through LDS and leave the block as contiguous float4 stores.
+//
+// Physics: the reference's op order, restated from
+//   DroneEnv.step            /root/reference/drone.py:81-159
+//   DroneEnv._rotation_matrix /root/reference/drone.py:161-174 (column 2 only)
+//   DroneEnv._euler_angle_rates /root/reference/drone.py:176-186
+//   DroneEnv.reset           /root/reference/drone.py:48-75
+//   DroneEnv._get_obs        /root/reference/drone.py:77-79
+//   VectorizedDroneEnv.*     /root/reference/vectorized_drone.py:38-216
+// compiled with -ffp-contract=off so no product/sum pair is fused into an FMA
+// that numpy would round twice.  The state scalar S is double (reference
+// precision) or float (throughput mode).
+
+#include <cstring>
+#include <new>
+#include <string>
+
+#include "common.h"
+
+#pragma clang fp contract(off)
+
+namespace dr {
+namespace {
+
+// Physical constants (drone.py:14-43, 263; vectorized_drone.py:13-33).
+constexpr double kG = 9.81;
+constexpr double kMass = 1.0;
+constexpr double kIxx = 0.005, kIyy = 0.005, kIzz = 0.01;
+constexpr double kArm = 0.5;
+constexpr double kFactor = kArm / 1.4142135623730951;  // L / np.sqrt(2)
+constexpr float kKyaw32 = 0.01f;  // python float * np.float32 -> f32 (NEP 50)
+constexpr double kDt = 0.02;
+
+__device__ inline double m_sin(double x) { return sin(x); }
+__device__ inline float m_sin(float x) { return sinf(x); }
+__device__ inline double m_cos(double x) { return cos(x); }
+__device__ inline float m_cos(float x) { return cosf(x); }
+__device__ inline double m_tan(double x) { return tan(x); }
+__device__ inline float m_tan(float x) { return tanf(x); }
+__device__ inline double m_sqrt(double x) { return sqrt(x); }
+__device__ inline float m_sqrt(float x) { return sqrtf(x); }
+
+enum : int { F_POS = 0, F_VEL = 3, F_EUL = 6, F_OMG = 9, F_TGT = 12, F_N = 15 };
+
+template <typename S>
+struct EnvView {
+    S *f;             // F_N arrays, array k at f + k * stride
+    int64_t stride;
+    int32_t *step;
+    int32_t *ep_num;
+    double *eps;
+    float *ep_ret;
+    int32_t *ep_len;
+    int64_t n;
+    int64_t env_id_offset;
+    const double *host_u;  // DR_RNG_HOST_UNIFORMS buffer, else nullptr
+    uint32_t seed_lo, seed_hi;
+    int32_t max_steps;
+    S dt;
+    __host__ __device__ S *field(int k) const { return f + k * stride; }
+};
+
+struct StepIO {
+    const float *actions;
+    float *obs;
+    float *rew;
+    uint8_t *done;
+    float *term_obs;
+    float *ep_ret_out;
+    int32_t *ep_len_out;
+    int auto_reset;
+};
+
+// The five reset draws of env i starting episode `ep_new`, in the reference
+// order: pos x, pos y, target x, y, z (drone.py:57,73).  mode: 0 Philox,
+// 1 host buffer, 2 constant 0.5 (constructor reset in host-uniform mode).
+template <typename S>
+__device__ inline void reset_uniforms(const EnvView<S> &v, int64_t i,
+                                      int32_t ep_new, int mode, double u[5]) {
+    if (mode == 1) {
+#pragma unroll
+        for (int k = 0; k < 5; ++k) u[k] = v.host_u[i * 5 + k];
+        return;
+    }
+    if (mode == 2) {
+#pragma unroll
+        for (int k = 0; k < 5; ++k) u[k] = 0.5;
+        return;
+    }
+    const uint64_t gid = (uint64_t)(v.env_id_offset + i);
+    u32x4 c{(uint32_t)ep_new, (uint32_t)gid, (uint32_t)(gid >> 32), TAG_RESET};
+    const u32x4 r0 = philox4x32_10(c, v.seed_lo, v.seed_hi);
+    c.w = TAG_RESET | 1u;
+    const u32x4 r1 = philox4x32_10(c, v.seed_lo, v.seed_hi);
+    c.w = TAG_RESET | 2u;
+    const u32x4 r2 = philox4x32_10(c, v.seed_lo, v.seed_hi);
+    u[0] = u01_f64(r0.x, r0.y);
+    u[1] = u01_f64(r0.z, r0.w);
+    u[2] = u01_f64(r1.x, r1.y);
+    u[3] = u01_f64(r1.z, r1.w);
+    u[4] = u01_f64(r2.x, r2.y);
+}
+
+// DroneEnv.reset (drone.py:48-75) on registers st[F_N]; updates ep_num/eps
+// in memory, returns the new step counter (0).
+template <typename S>
+__device__ inline void gym_reset_regs(const EnvView<S> &v, int64_t i, int mode,
+                                      S st[F_N]) {
+    const int32_t ep_new = v.ep_num[i] + 1;   // ep_num += 1          (61)
+    double u[5];
+    reset_uniforms(v, i, ep_new, mode, u);
+    double eps = v.eps[i];
+    if (ep_new % 2000 == 0) {                 // curriculum bump      (68-70)
+        eps += 0.1;
+        v.eps[i] = eps;
+    }
+    v.ep_num[i] = ep_new;
+    st[F_POS + 0] = (S)(u[0] - 0.5);          // (57)
+    st[F_POS + 1] = (S)(u[1] - 0.5);
+    st[F_POS + 2] = (S)1.0;
+#pragma unroll
+    for (int k = 3; k < 12; ++k) st[k] = (S)0;   // vel, euler, omega (58-60)
+    st[F_TGT + 0] = (S)(eps * u[2]);          // (73)
+    st[F_TGT + 1] = (S)(eps * u[3]);
+    st[F_TGT + 2] = (S)(eps * u[4] + 1.0 + 0.0);
+}
+
+template <typename S>
+__device__ inline void vec_reset_regs(S st[F_N]) {
+    // VectorizedDroneEnv.reset: every env at (0.1,0.1,0.1), at rest
+    // (vectorized_drone.py:50-53); fixed target (0,0,10) (line 30).
+#pragma unroll
+    for (int k = 0; k < 3; ++k) st[F_POS + k] = (S)0.1;
+#pragma unroll
+    for (int k = 3; k < 12; ++k) st[k] = (S)0;
+    st[F_TGT + 0] = (S)0;
+    st[F_TGT + 1] = (S)0;
+    st[F_TGT + 2] = (S)10.0;
+}
+
+template <typename S, int OD>
+__device__ inline void make_obs(const S st[F_N], float ob[OD]) {
+    // _get_obs: f32(concat(pos, vel, euler, omega[, target - pos]))  (79)
+#pragma unroll
+    for (int k = 0; k < 12; ++k) ob[k] = (float)st[k];
+    if constexpr (OD == 15) {
+#pragma unroll
+        for (int k = 0; k < 3; ++k) ob[12 + k] = (float)(st[F_TGT + k] - st[F_POS + k]);
+    }
+}
+
+// One physics step on registers.  Returns the reward, sets `crash` (z<0 or
+// |p|>50).  VAR selects the two places the variants differ (W row 3 and the
+// reward form / bonus radius).
+template <typename S, int VAR>
+__device__ inline S physics_step(S st[F_N], float4 act, S dt, bool &crash) {
+    const float a0 = act.x, a1 = act.y, a2 = act.z, a3 = act.w;
+    // thrust / torques (drone.py:106, 113-117): f32 sums, f64 factor product,
+    // the yaw torque stays f32.
+    const float thr = ((a0 + a1) + a2) + a3;
+    const S tau_phi = (S)kFactor * (S)(((a0 + a1) - a2) - a3);
+    const S tau_theta = (S)kFactor * (S)(((-a0 + a1) + a2) - a3);
+    const float tau_psi = kKyaw32 * (((a0 - a1) + a2) - a3);
+
+    const S phi = st[F_EUL + 0], theta = st[F_EUL + 1], psi = st[F_EUL + 2];
+    const S cph = m_cos(phi), sph = m_sin(phi);
+    const S cth = m_cos(theta), sth = m_sin(theta);
+    const S cps = m_cos(psi), sps = m_sin(psi);
+    // R(old euler) column 2 (drone.py:169-173): thrust is body-z only.
+    const S r02 = cps * sth * cph + sps * sph;
+    const S r12 = sps * sth * cph - cps * sph;
+    const S r22 = cth * cph;
+    const S T = (S)thr;
+    const S acc0 = (S)0 + (r02 * T) / (S)kMass;      // (124)
+    const S acc1 = (S)0 + (r12 * T) / (S)kMass;
+    const S acc2 = (S)(-kG) + (r22 * T) / (S)kMass;
+    st[F_VEL + 0] += acc0 * dt;                      // (127)
+    st[F_VEL + 1] += acc1 * dt;
+    st[F_VEL + 2] += acc2 * dt;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) st[F_POS + k] += st[F_VEL + k] * dt;  // (128)
+
+    // Euler-angle rates from the OLD omega (131-132, 176-186).
+    const S w0 = st[F_OMG + 0], w1 = st[F_OMG + 1], w2 = st[F_OMG + 2];
+    const S tth = m_tan(theta);
+    S ed2;
+    if constexpr (VAR == DR_VARIANT_GYM) {
+        ed2 = ((S)0 * w0 + (sph / cth) * w1) + (cph / cth) * w2;      // (184)
+    } else {
+        const S sec = (S)1 / cth;                                      // vd:116
+        ed2 = ((S)0 * w0 + (sph * sec) * w1) + (cph * sec) * w2;
+    }
+    const S ed0 = ((S)1 * w0 + (sph * tth) * w1) + (cph * tth) * w2;
+    const S ed1 = ((S)0 * w0 + cph * w1) + (-sph) * w2;
+    st[F_EUL + 0] += ed0 * dt;
+    st[F_EUL + 1] += ed1 * dt;
+    st[F_EUL + 2] += ed2 * dt;
+
+    // Angular dynamics, diagonal inertia, old omega (135-139).
+    const S wd0 = (tau_phi - (S)(kIyy - kIzz) * w1 * w2) / (S)kIxx;
+    const S wd1 = (tau_theta - (S)(kIzz - kIxx) * w0 * w2) / (S)kIyy;
+    const S wd2 = ((S)tau_psi - (S)(kIxx - kIyy) * w0 * w1) / (S)kIzz;
+    st[F_OMG + 0] += wd0 * dt;
+    st[F_OMG + 1] += wd1 * dt;
+    st[F_OMG + 2] += wd2 * dt;
+
+    // Reward on the new position (142-148; vectorized_drone.py:204-207).
+    const S dx = st[F_POS + 0] - st[F_TGT + 0];
+    const S dy = st[F_POS + 1] - st[F_TGT + 1];
+    const S dz = st[F_POS + 2] - st[F_TGT + 2];
+    const S d = m_sqrt((dx * dx + dy * dy) + dz * dz);
+    S r;
+    if constexpr (VAR == DR_VARIANT_GYM) {
+        r = (S)0.01 * -d;
+        if (d < (S)0.05) r += (S)1;
+    } else {
+        r = (S)(-0.01) * d;
+        if (d < (S)1) r += (S)1;
+    }
+    // Termination (154; vectorized_drone.py:211).  NaN compares false.
+    const S px = st[F_POS + 0], py = st[F_POS + 1], pz = st[F_POS + 2];
+    const S pn = m_sqrt((px * px + py * py) + pz * pz);
+    crash = (pz < (S)0) || (pn > (S)50);
+    return r;
+}
+
+template <int OD>
+__device__ inline void store_obs_block(float *sh, const float ob[OD],
+                                       float *dst_all, int64_t base,
+                                       int64_t n) {
+    const int tid = threadIdx.x;
+#pragma unroll
+    for (int k = 0; k < OD; ++k) sh[tid * OD + k] = ob[k];
+    __syncthreads();
+    const int64_t nvalid = (n - base) < kBlock ? (n - base) : kBlock;
+    float *dst = dst_all + base * OD;
+    const int total = (int)nvalid * OD;
+    if (nvalid == kBlock && (((uintptr_t)dst) & 15) == 0) {
+        const float4 *s4 = reinterpret_cast<const float4 *>(sh);
+        float4 *d4 = reinterpret_cast<float4 *>(dst);
+#pragma unroll
+        for (int q = tid; q < kBlock * OD / 4; q += kBlock) d4[q] = s4[q];
+    } else {
+        for (int q = tid; q < total; q += kBlock) dst[q] = sh[q];
+    }
+}
+
+template <typename S, int VAR, bool MON>
+__global__ __launch_bounds__(kBlock) void env_step_kernel(EnvView<S> v,
+                                                          StepIO io) {
+    constexpr int OD = (VAR == DR_VARIANT_GYM) ? 15 : 12;
+    __shared__ float4 sh4[kBlock * OD / 4];
+    const int64_t base = (int64_t)blockIdx.x * kBlock;
+    const int64_t i = base + threadIdx.x;
+    float ob[OD];
+    if (i < v.n) {
+        S st[F_N];
+#pragma unroll
+        for (int k = 0; k < 12; ++k) st[k] = v.field(k)[i];
+        if constexpr (VAR == DR_VARIANT_GYM) {
+#pragma unroll
+            for (int k = F_TGT; k < F_N; ++k) st[k] = v.field(k)[i];
+        } else {
+            st[F_TGT + 0] = (S)0;
+            st[F_TGT + 1] = (S)0;
+            st[F_TGT + 2] = (S)10.0;
+        }
+        const float4 act = reinterpret_cast<const float4 *>(io.actions)[i];
+        int32_t step = v.step[i];
+
+        bool crash;
+        const S r = physics_step<S, VAR>(st, act, v.dt, crash);
+        step += 1;                                         // (155)
+        bool done = crash || (step >= v.max_steps);        // (156-157)
+        const float rf = (float)r;                         // SB3 f32 buffer
+        io.rew[i] = rf;
+        io.done[i] = (uint8_t)done;
+        make_obs<S, OD>(st, ob);
+
+        float ret = 0.f;
+        int32_t len = 0;
+        if constexpr (MON) {
+            ret = v.ep_ret[i] + rf;                        // VecMonitor
+            len = v.ep_len[i] + 1;
+        }
+        if constexpr (VAR == DR_VARIANT_GYM) {
+            if (done && io.auto_reset) {
+                // DummyVecEnv: keep the terminal obs, reset in the same step.
+                if (io.term_obs) {
+#pragma unroll
+                    for (int k = 0; k < OD; ++k) io.term_obs[i * OD + k] = ob[k];
+                }
+                gym_reset_regs(v, i, v.host_u ? 1 : 0, st);
+                step = 0;
+#pragma unroll
+                for (int k = F_TGT; k < F_N; ++k) v.field(k)[i] = st[k];
+                make_obs<S, OD>(st, ob);
+            }
+        }
+        if constexpr (MON) {
+            if (done) {           // VecMonitor: report, then restart counters
+                io.ep_ret_out[i] = ret;
+                io.ep_len_out[i] = len;
+                ret = 0.f;
+                len = 0;
+            }
+            v.ep_ret[i] = ret;
+            v.ep_len[i] = len;
+        }
+#pragma unroll
+        for (int k = 0; k < 12; ++k) v.field(k)[i] = st[k];
+        v.step[i] = step;
+    } else {
+#pragma unroll
+        for (int k = 0; k < OD; ++k) ob[k] = 0.f;
+    }
+    store_obs_block<OD>(reinterpret_cast<float *>(sh4), ob, io.obs, base, v.n);
+}
+
+// Reset (all envs, or those with mask[i] != 0) and write every env's obs.
+// mode: 0 Philox, 1 host uniforms, 2 constant 0.5.  `init` additionally
+// clears ep_num / eps / monitor counters first (constructor).
+template <typename S, int VAR>
+__global__ __launch_bounds__(kBlock) void env_reset_kernel(EnvView<S> v,
+                                                           const uint8_t *mask,
+                                                           float *obs, int mode,
+                                                           int init) {
+    constexpr int OD = (VAR == DR_VARIANT_GYM) ? 15 : 12;
+    __shared__ float4 sh4[kBlock * OD / 4];
+    const int64_t base = (int64_t)blockIdx.x * kBlock;
+    const int64_t i = base + threadIdx.x;
+    float ob[OD];
+    if (i < v.n) {
+        if (init) {
+            v.ep_num[i] = 0;
+            v.eps[i] = 0.0;
+            v.ep_ret[i] = 0.f;
+            v.ep_len[i] = 0;
+        }
+        S st[F_N];
+        const bool doit = (mask == nullptr) || mask[i];
+        if (doit) {
+            if constexpr (VAR == DR_VARIANT_GYM) {
+                gym_reset_regs(v, i, mode, st);
+            } else {
+                vec_reset_regs(st);
+            }
+#pragma unroll
+            for (int k = 0; k < F_N; ++k) v.field(k)[i] = st[k];
+            v.step[i] = 0;
+        } else {
+#pragma unroll
+            for (int k = 0; k < F_N; ++k) st[k] = v.field(k)[i];
+        }
+        make_obs<S, OD>(st, ob);
+    } else {
+#pragma unroll
+        for (int k = 0; k < OD; ++k) ob[k] = 0.f;
+    }
+    if (obs) store_obs_block<OD>(reinterpret_cast<float *>(sh4), ob, obs, base, v.n);
+}
+
+template <typename S>
+__global__ void get_field_kernel(EnvView<S> v, int field, void *out) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= v.n) return;
+    if (field <= DR_FIELD_TARGET) {
+        double *o = static_cast<double *>(out);
+#pragma unroll
+        for (int k = 0; k < 3; ++k) o[i * 3 + k] = (double)v.field(field * 3 + k)[i];
+    } else if (field == DR_FIELD_STEP) {
+        static_cast<int32_t *>(out)[i] = v.step[i];
+    } else if (field == DR_FIELD_EP_NUM) {
+        static_cast<int32_t *>(out)[i] = v.ep_num[i];
+    } else if (field == DR_FIELD_EPS) {
+        static_cast<double *>(out)[i] = v.eps[i];
+    } else if (field == DR_FIELD_EP_RETURN) {
+        static_cast<float *>(out)[i] = v.ep_ret[i];
+    } else if (field == DR_FIELD_EP_LENGTH) {
+        static_cast<int32_t *>(out)[i] = v.ep_len[i];
+    }
+}
+
+template <typename S>
+__global__ void set_field_kernel(EnvView<S> v, int field, const void *in) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= v.n) return;
+    if (field <= DR_FIELD_TARGET) {
+        const double *p = static_cast<const double *>(in);
+#pragma unroll
+        for (int k = 0; k < 3; ++k) v.field(field * 3 + k)[i] = (S)p[i * 3 + k];
+    } else if (field == DR_FIELD_STEP) {
+        v.step[i] = static_cast<const int32_t *>(in)[i];
+    } else if (field == DR_FIELD_EP_NUM) {
+        v.ep_num[i] = static_cast<const int32_t *>(in)[i];
+    } else if (field == DR_FIELD_EPS) {
+        v.eps[i] = static_cast<const double *>(in)[i];
+    } else if (field == DR_FIELD_EP_RETURN) {
+        v.ep_ret[i] = static_cast<const float *>(in)[i];
+    } else if (field == DR_FIELD_EP_LENGTH) {
+        v.ep_len[i] = static_cast<const int32_t *>(in)[i];
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void random_actions_kernel(
+    int64_t n, uint32_t k0, uint32_t k1, int64_t env_off, uint64_t step,
+    float lo, float span, float4 *out) {
+    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n) return;
+    const uint64_t gid = (uint64_t)(env_off + i);
+    const u32x4 r = philox4x32_10(
+        u32x4{(uint32_t)step, (uint32_t)(step >> 32), (uint32_t)gid,
+              TAG_ACTION ^ (uint32_t)(gid >> 32)},
+        k0, k1);
+    out[i] = make_float4(lo + span * u01_f32(r.x), lo + span * u01_f32(r.y),
+                         lo + span * u01_f32(r.z), lo + span * u01_f32(r.w));
+}
+
+}  // namespace
+}  // namespace dr
+
+// ============================================================================
+// C ABI
+// ============================================================================
+using namespace dr;
+
+struct dr_handle {
+    dr_config cfg{};
+    int64_t n = 0;
+    int64_t stride = 0;
+    int obs_dim = 15;
+    void *mem = nullptr;
+    const double *host_u = nullptr;
+    std::string err;
+};
+
+namespace dr {
+static thread_local std::string g_err;
+void set_global_error(const std::string &msg) { g_err = msg; }
+const char *global_error() { return g_err.c_str(); }
+}  // namespace dr
+
+namespace {
+
+int fail(dr_handle *h, int code, const std::string &msg) {
+    if (h)
+        h->err = msg;
+    else
+        set_global_error(msg);
+    return code;
+}
+
+template <typename S>
+EnvView<S> view_of(const dr_handle *h) {
+    EnvView<S> v{};
+    char *m = static_cast<char *>(h->mem);
+    const int64_t sp = h->stride;
+    v.f = reinterpret_cast<S *>(m);
+    v.stride = sp;
+    m += (size_t)F_N * sp * sizeof(S);
+    v.eps = reinterpret_cast<double *>(m);
+    m += sp * sizeof(double);
+    v.step = reinterpret_cast<int32_t *>(m);
+    m += sp * sizeof(int32_t);
+    v.ep_num = reinterpret_cast<int32_t *>(m);
+    m += sp * sizeof(int32_t);
+    v.ep_ret = reinterpret_cast<float *>(m);
+    m += sp * sizeof(float);
+    v.ep_len = reinterpret_cast<int32_t *>(m);
+    v.n = h->n;
+    v.env_id_offset = h->cfg.env_id_offset;
+    v.host_u = h->host_u;
+    v.seed_lo = (uint32_t)h->cfg.seed;
+    v.seed_hi = (uint32_t)(h->cfg.seed >> 32);
+    v.max_steps = h->cfg.max_steps;
+    v.dt = (S)h->cfg.dt;
+    return v;
+}
+
+size_t state_bytes(int64_t stride, int dtype) {
+    const size_t s = dtype == DR_STATE_F64 ? sizeof(double) : sizeof(float);
+    return (size_t)F_N * stride * s + (size_t)stride * (8 + 4 + 4 + 4 + 4);
+}
+
+inline hipStream_t as_stream(void *s) { return static_cast<hipStream_t>(s); }
+
+template <typename S, int VAR>
+int launch_reset(dr_handle *h, const uint8_t *mask, float *obs, int mode,
+                 int init, hipStream_t st) {
+    EnvView<S> v = view_of<S>(h);
+    hipLaunchKernelGGL((env_reset_kernel<S, VAR>), dim3(grid_for(h->n)),
+                       dim3(kBlock), 0, st, v, mask, obs, mode, init);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess)
+        return fail(h, DR_ERR_HIP, std::string("env_reset_kernel: ") + hipGetErrorString(e));
+    return DR_OK;
+}
+
+int dispatch_reset(dr_handle *h, const uint8_t *mask, float *obs, int mode,
+                   int init, hipStream_t st) {
+    const bool f64 = h->cfg.state_dtype == DR_STATE_F64;
+    if (h->cfg.variant == DR_VARIANT_GYM)
+        return f64 ? launch_reset<double, DR_VARIANT_GYM>(h, mask, obs, mode, init, st)
+                   : launch_reset<float, DR_VARIANT_GYM>(h, mask, obs, mode, init, st);
+    return f64 ? launch_reset<double, DR_VARIANT_VECTORIZED>(h, mask, obs, mode, init, st)
+               : launch_reset<float, DR_VARIANT_VECTORIZED>(h, mask, obs, mode, init, st);
+}
+
+template <typename S, int VAR, bool MON>
+int launch_step(dr_handle *h, const StepIO &io, hipStream_t st) {
+    EnvView<S> v = view_of<S>(h);
+    hipLaunchKernelGGL((env_step_kernel<S, VAR, MON>), dim3(grid_for(h->n)),
+                       dim3(kBlock), 0, st, v, io);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess)
+        return fail(h, DR_ERR_HIP, std::string("env_step_kernel: ") + hipGetErrorString(e));
+    return DR_OK;
+}
+
+template <bool MON>
+int dispatch_step(dr_handle *h, const StepIO &io, hipStream_t st) {
+    const bool f64 = h->cfg.state_dtype == DR_STATE_F64;
+    if (h->cfg.variant == DR_VARIANT_GYM)
+        return f64 ? launch_step<double, DR_VARIANT_GYM, MON>(h, io, st)
+                   : launch_step<float, DR_VARIANT_GYM, MON>(h, io, st);
+    return f64 ? launch_step<double, DR_VARIANT_VECTORIZED, MON>(h, io, st)
+               : launch_step<float, DR_VARIANT_VECTORIZED, MON>(h, io, st);
+}
+
+int check_rng(dr_handle *h) {
+    if (h->cfg.rng_mode == DR_RNG_HOST_UNIFORMS && h->host_u == nullptr &&
+        h->cfg.variant == DR_VARIANT_GYM)
+        return fail(h, DR_ERR_INVALID,
+                    "rng_mode DR_RNG_HOST_UNIFORMS: call dr_set_reset_uniforms first");
+    return DR_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int dr_abi_version(void) { return DR_ABI_VERSION; }
+
+int dr_create(const dr_config *cfg_in, dr_handle **out) {
+    if (!cfg_in || !out) return fail(nullptr, DR_ERR_INVALID, "dr_create: null argument");
+    *out = nullptr;
+    dr_config cfg = *cfg_in;
+    if (cfg.num_envs < 1) return fail(nullptr, DR_ERR_INVALID, "dr_create: num_envs must be >= 1");
+    if (cfg.variant != DR_VARIANT_GYM && cfg.variant != DR_VARIANT_VECTORIZED)
+        return fail(nullptr, DR_ERR_INVALID, "dr_create: unknown variant");
+    if (cfg.state_dtype != DR_STATE_F64 && cfg.state_dtype != DR_STATE_F32)
+        return fail(nullptr, DR_ERR_INVALID, "dr_create: unknown state_dtype");
+    if (cfg.rng_mode != DR_RNG_PHILOX && cfg.rng_mode != DR_RNG_HOST_UNIFORMS)
+        return fail(nullptr, DR_ERR_INVALID, "dr_create: unknown rng_mode");
+    if (cfg.num_envs > (int64_t)1 << 31)
+        return fail(nullptr, DR_ERR_INVALID, "dr_create: num_envs above 2^31 per handle");
+    if (cfg.max_steps == 0) cfg.max_steps = cfg.variant == DR_VARIANT_GYM ? 200 : 1000;
+    if (cfg.max_steps < 0) return fail(nullptr, DR_ERR_INVALID, "dr_create: max_steps < 0");
+    if (cfg.dt == 0.0) cfg.dt = kDt;
+    if (cfg.variant == DR_VARIANT_VECTORIZED) cfg.auto_reset = 0;
+
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0)
+        return fail(nullptr, DR_ERR_HIP, "dr_create: no HIP device available");
+    if (cfg.device < 0 || cfg.device >= ndev)
+        return fail(nullptr, DR_ERR_INVALID, "dr_create: device ordinal out of range");
+
+    dr_handle *h = new (std::nothrow) dr_handle();
+    if (!h) return fail(nullptr, DR_ERR_NOMEM, "dr_create: host allocation failed");
+    h->cfg = cfg;
+    h->n = cfg.num_envs;
+    h->stride = (cfg.num_envs + 63) / 64 * 64;
+    h->obs_dim = cfg.variant == DR_VARIANT_GYM ? 15 : 12;
+
+    DeviceGuard g(cfg.device);
+    const size_t bytes = state_bytes(h->stride, cfg.state_dtype);
+    hipError_t e = hipMalloc(&h->mem, bytes);
+    if (e != hipSuccess) {
+        delete h;
+        return fail(nullptr, DR_ERR_NOMEM, std::string("dr_create: hipMalloc: ") + hipGetErrorString(e));
+    }
+    // Constructor reset (drone.py:46): ep_num 0 -> 1.
+    const int mode = cfg.rng_mode == DR_RNG_PHILOX ? 0 : 2;
+    int rc = dispatch_reset(h, nullptr, nullptr, mode, 1, nullptr);
+    if (rc == DR_OK) {
+        e = hipDeviceSynchronize();
+        if (e != hipSuccess) rc = fail(h, DR_ERR_HIP, hipGetErrorString(e));
+    }
+    if (rc != DR_OK) {
+        set_global_error(h->err);
+        (void)hipFree(h->mem);
+        delete h;
+        return rc;
+    }
+    *out = h;
+    return DR_OK;
+}
+
+int dr_destroy(dr_handle *h) {
+    if (!h) return DR_OK;
+    DeviceGuard g(h->cfg.device);
+    if (h->mem) {
+        // The caller's streams may still use the state: drain first.
+        (void)hipDeviceSynchronize();
+        (void)hipFree(h->mem);
+    }
+    delete h;
+    return DR_OK;
+}
+
+int64_t dr_num_envs(const dr_handle *h) { return h ? h->n : -1; }
+int dr_obs_dim(const dr_handle *h) { return h ? h->obs_dim : -1; }
+
+int dr_reset(dr_handle *h, float *obs_out, void *stream) {
+    if (!h) return fail(nullptr, DR_ERR_INVALID, "dr_reset: null handle");
+    if (!obs_out) return fail(h, DR_ERR_INVALID, "dr_reset: obs_out is null");
+    int rc = check_rng(h);
+    if (rc) return rc;
+    DeviceGuard g(h->cfg.device);
+    return dispatch_reset(h, nullptr, obs_out, h->host_u ? 1 : 0, 0, as_stream(stream));
+}
+
+int dr_reset_masked(dr_handle *h, const uint8_t *mask, float *obs_out, void *stream) {
+    if (!h) return fail(nullptr, DR_ERR_INVALID, "dr_reset_masked: null handle");
+    if (!mask) return fail(h, DR_ERR_INVALID, "dr_reset_masked: mask is null");
+    if (h->cfg.variant != DR_VARIANT_GYM)
+        return fail(h, DR_ERR_UNSUPPORTED, "dr_reset_masked: vectorized variant resets globally");
+    int rc = check_rng(h);
+    if (rc) return rc;
+    DeviceGuard g(h->cfg.device);
+    return dispatch_reset(h, mask, obs_out, h->host_u ? 1 : 0, 0, as_stream(stream));
+}
+
+static int step_common(dr_handle *h, const float *actions, float *obs_out,
+                       float *rew_out, uint8_t *done_out, float *term_obs_out,
+                       float *ep_ret_out, int32_t *ep_len_out, bool mon,
+                       void *stream) {
+    if (!h) return fail(nullptr, DR_ERR_INVALID, "dr_step: null handle");
+    if (!actions || !obs_out || !rew_out || !done_out)
+        return fail(h, DR_ERR_INVALID, "dr_step: actions/obs/rew/done must be non-null");
+    if (((uintptr_t)actions) & 15)
+        return fail(h, DR_ERR_INVALID, "dr_step: actions must be 16-byte aligned");
+    if (mon && (!ep_ret_out || !ep_len_out))
+        return fail(h, DR_ERR_INVALID, "dr_step_monitored: episode outputs must be non-null");
+    if (h->cfg.auto_reset) {
+        int rc = check_rng(h);
+        if (rc) return rc;
+    }
+    StepIO io{actions, obs_out, rew_out, done_out, term_obs_out, ep_ret_out,
+              ep_len_out, h->cfg.auto_reset};
+    DeviceGuard g(h->cfg.device);
+    return mon ? dispatch_step<true>(h, io, as_stream(stream))
+               : dispatch_step<false>(h, io, as_stream(stream));
+}
+
+int dr_step(dr_handle *h, const float *actions, float *obs_out, float *rew_out,
+            uint8_t *done_out, float *terminal_obs_out, void *stream) {
+    return step_common(h, actions, obs_out, rew_out, done_out, terminal_obs_out,
+                       nullptr, nullptr, false, stream);
+}
+
+int dr_step_monitored(dr_handle *h, const float *actions, float *obs_out,
+                      float *rew_out, uint8_t *done_out, float *terminal_obs_out,
+                      float *ep_return_out, int32_t *ep_length_out, void *stream) {
+    return step_common(h, actions, obs_out, rew_out, done_out, terminal_obs_out,
+                       ep_return_out, ep_length_out, true, stream);
+}
+
+int dr_get_state(dr_handle *h, int field, void *out, void *stream) {
+    if (!h) return fail(nullptr, DR_ERR_INVALID, "dr_get_state: null handle");
+    if (!out) return fail(h, DR_ERR_INVALID, "dr_get_state: out is null");
+    if (field < DR_FIELD_POS || field > DR_FIELD_EP_LENGTH)
+        return fail(h, DR_ERR_INVALID, "dr_get_state: unknown field");
+    DeviceGuard g(h->cfg.device);
+    if (h->cfg.state_dtype == DR_STATE_F64)
+        hipLaunchKernelGGL(get_field_kernel<double>, dim3(grid_for(h->n)), dim3(kBlock), 0,
+                           as_stream(stream), view_of<double>(h), field, out);
+    else
+        hipLaunchKernelGGL(get_field_kernel<float>, dim3(grid_for(h->n)), dim3(kBlock), 0,
+                           as_stream(stream), view_of<float>(h), field, out);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return fail(h, DR_ERR_HIP, std::string("get_field: ") + hipGetErrorString(e));
+    return DR_OK;
+}
+
+int dr_set_state(dr_handle *h, int field, const void *in, void *stream) {
+    if (!h) return fail(nullptr, DR_ERR_INVALID, "dr_set_state: null handle");
+    if (!in) return fail(h, DR_ERR_INVALID, "dr_set_state: in is null");
+    if (field < DR_FIELD_POS || field > DR_FIELD_EP_LENGTH)
+        return fail(h, DR_ERR_INVALID, "dr_set_state: unknown field");
+    DeviceGuard g(h->cfg.device);
+    if (h->cfg.state_dtype == DR_STATE_F64)
+        hipLaunchKernelGGL(set_field_kernel<double>, dim3(grid_for(h->n)), dim3(kBlock), 0,
+                           as_stream(stream), view_of<double>(h), field, in);
+    else
+        hipLaunchKernelGGL(set_field_kernel<float>, dim3(grid_for(h->n)), dim3(kBlock), 0,
+                           as_stream(stream), view_of<float>(h), field, in);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return fail(h, DR_ERR_HIP, std::string("set_field: ") + hipGetErrorString(e));
+    return DR_OK;
+}
+
+int dr_set_reset_uniforms(dr_handle *h, const double *u_dev) {
+    if (!h) return fail(nullptr, DR_ERR_INVALID, "dr_set_reset_uniforms: null handle");
+    if (h->cfg.rng_mode != DR_RNG_HOST_UNIFORMS)
+        return fail(h, DR_ERR_INVALID, "dr_set_reset_uniforms: handle uses DR_RNG_PHILOX");
+    h->host_u = u_dev;
+    return DR_OK;
+}
+
+int dr_random_actions(int64_t n, uint64_t seed, int64_t env_id_offset,
+                      int64_t step, float lo, float hi, float *out, void *stream) {
+    if (n < 0 || !out) return fail(nullptr, DR_ERR_INVALID, "dr_random_actions: bad arguments");
+    if (((uintptr_t)out) & 15) return fail(nullptr, DR_ERR_INVALID, "dr_random_actions: out must be 16-byte aligned");
+    if (n == 0) return DR_OK;
+    hipLaunchKernelGGL(random_actions_kernel, dim3(grid_for(n)), dim3(kBlock), 0,
+                       as_stream(stream), n, (uint32_t)seed, (uint32_t)(seed >> 32),
+                       env_id_offset, (uint64_t)step, lo, hi - lo,
+                       reinterpret_cast<float4 *>(out));
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess)
+        return fail(nullptr, DR_ERR_HIP, std::string("random_actions: ") + hipGetErrorString(e));
+    return DR_OK;
+}
+
+const char *dr_last_error(const dr_handle *h) {
+    return h ? h->err.c_str() : global_error();
+}
+
+}  // extern "C"

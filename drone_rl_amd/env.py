@@ -1,0 +1,285 @@
+"""GPU-resident batch of quadrotor envs over libdronerl.so.
+
+`DroneBatch` is the zero-copy torch path (every buffer is a device tensor,
+all work is enqueued on the current HIP stream); `DroneGymEnv` mirrors the
+reference's single-env gym class (/root/reference/drone.py:254-274) on top of
+a one-env batch.  The SB3 / gymnasium vector facades live in vec_env.py.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+import torch
+
+from . import _lib
+from ._lib import check, ptr
+
+# Physical constants of the reference (drone.py:14-43, 263); exposed as
+# attributes because callers read them (e.g. env.mass, env.g: drone.py:263,292).
+DT = 0.02
+MASS = 1.0
+G = 9.81
+INERTIA = (0.005, 0.005, 0.01)
+ARM_LENGTH = 0.5
+K_YAW = 0.01
+MAX_STEPS = 200
+MOTOR_MAX = 3 * MASS * G / 4.0          # 7.3575, action_space.high
+OBS_DIM = {"gym": 15, "vectorized": 12}
+
+_VEC_FIELDS = ("pos", "vel", "euler", "omega", "target")
+
+
+def _stream(device):
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+class DroneBatch:
+    """N independent quadrotor envs in HBM (struct of arrays).
+
+    variant    "gym" (DroneGymEnv, drone.py) or "vectorized"
+               (VectorizedDroneEnv, vectorized_drone.py)
+    dtype      torch.float64 (reference precision) or torch.float32 state
+    rng        "philox" (counter-based, seeded) or "host" (caller supplies
+               the reset uniforms: numpy-MT19937 replay for parity tests)
+    auto_reset DummyVecEnv semantics: a done env is reset inside the step
+               and obs holds the reset observation.
+    """
+
+    def __init__(self, num_envs: int, variant: str = "gym",
+                 dtype: torch.dtype = torch.float64, device=None, seed: int = 0,
+                 auto_reset: bool = True, rng: str = "philox",
+                 env_id_offset: int = 0, max_steps: int | None = None,
+                 keep_terminal_obs: bool = False, monitor: bool = False):
+        if variant not in OBS_DIM:
+            raise ValueError(f"unknown variant {variant!r}")
+        if dtype not in (torch.float64, torch.float32):
+            raise ValueError("dtype must be torch.float64 or torch.float32")
+        if rng not in ("philox", "host"):
+            raise ValueError("rng must be 'philox' or 'host'")
+        if not torch.cuda.is_available():
+            raise RuntimeError("DroneBatch needs a HIP device (no CPU fallback)")
+        self.L = _lib.lib()
+        self.device = torch.device("cuda", torch.cuda.current_device()) \
+            if device is None else torch.device(device)
+        if self.device.index is None:
+            self.device = torch.device("cuda", torch.cuda.current_device())
+        self.num_envs = int(num_envs)
+        self.variant = variant
+        self.dtype = dtype
+        self.obs_dim = OBS_DIM[variant]
+        self.auto_reset = bool(auto_reset) and variant == "gym"
+        self.monitor = monitor
+        self.seed_value = int(seed)
+        self.env_id_offset = int(env_id_offset)
+        cfg = _lib.dr_config(
+            num_envs=self.num_envs,
+            variant=_lib.DR_VARIANT_GYM if variant == "gym" else _lib.DR_VARIANT_VECTORIZED,
+            state_dtype=_lib.DR_STATE_F64 if dtype == torch.float64 else _lib.DR_STATE_F32,
+            rng_mode=_lib.DR_RNG_PHILOX if rng == "philox" else _lib.DR_RNG_HOST_UNIFORMS,
+            auto_reset=int(self.auto_reset), device=self.device.index,
+            max_steps=int(max_steps or 0), seed=self.seed_value & (2**64 - 1),
+            env_id_offset=self.env_id_offset, dt=DT)
+        h = ctypes.c_void_p()
+        check(self.L.dr_create(ctypes.byref(cfg), ctypes.byref(h)))
+        self.handle = h
+        self.max_steps = int(max_steps or (MAX_STEPS if variant == "gym" else 1000))
+        n, od, dev = self.num_envs, self.obs_dim, self.device
+        self.obs = torch.zeros(n, od, dtype=torch.float32, device=dev)
+        self.rew = torch.zeros(n, dtype=torch.float32, device=dev)
+        self.done = torch.zeros(n, dtype=torch.uint8, device=dev)
+        self.term_obs = torch.zeros(n, od, dtype=torch.float32, device=dev) \
+            if keep_terminal_obs else None
+        self.ep_ret = torch.zeros(n, dtype=torch.float32, device=dev) if monitor else None
+        self.ep_len = torch.zeros(n, dtype=torch.int32, device=dev) if monitor else None
+        self._uniforms = None
+
+    # -- lifecycle -------------------------------------------------------
+    def close(self):
+        if getattr(self, "handle", None) is not None and self.handle.value:
+            self.L.dr_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # -- core API ----------------------------------------------------------
+    def reset(self, obs_out: torch.Tensor | None = None) -> torch.Tensor:
+        out = self.obs if obs_out is None else obs_out
+        self._check_out(out, (self.num_envs, self.obs_dim), torch.float32)
+        check(self.L.dr_reset(self.handle, ptr(out), _stream(self.device)), self.handle)
+        return out
+
+    def reset_masked(self, mask: torch.Tensor, obs_out: torch.Tensor | None = None):
+        out = self.obs if obs_out is None else obs_out
+        mask = mask.to(device=self.device, dtype=torch.uint8).contiguous()
+        check(self.L.dr_reset_masked(self.handle, ptr(mask), ptr(out),
+                                     _stream(self.device)), self.handle)
+        return out
+
+    def step(self, actions: torch.Tensor, obs_out=None, rew_out=None, done_out=None):
+        """Advance every env one step.  `actions` (N,4) f32 on the device.
+        Returns (obs, rew, done) device tensors (the batch's own buffers unless
+        *_out are given: copy them before the next step if you keep them)."""
+        obs = self.obs if obs_out is None else obs_out
+        rew = self.rew if rew_out is None else rew_out
+        done = self.done if done_out is None else done_out
+        a = actions
+        if a.dtype != torch.float32 or a.device != self.device or not a.is_contiguous() \
+                or a.data_ptr() % 16:
+            a = a.to(device=self.device, dtype=torch.float32).contiguous()
+        if a.shape != (self.num_envs, 4):
+            raise ValueError(f"actions must be ({self.num_envs}, 4), got {tuple(a.shape)}")
+        self._check_out(obs, (self.num_envs, self.obs_dim), torch.float32)
+        self._check_out(rew, (self.num_envs,), torch.float32)
+        self._check_out(done, (self.num_envs,), torch.uint8)
+        s = _stream(self.device)
+        if self.monitor:
+            check(self.L.dr_step_monitored(self.handle, ptr(a), ptr(obs), ptr(rew), ptr(done),
+                                           ptr(self.term_obs), ptr(self.ep_ret),
+                                           ptr(self.ep_len), s), self.handle)
+        else:
+            check(self.L.dr_step(self.handle, ptr(a), ptr(obs), ptr(rew), ptr(done),
+                                 ptr(self.term_obs), s), self.handle)
+        return obs, rew, done
+
+    # -- state access ------------------------------------------------------
+    def get(self, field: str) -> torch.Tensor:
+        fid = _lib.FIELDS[field]
+        n = self.num_envs
+        if field in _VEC_FIELDS:
+            out = torch.empty(n, 3, dtype=torch.float64, device=self.device)
+        elif field == "eps":
+            out = torch.empty(n, dtype=torch.float64, device=self.device)
+        elif field == "ep_return":
+            out = torch.empty(n, dtype=torch.float32, device=self.device)
+        else:
+            out = torch.empty(n, dtype=torch.int32, device=self.device)
+        check(self.L.dr_get_state(self.handle, fid, ptr(out), _stream(self.device)), self.handle)
+        return out
+
+    def set(self, field: str, value) -> None:
+        fid = _lib.FIELDS[field]
+        if field in _VEC_FIELDS:
+            dt, shape = torch.float64, (self.num_envs, 3)
+        elif field == "eps":
+            dt, shape = torch.float64, (self.num_envs,)
+        elif field == "ep_return":
+            dt, shape = torch.float32, (self.num_envs,)
+        else:
+            dt, shape = torch.int32, (self.num_envs,)
+        v = torch.as_tensor(value, dtype=dt).to(self.device).reshape(shape).contiguous()
+        check(self.L.dr_set_state(self.handle, fid, ptr(v), _stream(self.device)), self.handle)
+        torch.cuda.current_stream(self.device).synchronize()   # v may be freed
+
+    def set_reset_uniforms(self, u) -> None:
+        """rng='host': (N,5) f64 uniforms consumed by the next resets."""
+        t = torch.as_tensor(u, dtype=torch.float64).to(self.device).reshape(
+            self.num_envs, 5).contiguous()
+        self._uniforms = t          # keep alive while kernels may read it
+        check(self.L.dr_set_reset_uniforms(self.handle, ptr(t)), self.handle)
+
+    @staticmethod
+    def _check_out(t, shape, dtype):
+        if t.dtype != dtype or tuple(t.shape) != shape or not t.is_contiguous():
+            raise ValueError(f"output buffer must be contiguous {dtype} {shape}")
+
+
+def random_actions(n: int, seed: int, step: int, env_id_offset: int = 0,
+                   lo: float = 0.0, hi: float = MOTOR_MAX, out=None, device=None):
+    """Synthetic random policy: (n,4) f32 i.i.d. U[lo,hi) (Philox)."""
+    dev = torch.device("cuda", torch.cuda.current_device()) if device is None else device
+    if out is None:
+        out = torch.empty(n, 4, dtype=torch.float32, device=dev)
+    check(_lib.lib().dr_random_actions(n, seed & (2**64 - 1), env_id_offset, step, lo, hi,
+                                       ptr(out), _stream(out.device)))
+    return out
+
+
+class _Box:
+    """Minimal gym.spaces.Box stand-in (gym/gymnasium are optional)."""
+
+    def __init__(self, low, high, shape, dtype=np.float32):
+        self.shape = tuple(shape)
+        self.dtype = np.dtype(dtype)
+        self.low = np.full(self.shape, low, dtype=self.dtype)
+        self.high = np.full(self.shape, high, dtype=self.dtype)
+        self._rng = np.random.default_rng()
+
+    def sample(self):
+        lo = np.where(np.isfinite(self.low), self.low, -1.0)
+        hi = np.where(np.isfinite(self.high), self.high, 1.0)
+        return self._rng.uniform(lo, hi).astype(self.dtype)
+
+    def contains(self, x):
+        x = np.asarray(x)
+        return x.shape == self.shape and bool(np.all(x >= self.low) and np.all(x <= self.high))
+
+    def seed(self, seed=None):
+        self._rng = np.random.default_rng(seed)
+        return [seed]
+
+    def __repr__(self):
+        return f"Box({self.low.min()}, {self.high.max()}, {self.shape}, {self.dtype})"
+
+
+def make_box(low, high, shape, dtype=np.float32):
+    """gymnasium.spaces.Box if importable, then gym's, else a stand-in."""
+    for mod in ("gymnasium", "gym"):
+        try:
+            spaces = __import__(mod + ".spaces", fromlist=["Box"])
+            return spaces.Box(low=low, high=high, shape=shape, dtype=dtype)
+        except Exception:
+            continue
+    return _Box(low, high, shape, dtype)
+
+
+class DroneGymEnv:
+    """Single-env drop-in for the reference's DroneGymEnv (drone.py:254-274),
+    backed by a one-env GPU batch with raw (non-auto-reset) semantics:
+    reset() -> obs (15,) f32; step(a) -> (obs, reward float, done bool, {})."""
+
+    metadata = {"render_modes": []}
+
+    def __init__(self, dt: float = DT, device=None, seed: int | None = None,
+                 dtype: torch.dtype = torch.float64):
+        if dt != DT:
+            raise ValueError("only the reference dt=0.02 is supported")
+        seed = int(np.random.randint(0, 2**31 - 1)) if seed is None else seed
+        self._b = DroneBatch(1, "gym", dtype=dtype, device=device, seed=seed,
+                             auto_reset=False)
+        self.mass, self.g, self.dt = MASS, G, DT
+        self.I = np.array(INERTIA)
+        self.arm_length, self.k_yaw, self.max_steps = ARM_LENGTH, K_YAW, MAX_STEPS
+        self.observation_space = make_box(-np.inf, np.inf, (15,), np.float32)
+        self.action_space = make_box(0, MOTOR_MAX, (4,), np.float32)
+        self._act = torch.zeros(1, 4, dtype=torch.float32, device=self._b.device)
+
+    def reset(self):
+        return self._b.reset()[0].cpu().numpy()
+
+    def step(self, action):
+        self._act.copy_(torch.as_tensor(np.asarray(action, np.float32).reshape(1, 4)))
+        obs, rew, done = self._b.step(self._act)
+        return (obs[0].cpu().numpy(), float(rew[0].item()), bool(done[0].item()), {})
+
+    def _vec(self, f):
+        return self._b.get(f)[0].cpu().numpy()
+
+    pos = property(lambda self: self._vec("pos"))
+    vel = property(lambda self: self._vec("vel"))
+    euler = property(lambda self: self._vec("euler"))
+    omega = property(lambda self: self._vec("omega"))
+    target = property(lambda self: self._vec("target"))
+    current_step = property(lambda self: int(self._b.get("current_step")[0].item()))
+    ep_num = property(lambda self: int(self._b.get("ep_num")[0].item()))
+    eps = property(lambda self: float(self._b.get("eps")[0].item()))
+
+    def render(self, mode="human", close=False):
+        raise NotImplementedError("rendering is out of scope (SURVEY.md 2 #11)")
+
+    def close(self):
+        self._b.close()

@@ -1,0 +1,131 @@
+"""torch-facing wrappers of the PPO HIP kernels in libdronerl.so.
+
+Each call enqueues work on the current HIP stream of the tensors' device and
+returns device tensors; nothing here synchronises with the host.  Semantics
+follow stable-baselines3 PPO (reference call sites
+/root/reference/train.py:36-43, 63-68).
+"""
+from __future__ import annotations
+
+import torch
+
+from . import _lib
+from ._lib import check, ptr
+
+
+def _s(t: torch.Tensor) -> int:
+    return torch.cuda.current_stream(t.device).cuda_stream
+
+
+def _f32(t):
+    assert t.dtype == torch.float32 and t.is_cuda and t.is_contiguous(), \
+        "expected a contiguous f32 device tensor"
+    return t
+
+
+def gae(rewards, values, episode_starts, last_values, last_dones, gamma=0.99,
+        gae_lambda=0.95, advantages=None, returns=None):
+    """(T,N) rewards/values/episode_starts(u8), (N,) last_values/last_dones(u8)
+    -> advantages, returns (T,N) f32 (RolloutBuffer.compute_returns_and_advantage)."""
+    T, N = rewards.shape
+    adv = torch.empty_like(rewards) if advantages is None else advantages
+    ret = torch.empty_like(rewards) if returns is None else returns
+    check(_lib.lib().dr_gae(T, N, ptr(_f32(rewards)), ptr(_f32(values)),
+                            ptr(episode_starts.contiguous()), ptr(_f32(last_values)),
+                            ptr(last_dones.contiguous()), float(gamma), float(gae_lambda),
+                            ptr(adv), ptr(ret), _s(rewards)))
+    return adv, ret
+
+
+def policy_sample(mean, log_std, seed, counter, lo, hi, actions_raw=None,
+                  actions_clipped=None, logp=None):
+    """Diagonal-Gaussian sample a = mean + exp(log_std) z, its log-prob, and
+    the clipped action passed to the env (SB3 collect_rollouts)."""
+    n = mean.shape[0]
+    check(_lib.lib().dr_policy_sample(n, ptr(_f32(mean)), ptr(_f32(log_std)),
+                                      seed & (2**64 - 1), counter & (2**64 - 1),
+                                      float(lo), float(hi), ptr(actions_raw),
+                                      ptr(actions_clipped), ptr(logp), _s(mean)))
+    return actions_raw, actions_clipped, logp
+
+
+class Permuter:
+    """Uniform random permutations of [0, n) (RolloutBuffer.get)."""
+
+    def __init__(self, n: int, device):
+        self.n = n
+        nbytes = _lib.lib().dr_permutation_workspace_bytes(n)
+        self.ws = torch.empty(max(nbytes, 1), dtype=torch.uint8, device=device)
+        self.out = torch.empty(n, dtype=torch.int32, device=device)
+
+    def __call__(self, seed: int, counter: int, out=None):
+        o = self.out if out is None else out
+        check(_lib.lib().dr_permutation(self.n, seed & (2**64 - 1), counter & (2**64 - 1),
+                                        ptr(o), ptr(self.ws), self.ws.numel(), _s(o)))
+        return o
+
+
+def gather_rows(idx, src, out=None):
+    """out[k] = src[idx[k]] for a 2-D f32 src (row width = src.shape[1])."""
+    src2 = src.reshape(src.shape[0], -1)
+    m, w = idx.shape[0], src2.shape[1]
+    o = torch.empty(m, w, dtype=torch.float32, device=src.device) if out is None else out
+    check(_lib.lib().dr_gather_rows(m, w, ptr(idx), ptr(_f32(src2)), ptr(o), _s(src)))
+    return o
+
+
+class PPOLoss:
+    """Fused PPO minibatch loss and its gradient w.r.t. the policy head
+    outputs (mean (m,4), log_std (4,), values (m,))."""
+
+    STATS = ("loss", "policy_loss", "value_loss", "entropy_loss", "clip_fraction",
+             "approx_kl", "adv_mean", "adv_std")
+
+    def __init__(self, m: int, device, clip_range=0.2, ent_coef=0.0, vf_coef=0.5,
+                 normalize_advantage=True):
+        self.m = m
+        self.clip, self.ent, self.vf = clip_range, ent_coef, vf_coef
+        self.norm = int(bool(normalize_advantage))
+        nbytes = _lib.lib().dr_ppo_loss_workspace_bytes(m)
+        self.ws = torch.empty(nbytes, dtype=torch.uint8, device=device)
+        self.grad_mean = torch.empty(m, 4, dtype=torch.float32, device=device)
+        self.grad_values = torch.empty(m, dtype=torch.float32, device=device)
+        self.grad_log_std = torch.empty(4, dtype=torch.float32, device=device)
+        self.stats = torch.empty(8, dtype=torch.float32, device=device)
+
+    def __call__(self, mean, log_std, values, actions, old_logp, advantages, returns):
+        m = mean.shape[0]
+        assert m == self.m
+        check(_lib.lib().dr_ppo_loss(
+            m, ptr(_f32(mean)), ptr(_f32(log_std)), ptr(_f32(values)), ptr(_f32(actions)),
+            ptr(_f32(old_logp)), ptr(_f32(advantages)), ptr(_f32(returns)),
+            float(self.clip), float(self.ent), float(self.vf), self.norm,
+            ptr(self.grad_mean), ptr(self.grad_values), ptr(self.grad_log_std),
+            ptr(self.stats), ptr(self.ws), self.ws.numel(), _s(mean)))
+        return self.grad_mean, self.grad_log_std, self.grad_values, self.stats
+
+
+class ClipAdam:
+    """clip_grad_norm_(max_norm) + torch.optim.Adam over one flat f32 buffer."""
+
+    def __init__(self, params: torch.Tensor, lr=3e-4, betas=(0.9, 0.999), eps=1e-5,
+                 max_grad_norm=0.5):
+        self.p = params
+        self.m = torch.zeros_like(params)
+        self.v = torch.zeros_like(params)
+        self.lr, self.b1, self.b2, self.eps = lr, betas[0], betas[1], eps
+        self.max_norm = max_grad_norm
+        self.t = 0
+        n = params.numel()
+        self.ws = torch.empty(_lib.lib().dr_adam_workspace_bytes(n), dtype=torch.uint8,
+                              device=params.device)
+        self.grad_norm = torch.zeros(1, dtype=torch.float32, device=params.device)
+
+    def step(self, grads: torch.Tensor, lr=None):
+        self.t += 1
+        check(_lib.lib().dr_clip_adam(
+            self.p.numel(), ptr(self.p), ptr(_f32(grads)), ptr(self.m), ptr(self.v),
+            float(self.lr if lr is None else lr), float(self.b1), float(self.b2),
+            float(self.eps), float(self.max_norm), self.t, ptr(self.grad_norm),
+            ptr(self.ws), self.ws.numel(), _s(self.p)))
+        return self.grad_norm

@@ -1,0 +1,242 @@
+/*
+ * dronerl.h -- C ABI of libdronerl.so, the MI355X (gfx950) batched
+ * quadrotor environment and PPO kernels.
+ *
+ * Boundary.  The reference's env boundary is the gym.Env pair
+ *   DroneGymEnv.reset() -> obs(15,) f32               /root/reference/drone.py:270-271 (-> 48-75)
+ *   DroneGymEnv.step(a(4,) f32) -> (obs, r, done, {})  /root/reference/drone.py:266-268 (-> 81-159)
+ * consumed through SB3 DummyVecEnv + VecMonitor (train.py:33-35), and the
+ * batched variant VectorizedDroneEnv.reset/step (vectorized_drone.py:38-57,
+ * 135-216).  This library replaces that whole layer (L0 physics + L1 env API
+ * + L2 vectorisation) with one GPU-resident batch of N envs.
+ *
+ * Conventions
+ *  - Every data pointer passed to a compute entry point is DEVICE memory
+ *    (e.g. a torch tensor's data_ptr on the handle's device).  The caller owns
+ *    all I/O buffers; the library owns the persistent env state (SoA).
+ *  - `stream` is a hipStream_t passed as void* (NULL = the null stream).
+ *    Compute entry points only enqueue work: they are asynchronous with
+ *    respect to the host and safe to capture into a hipGraph.
+ *  - Return value: DR_OK (0) or a negative DR_ERR_* code.  A message for the
+ *    last error on a handle is available from dr_last_error(handle);
+ *    dr_last_error(NULL) reports errors that happened without a handle
+ *    (dr_create).  No C++ exception crosses this ABI.
+ *  - A handle is not thread-safe; use one handle per host thread.
+ *  - Layouts: actions (N,4) f32 row-major; obs (N,15) f32 row-major for the
+ *    "gym" variant, (N,12) for "vectorized"; rewards (N,) f32; dones (N,) u8.
+ */
+#ifndef DRONERL_H_
+#define DRONERL_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define DR_ABI_VERSION 1
+
+enum dr_status {
+    DR_OK = 0,
+    DR_ERR_INVALID = -1,   /* bad argument / shape / null handle          */
+    DR_ERR_HIP = -2,       /* a HIP runtime call or kernel launch failed  */
+    DR_ERR_NOMEM = -3,     /* device allocation failed                    */
+    DR_ERR_UNSUPPORTED = -4
+};
+
+enum dr_variant {
+    DR_VARIANT_GYM = 0,        /* DroneGymEnv, drone.py:13-274             */
+    DR_VARIANT_VECTORIZED = 1  /* VectorizedDroneEnv, vectorized_drone.py  */
+};
+
+enum dr_state_dtype {
+    DR_STATE_F64 = 0,  /* reference precision (numpy float64 state)       */
+    DR_STATE_F32 = 1   /* fp32 state: half the state bytes, unit-floor parity */
+};
+
+enum dr_rng_mode {
+    /* reset uniforms from counter-based Philox4x32-10 keyed by
+       (seed, global env id, episode number): reproducible, order-free   */
+    DR_RNG_PHILOX = 0,
+    /* reset uniforms read from a caller-provided device buffer (N,5) f64,
+       row i = the 5 draws env i's next reset consumes, in the reference's
+       draw order (pos x, pos y, target x, y, z; drone.py:57,73).  This is
+       how parity runs replay numpy's MT19937 stream.                     */
+    DR_RNG_HOST_UNIFORMS = 1
+};
+
+enum dr_field {   /* dr_get_state / dr_set_state, all device buffers      */
+    DR_FIELD_POS = 0,       /* (N,3) f64                                     */
+    DR_FIELD_VEL = 1,       /* (N,3) f64                                     */
+    DR_FIELD_EULER = 2,     /* (N,3) f64  roll, pitch, yaw (never wrapped)   */
+    DR_FIELD_OMEGA = 3,     /* (N,3) f64                                     */
+    DR_FIELD_TARGET = 4,    /* (N,3) f64                                     */
+    DR_FIELD_STEP = 5,      /* (N,)  i32  current_step (drone.py:28,155)     */
+    DR_FIELD_EP_NUM = 6,    /* (N,)  i32  ep_num (drone.py:18,61)            */
+    DR_FIELD_EPS = 7,       /* (N,)  f64  curriculum eps (drone.py:33,70)    */
+    DR_FIELD_EP_RETURN = 8, /* (N,)  f32  running episode return (monitor)   */
+    DR_FIELD_EP_LENGTH = 9  /* (N,)  i32  running episode length (monitor)   */
+};
+
+typedef struct dr_config {
+    int64_t num_envs;       /* N >= 1                                        */
+    int32_t variant;        /* enum dr_variant                               */
+    int32_t state_dtype;    /* enum dr_state_dtype                           */
+    int32_t rng_mode;       /* enum dr_rng_mode                              */
+    int32_t auto_reset;     /* 1: DummyVecEnv semantics (reset a done env in
+                               the same step, obs_out = reset obs); 0: raw
+                               env semantics (caller resets).  Ignored (0)
+                               for the vectorized variant, which never
+                               auto-resets (vectorized_drone.py:211-213).    */
+    int32_t device;         /* HIP device ordinal                            */
+    int32_t max_steps;      /* 0 = variant default (200 gym, 1000 vectorized) */
+    uint64_t seed;          /* Philox key                                    */
+    int64_t env_id_offset;  /* global id of env 0 (rank * N for DP shards)   */
+    double dt;              /* 0 = reference default 0.02 (drone.py:14)      */
+} dr_config;
+
+typedef struct dr_handle dr_handle;
+
+/* Library ABI version (DR_ABI_VERSION of the build). */
+int dr_abi_version(void);
+
+/* Create N envs on cfg->device.  Mirrors the reference constructor: every
+   env performs one reset (drone.py:46), so ep_num starts at 1.  In
+   DR_RNG_HOST_UNIFORMS mode no uniform buffer exists yet, so that first
+   reset uses u = 0.5 for all five draws (pos (0,0,1); the target is
+   (0,0,1) anyway while eps = 0).  Replaces DroneGymEnv.__init__
+   (drone.py:255-264) and VectorizedDroneEnv.__init__ (vectorized_drone.py:13-36).
+   Synchronous: returns after the state is initialised. */
+int dr_create(const dr_config *cfg, dr_handle **out);
+int dr_destroy(dr_handle *h);
+
+int64_t dr_num_envs(const dr_handle *h);
+int dr_obs_dim(const dr_handle *h);   /* 15 gym, 12 vectorized */
+
+/* Reset every env and write (N,obs_dim) obs.  Replaces DroneEnv.reset
+   (drone.py:48-75) called on each env by VecEnv.reset, and
+   VectorizedDroneEnv.reset (vectorized_drone.py:38-57). */
+int dr_reset(dr_handle *h, float *obs_out, void *stream);
+
+/* Reset only envs with mask[i] != 0 ((N,) u8); obs_out rows of other envs are
+   rewritten with their current obs.  (DummyVecEnv-free callers, test
+   harnesses.)  Not available for the vectorized variant. */
+int dr_reset_masked(dr_handle *h, const uint8_t *mask, float *obs_out,
+                    void *stream);
+
+/* One env step for all N envs.  Replaces DroneEnv.step (drone.py:81-159)
+   looped by DummyVecEnv.step_wait, and VectorizedDroneEnv.step
+   (vectorized_drone.py:135-216).
+     actions        (N,4) f32, NOT clipped (the reference env does not clip)
+     obs_out        (N,obs_dim) f32; with auto_reset, rows of done envs hold
+                    the reset observation (DummyVecEnv semantics)
+     rew_out        (N,) f32 (SB3 buffers rewards as f32)
+     done_out       (N,) u8
+     terminal_obs_out  nullable (N,obs_dim) f32: for done envs the obs
+                    BEFORE the auto-reset ("terminal_observation"); rows of
+                    envs that are not done are left untouched.            */
+int dr_step(dr_handle *h, const float *actions, float *obs_out,
+            float *rew_out, uint8_t *done_out, float *terminal_obs_out,
+            void *stream);
+
+/* dr_step plus VecMonitor bookkeeping (running f32 return, i32 length per
+   env): for done envs the finished episode's return/length are written to
+   ep_return_out / ep_length_out ((N,) each; other rows untouched) and the
+   running counters restart.  SB3 VecMonitor.step_wait equivalent. */
+int dr_step_monitored(dr_handle *h, const float *actions, float *obs_out,
+                      float *rew_out, uint8_t *done_out,
+                      float *terminal_obs_out, float *ep_return_out,
+                      int32_t *ep_length_out, void *stream);
+
+/* Device-side state access (parity injection, checkpointing, get_attr). */
+int dr_get_state(dr_handle *h, int field, void *out, void *stream);
+int dr_set_state(dr_handle *h, int field, const void *in, void *stream);
+
+/* DR_RNG_HOST_UNIFORMS: device pointer to (N,5) f64 read by every later
+   reset until replaced.  The buffer must stay alive while work using it is
+   in flight. */
+int dr_set_reset_uniforms(dr_handle *h, const double *u_dev);
+
+/* Synthetic random policy: out (n,4) f32 i.i.d. U[lo,hi) from Philox keyed
+   by seed with counter (env_id_offset + i, step).  Not part of the
+   reference; it generates the benchmark's action stream. */
+int dr_random_actions(int64_t n, uint64_t seed, int64_t env_id_offset,
+                      int64_t step, float lo, float hi, float *out,
+                      void *stream);
+
+const char *dr_last_error(const dr_handle *h);
+
+/* ---------------------------------------------------------------------------
+ * PPO kernels (stable-baselines3 PPO arithmetic; the
+ * reference calls it at train.py:36-43, 63-68).  All buffers are device
+ * memory; layouts are time-major (T,N) so a fixed step is contiguous.
+ * ------------------------------------------------------------------------- */
+
+/* GAE reverse scan, RolloutBuffer.compute_returns_and_advantage:
+   delta_t = r_t + g*V_{t+1}*(1-start_{t+1}) - V_t,
+   A_t = delta_t + g*l*(1-start_{t+1})*A_{t+1}; the last step uses
+   (1-last_dones) and last_values; R = A + V.  All arithmetic is f32 with
+   numpy's NEP-50 rounding: gamma -> f32, gamma*lambda formed in f64 then
+   rounded to f32 (SB3 multiplies two python floats first). */
+int dr_gae(int64_t T, int64_t N, const float *rewards, const float *values,
+           const uint8_t *episode_starts, const float *last_values,
+           const uint8_t *last_dones, double gamma, double gae_lambda,
+           float *advantages, float *returns, void *stream);
+
+/* Diagonal-Gaussian action sampling for the rollout:
+   a = mean + exp(log_std) * z, z ~ N(0,1) (Philox + Box-Muller keyed by
+   (seed, counter, row)); logp = sum_j log N(a_j; mean_j, std_j);
+   actions_clipped = clip(a, lo, hi) (what SB3 passes to env.step).
+   actions_raw / logp / actions_clipped may each be NULL. */
+int dr_policy_sample(int64_t n, const float *mean, const float *log_std,
+                     uint64_t seed, uint64_t counter, float lo, float hi,
+                     float *actions_raw, float *actions_clipped, float *logp,
+                     void *stream);
+
+/* Uniform random permutation of [0,n) (RolloutBuffer.get's
+   np.random.permutation): sort-by-random-key with a hipCUB radix sort.
+   dr_permutation_workspace_bytes gives the scratch size for n. */
+size_t dr_permutation_workspace_bytes(int64_t n);
+int dr_permutation(int64_t n, uint64_t seed, uint64_t counter, int32_t *out,
+                   void *workspace, size_t workspace_bytes, void *stream);
+
+/* Gather a minibatch: dst[k,:] = src[idx[k],:] for row width `width`
+   (floats), k < m.  Used to form minibatches from the flat rollout. */
+int dr_gather_rows(int64_t m, int64_t width, const int32_t *idx,
+                   const float *src, float *dst, void *stream);
+
+/* Fused PPO loss + gradient of the loss w.r.t. the policy head outputs
+   (PPO.train: normalised advantage, ratio/clip surrogate, value MSE,
+   entropy).  Inputs for a minibatch of m rows:
+     mean (m,4), log_std (4), values (m), actions (m,4), old_logp (m),
+     advantages (m), returns (m).
+   Outputs:
+     grad_mean (m,4), grad_values (m), grad_log_std (4): dLoss/d(.)
+     stats (8) f32: [loss, policy_loss, value_loss, entropy_loss,
+                     clip_fraction, approx_kl, adv_mean, adv_std]
+   `workspace` >= dr_ppo_loss_workspace_bytes(m). */
+size_t dr_ppo_loss_workspace_bytes(int64_t m);
+int dr_ppo_loss(int64_t m, const float *mean, const float *log_std,
+                const float *values, const float *actions,
+                const float *old_logp, const float *advantages,
+                const float *returns, float clip_range, float ent_coef,
+                float vf_coef, int normalize_advantage, float *grad_mean,
+                float *grad_values, float *grad_log_std, float *stats,
+                void *workspace, size_t workspace_bytes, void *stream);
+
+/* clip_grad_norm_(max_norm) + Adam step over one flat fp32 parameter
+   buffer (torch.optim.Adam semantics, bias-corrected, eps outside sqrt).
+   `step` is the 1-based Adam step count.  grad_norm_out (1) f32 nullable.
+   `workspace` >= dr_adam_workspace_bytes(n). */
+size_t dr_adam_workspace_bytes(int64_t n);
+int dr_clip_adam(int64_t n, float *params, float *grads, float *exp_avg,
+                 float *exp_avg_sq, float lr, float beta1, float beta2,
+                 float eps, float max_grad_norm, int64_t step,
+                 float *grad_norm_out, void *workspace,
+                 size_t workspace_bytes, void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* DRONERL_H_ */
