@@ -182,13 +182,21 @@ def main():
         out["cpu_baseline"] = cpu
     if args.extra and world == 1:
         ex = {}
-        for dn, n in (("f32", N), ("f64", 1 << 22), ("f32", 1 << 22)):
-            k = 200 if n > N else args.steps
-            el, gm, _ = time_env(args, dn, n, 0, 1, device, k, 20)
-            pl = gm / 1e3 / k
-            ex[f"{dn}_{n}"] = {"env_steps_per_s": round(n * k / el, 1),
-                              "avg_launch_us": round(pl * 1e6, 3),
-                              "achieved_GBs": round(n * BYTES_PER_ENV_STEP[dn] / pl / 1e9, 1)}
+        saved = os.environ.get("DRONERL_STEP_KERNEL")
+        for kern in ("quad", "lane"):
+            os.environ["DRONERL_STEP_KERNEL"] = kern
+            for dn, n in (("f64", N), ("f32", N), ("f64", 1 << 22), ("f32", 1 << 22)):
+                k = 200 if n > N else args.steps
+                el, gm, _ = time_env(args, dn, n, 0, 1, device, k, 20)
+                pl = gm / 1e3 / k
+                ex[f"{kern}_{dn}_{n}"] = {
+                    "env_steps_per_s": round(n * k / el, 1),
+                    "avg_launch_us": round(pl * 1e6, 3),
+                    "achieved_GBs": round(n * BYTES_PER_ENV_STEP[dn] / pl / 1e9, 1)}
+        if saved is None:
+            os.environ.pop("DRONERL_STEP_KERNEL", None)
+        else:
+            os.environ["DRONERL_STEP_KERNEL"] = saved
         out["extra"] = ex
     if rank == 0:
         print(json.dumps(out), flush=True)

@@ -81,8 +81,8 @@ SIGNATURES = {
                             c_float, c_float, c_int, _P, _P, _P, _P, _P,
                             c_size_t, _P]),
     "dr_adam_workspace_bytes": (c_size_t, [c_int64]),
-    "dr_clip_adam": (c_int, [c_int64, _P, _P, _P, _P, c_float, c_float, c_float,
-                             c_float, c_float, c_int64, _P, _P, c_size_t, _P]),
+    "dr_clip_adam": (c_int, [c_int64, _P, _P, _P, _P, c_double, c_double, c_double,
+                             c_double, c_float, c_int64, _P, _P, c_size_t, _P]),
 }
 
 _lib = None

@@ -19,6 +19,7 @@
 // that numpy would round twice.  The state scalar S is double (reference
 // precision) or float (throughput mode).
 
+#include <cstdlib>
 #include <cstring>
 #include <new>
 #include <string>
@@ -39,12 +40,8 @@ constexpr double kFactor = kArm / 1.4142135623730951;  // L / np.sqrt(2)
 constexpr float kKyaw32 = 0.01f;  // python float * np.float32 -> f32 (NEP 50)
 constexpr double kDt = 0.02;
 
-__device__ inline double m_sin(double x) { return sin(x); }
-__device__ inline float m_sin(float x) { return sinf(x); }
-__device__ inline double m_cos(double x) { return cos(x); }
-__device__ inline float m_cos(float x) { return cosf(x); }
-__device__ inline double m_tan(double x) { return tan(x); }
-__device__ inline float m_tan(float x) { return tanf(x); }
+__device__ inline void m_sincos(double x, double *s, double *c) { sincos(x, s, c); }
+__device__ inline void m_sincos(float x, float *s, float *c) { sincosf(x, s, c); }
 __device__ inline double m_sqrt(double x) { return sqrt(x); }
 __device__ inline float m_sqrt(float x) { return sqrtf(x); }
 
@@ -170,10 +167,13 @@ __device__ inline S physics_step(S st[F_N], float4 act, S dt, bool &crash) {
     const S tau_theta = (S)kFactor * (S)(((-a0 + a1) + a2) - a3);
     const float tau_psi = kKyaw32 * (((a0 - a1) + a2) - a3);
 
-    const S phi = st[F_EUL + 0], theta = st[F_EUL + 1], psi = st[F_EUL + 2];
-    const S cph = m_cos(phi), sph = m_sin(phi);
-    const S cth = m_cos(theta), sth = m_sin(theta);
-    const S cps = m_cos(psi), sps = m_sin(psi);
+    // One sincos per angle: a shared range reduction yields exactly the
+    // separate sin() and cos() results at half the instructions.
+    const S theta = st[F_EUL + 1];
+    S sph, cph, sth, cth, sps, cps;
+    m_sincos(st[F_EUL + 0], &sph, &cph);
+    m_sincos(theta, &sth, &cth);
+    m_sincos(st[F_EUL + 2], &sps, &cps);
     // R(old euler) column 2 (drone.py:169-173): thrust is body-z only.
     const S r02 = cps * sth * cph + sps * sph;
     const S r12 = sps * sth * cph - cps * sph;
@@ -190,7 +190,9 @@ __device__ inline S physics_step(S st[F_N], float4 act, S dt, bool &crash) {
 
     // Euler-angle rates from the OLD omega (131-132, 176-186).
     const S w0 = st[F_OMG + 0], w1 = st[F_OMG + 1], w2 = st[F_OMG + 2];
-    const S tth = m_tan(theta);
+    // tan(theta) from the shared sincos (np.tan rounds once; this rounds the
+    // quotient once more: <= 2 ulp apart, far inside the parity bar).
+    const S tth = sth / cth;
     S ed2;
     if constexpr (VAR == DR_VARIANT_GYM) {
         ed2 = ((S)0 * w0 + (sph / cth) * w1) + (cph / cth) * w2;      // (184)
@@ -325,6 +327,235 @@ __global__ __launch_bounds__(kBlock) void env_step_kernel(EnvView<S> v,
     store_obs_block<OD>(reinterpret_cast<float *>(sh4), ob, io.obs, base, v.n);
 }
 
+// ----------------------------------------------------------------------------
+// Quad kernel: 4 lanes per env (one DPP quad), lane k < 3 owns component k of
+// pos / vel / euler / omega / target.  Every lane runs the SAME instruction
+// stream on its own component (SIMD-uniform: selects, never lane-divergent
+// branches), so one env's serial f64 chain -- three sincos range reductions,
+// the divides -- is split three ways and a launch of N envs has 4N lanes of
+// latency-hiding parallelism.  Lane 3 mirrors lane 2's data and its results
+// are discarded.  Values cross lanes with DPP quad_perm broadcasts.
+//
+// Exactness: each component is computed with the reference's own operation
+// order (the selects only pick operands; (-x) and 0*x+y forms are exact), so
+// the quad kernel and the one-lane kernel agree except tan(theta), formed
+// here as sin/cos from the shared sincos (<= 2 ulp from np.tan).
+// ----------------------------------------------------------------------------
+template <int J>
+__device__ inline uint32_t qb(uint32_t x) {
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, J * 0x55, 0xF, 0xF, false);
+}
+template <int J>
+__device__ inline float qb(float x) {
+    return __int_as_float((int)qb<J>((uint32_t)__float_as_int(x)));
+}
+template <int J>
+__device__ inline double qb(double x) {
+    const uint32_t lo = qb<J>((uint32_t)__double2loint(x));
+    const uint32_t hi = qb<J>((uint32_t)__double2hiint(x));
+    return __hiloint2double((int)hi, (int)lo);
+}
+
+template <typename T>
+__device__ inline T sel3(int k, T a0, T a1, T a2) {
+    return k == 0 ? a0 : (k == 1 ? a1 : a2);
+}
+
+template <typename S, int VAR, bool MON>
+__global__ __launch_bounds__(kBlock) void env_step_quad_kernel(EnvView<S> v,
+                                                               StepIO io) {
+    constexpr int OD = (VAR == DR_VARIANT_GYM) ? 15 : 12;
+    constexpr int EPB = kBlock / 4;                    // envs per block
+    __shared__ float4 sh4[EPB * OD / 4];
+    float *sh = reinterpret_cast<float *>(sh4);
+    const int q = threadIdx.x & 3;                     // lane in the quad
+    const int k = q < 3 ? q : 2;                       // component owned
+    const int el = threadIdx.x >> 2;                   // env within block
+    const int64_t base = (int64_t)blockIdx.x * EPB;
+    const int64_t e = base + el;
+    const bool live = e < v.n;
+    float ob[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
+    if (live) {
+        // ---- loads: component k of each 3-vector, the action row, counter
+        S p = v.field(F_POS + k)[e];
+        S vel = v.field(F_VEL + k)[e];
+        S ang = v.field(F_EUL + (q < 3 ? q : 1))[e];   // lane 3: theta again
+        S w = v.field(F_OMG + k)[e];
+        S tg;
+        if constexpr (VAR == DR_VARIANT_GYM) {
+            tg = v.field(F_TGT + k)[e];
+        } else {
+            tg = k == 2 ? (S)10.0 : (S)0;
+        }
+        const float4 act = reinterpret_cast<const float4 *>(io.actions)[e];
+        int32_t step = v.step[e];
+
+        // ---- thrust / torque component k (drone.py:106, 113-117)
+        const float a0 = act.x, a1 = act.y, a2 = act.z, a3 = act.w;
+        const float thr = ((a0 + a1) + a2) + a3;
+        const float x0 = k == 1 ? -a0 : a0;
+        const float x1 = k == 2 ? -a1 : a1;
+        const float x2 = k == 0 ? -a2 : a2;
+        const float tsum = ((x0 + x1) + x2) + (-a3);
+        const S tau = k == 2 ? (S)(kKyaw32 * tsum) : (S)kFactor * (S)tsum;
+
+        // ---- one sincos per lane, then share (phi, theta, psi)
+        S sn, cs;
+        m_sincos(ang, &sn, &cs);
+        const S sph = qb<0>(sn), cph = qb<0>(cs);
+        const S sth = qb<1>(sn), cth = qb<1>(cs);
+        const S sps = qb<2>(sn), cps = qb<2>(cs);
+        const S w0 = qb<0>(w), w1 = qb<1>(w), w2 = qb<2>(w);
+
+        // ---- linear: R(old euler) row k, column 2 (drone.py:120-128)
+        const S A = (k == 0 ? cps : sps) * sth;
+        const S t1 = A * cph;
+        const S Bp = (k == 0 ? sps : cps) * sph;
+        const S r = k == 0 ? t1 + Bp : (k == 1 ? t1 - Bp : cth * cph);
+        const S T = (S)thr;
+        const S acc = (k == 2 ? (S)(-kG) : (S)0) + (r * T) / (S)kMass;
+        vel += acc * v.dt;
+        p += vel * v.dt;
+
+        // ---- Euler-angle rates, row k of W(old phi, theta) (131-132, 176-186)
+        S c1, c2;
+        const S tth = sth / cth;
+        if constexpr (VAR == DR_VARIANT_GYM) {
+            c1 = sel3(k, sph * tth, cph, sph / cth);
+            c2 = sel3(k, cph * tth, -sph, cph / cth);
+        } else {
+            const S sec = (S)1 / cth;                      // vd:116
+            c1 = sel3(k, sph * tth, cph, sph * sec);
+            c2 = sel3(k, cph * tth, -sph, cph * sec);
+        }
+        const S c0 = k == 0 ? (S)1 : (S)0;
+        const S ed = (c0 * w0 + c1 * w1) + c2 * w2;
+        const S ang_new = ang + ed * v.dt;                 // lane 3's is unused
+
+        // ---- angular: omega component k from the old omega (135-139)
+        const S dI = (S)sel3(k, kIyy - kIzz, kIzz - kIxx, kIxx - kIyy);
+        const S Ik = (S)sel3(k, kIxx, kIyy, kIzz);
+        const S wa = k == 0 ? w1 : w0;
+        const S wb = k == 2 ? w1 : w2;
+        const S wd = (tau - dI * wa * wb) / Ik;
+        w += wd * v.dt;
+
+        // ---- reward / termination on the new position (142-157)
+        const S dx = p - tg;
+        const S dsq = dx * dx, psq = p * p;
+        const S d = m_sqrt((qb<0>(dsq) + qb<1>(dsq)) + qb<2>(dsq));
+        const S pn = m_sqrt((qb<0>(psq) + qb<1>(psq)) + qb<2>(psq));
+        const S pz = qb<2>(p);
+        S rw;
+        if constexpr (VAR == DR_VARIANT_GYM) {
+            rw = (S)0.01 * -d;
+            if (d < (S)0.05) rw += (S)1;
+        } else {
+            rw = (S)(-0.01) * d;
+            if (d < (S)1) rw += (S)1;
+        }
+        step += 1;
+        const bool done = (pz < (S)0) || (pn > (S)50) || (step >= v.max_steps);
+        const float rf = (float)rw;
+        ob[0] = (float)p;
+        ob[1] = (float)vel;
+        ob[2] = (float)ang_new;
+        ob[3] = (float)w;
+        ob[4] = (float)(tg - p);
+
+        float ret = 0.f;
+        int32_t len = 0;
+        if constexpr (MON) {
+            ret = v.ep_ret[e] + rf;
+            len = v.ep_len[e] + 1;
+        }
+        S ang_out = ang_new;
+        if constexpr (VAR == DR_VARIANT_GYM) {
+            if (done && io.auto_reset) {          // quad-uniform branch
+                if (io.term_obs && q < 3) {
+                    float *to = io.term_obs + e * OD;
+#pragma unroll
+                    for (int j = 0; j < 5; ++j) to[j * 3 + k] = ob[j];
+                }
+                // DroneEnv.reset (drone.py:48-75): lane k draws Philox block k
+                const int32_t ep_new = v.ep_num[e] + 1;
+                double u0, u1, u2, u3, u4;
+                if (v.host_u) {
+                    const double *hu = v.host_u + e * 5;
+                    u0 = hu[0]; u1 = hu[1]; u2 = hu[2]; u3 = hu[3]; u4 = hu[4];
+                } else {
+                    const uint64_t gid = (uint64_t)(v.env_id_offset + e);
+                    const u32x4 rr = philox4x32_10(
+                        u32x4{(uint32_t)ep_new, (uint32_t)gid, (uint32_t)(gid >> 32),
+                              TAG_RESET | (uint32_t)k},
+                        v.seed_lo, v.seed_hi);
+                    u0 = u01_f64(qb<0>(rr.x), qb<0>(rr.y));
+                    u1 = u01_f64(qb<0>(rr.z), qb<0>(rr.w));
+                    u2 = u01_f64(qb<1>(rr.x), qb<1>(rr.y));
+                    u3 = u01_f64(qb<1>(rr.z), qb<1>(rr.w));
+                    u4 = u01_f64(qb<2>(rr.x), qb<2>(rr.y));
+                }
+                double eps = v.eps[e];
+                const bool bump = (ep_new % 2000) == 0;
+                if (bump) eps += 0.1;
+                if (q == 0) {
+                    v.ep_num[e] = ep_new;
+                    if (bump) v.eps[e] = eps;
+                }
+                p = (S)sel3(k, u0 - 0.5, u1 - 0.5, 1.0);
+                tg = (S)sel3(k, eps * u2, eps * u3, eps * u4 + 1.0 + 0.0);
+                vel = (S)0;
+                ang_out = (S)0;
+                w = (S)0;
+                step = 0;
+                if (q < 3) v.field(F_TGT + k)[e] = tg;
+                ob[0] = (float)p;
+                ob[1] = 0.f;
+                ob[2] = 0.f;
+                ob[3] = 0.f;
+                ob[4] = (float)(tg - p);
+            }
+        }
+        if (q < 3) {
+            v.field(F_POS + k)[e] = p;
+            v.field(F_VEL + k)[e] = vel;
+            v.field(F_EUL + k)[e] = ang_out;
+            v.field(F_OMG + k)[e] = w;
+        }
+        if (q == 0) {
+            v.step[e] = step;
+            io.rew[e] = rf;
+            io.done[e] = (uint8_t)done;
+            if constexpr (MON) {
+                if (done) {
+                    io.ep_ret_out[e] = ret;
+                    io.ep_len_out[e] = len;
+                    ret = 0.f;
+                    len = 0;
+                }
+                v.ep_ret[e] = ret;
+                v.ep_len[e] = len;
+            }
+        }
+    }
+    // ---- obs rows through LDS, out as contiguous float4 (64 envs/block)
+    if (q < 3) {
+        constexpr int NJ = OD / 3;
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) sh[el * OD + j * 3 + k] = ob[j];
+    }
+    __syncthreads();
+    const int64_t nvalid = (v.n - base) < EPB ? (v.n - base) : EPB;
+    float *dst = io.obs + base * OD;
+    if (nvalid == EPB && (((uintptr_t)dst) & 15) == 0) {
+        float4 *d4 = reinterpret_cast<float4 *>(dst);
+        for (int t = threadIdx.x; t < EPB * OD / 4; t += kBlock) d4[t] = sh4[t];
+    } else {
+        const int total = (int)nvalid * OD;
+        for (int t = threadIdx.x; t < total; t += kBlock) dst[t] = sh[t];
+    }
+}
+
 // Reset (all envs, or those with mask[i] != 0) and write every env's obs.
 // mode: 0 Philox, 1 host uniforms, 2 constant 0.5.  `init` additionally
 // clears ep_num / eps / monitor counters first (constructor).
@@ -437,6 +668,7 @@ struct dr_handle {
     int64_t n = 0;
     int64_t stride = 0;
     int obs_dim = 15;
+    bool quad = false;  // true: 4 lanes per env (env_step_quad_kernel)
     void *mem = nullptr;
     const double *host_u = nullptr;
     std::string err;
@@ -517,8 +749,12 @@ int dispatch_reset(dr_handle *h, const uint8_t *mask, float *obs, int mode,
 template <typename S, int VAR, bool MON>
 int launch_step(dr_handle *h, const StepIO &io, hipStream_t st) {
     EnvView<S> v = view_of<S>(h);
-    hipLaunchKernelGGL((env_step_kernel<S, VAR, MON>), dim3(grid_for(h->n)),
-                       dim3(kBlock), 0, st, v, io);
+    if (h->quad)
+        hipLaunchKernelGGL((env_step_quad_kernel<S, VAR, MON>),
+                           dim3(grid_for(h->n, kBlock / 4)), dim3(kBlock), 0, st, v, io);
+    else
+        hipLaunchKernelGGL((env_step_kernel<S, VAR, MON>), dim3(grid_for(h->n)),
+                           dim3(kBlock), 0, st, v, io);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess)
         return fail(h, DR_ERR_HIP, std::string("env_step_kernel: ") + hipGetErrorString(e));
@@ -579,6 +815,11 @@ int dr_create(const dr_config *cfg_in, dr_handle **out) {
     h->n = cfg.num_envs;
     h->stride = (cfg.num_envs + 63) / 64 * 64;
     h->obs_dim = cfg.variant == DR_VARIANT_GYM ? 15 : 12;
+    // Step kernel choice: one lane per env unless DRONERL_STEP_KERNEL=quad
+    // (4 lanes per env; fewer serial f64 ops per lane, more total VALU work:
+    // slower on MI355X at every measured size, kept for A/B measurement).
+    if (const char *kk = std::getenv("DRONERL_STEP_KERNEL"))
+        h->quad = std::strcmp(kk, "quad") == 0;
 
     DeviceGuard g(cfg.device);
     const size_t bytes = state_bytes(h->stride, cfg.state_dtype);

@@ -375,7 +375,7 @@ __global__ __launch_bounds__(kBlock) void clip_adam_kernel(
         g[i] = gi;
         float mi = m[i];
         mi = mi + w1 * (gi - mi);                    // exp_avg.lerp_(g, 1-b1)
-        float vi = v[i] * beta2 + one_m_b2 * (gi * gi);
+        float vi = v[i] * beta2 + (one_m_b2 * gi) * gi;  // addcmul_: value*t1*t2
         m[i] = mi;
         v[i] = vi;
         const float denom = sqrtf(vi) / bc2_sqrt + eps;
@@ -521,7 +521,7 @@ size_t dr_adam_workspace_bytes(int64_t n) {
 }
 
 int dr_clip_adam(int64_t n, float *params, float *grads, float *exp_avg, float *exp_avg_sq,
-                 float lr, float beta1, float beta2, float eps, float max_grad_norm,
+                 double lr, double beta1, double beta2, double eps, float max_grad_norm,
                  int64_t step, float *grad_norm_out, void *workspace, size_t workspace_bytes,
                  void *stream) {
     if (n < 1 || !params || !grads || !exp_avg || !exp_avg_sq || step < 1)
@@ -538,11 +538,12 @@ int dr_clip_adam(int64_t n, float *params, float *grads, float *exp_avg, float *
     const double b1 = beta1, b2 = beta2;
     const double bc1 = 1.0 - std::pow(b1, (double)step);
     const double bc2 = 1.0 - std::pow(b2, (double)step);
-    const float step_size = (float)((double)lr / bc1);
+    const float step_size = (float)(lr / bc1);
     const float bc2_sqrt = (float)std::sqrt(bc2);
     hipLaunchKernelGGL(clip_adam_kernel, dim3(nb), dim3(kBlock), 0, st, n, params, grads,
                        exp_avg, exp_avg_sq, part, nb, max_grad_norm, (float)(1.0 - b1),
-                       beta2, (float)(1.0 - b2), step_size, bc2_sqrt, eps, grad_norm_out);
+                       (float)b2, (float)(1.0 - b2), step_size, bc2_sqrt, (float)eps,
+                       grad_norm_out);
     return check_launch("dr_clip_adam");
 }
 

@@ -228,11 +228,13 @@ int dr_ppo_loss(int64_t m, const float *mean, const float *log_std,
 /* clip_grad_norm_(max_norm) + Adam step over one flat fp32 parameter
    buffer (torch.optim.Adam semantics, bias-corrected, eps outside sqrt).
    `step` is the 1-based Adam step count.  grad_norm_out (1) f32 nullable.
+   lr / betas / eps are doubles because torch forms 1-beta, lr/bias_correction
+   from Python floats before rounding them to f32 scalars.
    `workspace` >= dr_adam_workspace_bytes(n). */
 size_t dr_adam_workspace_bytes(int64_t n);
 int dr_clip_adam(int64_t n, float *params, float *grads, float *exp_avg,
-                 float *exp_avg_sq, float lr, float beta1, float beta2,
-                 float eps, float max_grad_norm, int64_t step,
+                 float *exp_avg_sq, double lr, double beta1, double beta2,
+                 double eps, float max_grad_norm, int64_t step,
                  float *grad_norm_out, void *workspace,
                  size_t workspace_bytes, void *stream);
 

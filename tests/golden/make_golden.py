@@ -258,8 +258,15 @@ def gen_gym_traj(drone, rng, n_envs=16, n_steps=256):
         rew = np.zeros((n_steps, n_envs))
         done = np.zeros((n_steps, n_envs), bool)
         ru = np.full((n_steps, n_envs, 5), np.nan)
+        # full f64 pre-step state, so a replay can re-synchronise every step
+        pre = {k: np.zeros((n_steps, n_envs, 3)) for k in
+               ["pos", "vel", "euler", "omega", "target"]}
+        pre_step = np.zeros((n_steps, n_envs), np.int32)
         for t in range(n_steps):
             for i, e in enumerate(envs):
+                for k in pre:
+                    pre[k][t, i] = getattr(e, k)
+                pre_step[t, i] = e.current_step
                 o, r, d, _ = e.step(acts[t, i])
                 rew[t, i], done[t, i] = r, d
                 if d:
@@ -273,7 +280,8 @@ def gen_gym_traj(drone, rng, n_envs=16, n_steps=256):
         final_eps = np.array([e.eps for e in envs])
     return dict(ctor_u=ctor_u, reset_u=reset_u, obs0=obs0, actions=acts,
                 obs=obs, term_obs=term, reward=rew, done=done, reset_uniforms=ru,
-                final_ep_num=final_ep, final_eps=final_eps,
+                final_ep_num=final_ep, final_eps=final_eps, pre_step=pre_step,
+                **{"pre_" + k: v for k, v in pre.items()},
                 **{"s0_" + k: v for k, v in st.items()})
 
 

@@ -1,0 +1,136 @@
+"""GPU checks of the PPO HIP kernels against the CPU restatement of SB3's
+PPO arithmetic (oracle/ppo_ref.py, oracle/ppo_ref.c).  SB3 itself is not
+available, so these are "parity unpinned" w.r.t. the reference; they pin the
+kernels to the restatement: GAE bit-exact, Philox-derived streams bit-exact,
+float loss/gradients within 1e-5 (f32 reduction-order differences)."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import cref, ppo_ref
+
+pytestmark = pytest.mark.gpu
+
+
+def test_gae_bitexact_vs_oracle():
+    from drone_rl_amd import ppo_kernels as K
+    rng = np.random.default_rng(0)
+    T, N = 32, 50_000
+    r = rng.normal(size=(T, N)).astype(np.float32)
+    v = rng.normal(size=(T, N)).astype(np.float32)
+    st = (rng.random((T, N)) < 0.05).astype(np.uint8)
+    lv = rng.normal(size=N).astype(np.float32)
+    ld = (rng.random(N) < 0.05).astype(np.uint8)
+    cu = lambda x: torch.from_numpy(x).cuda()  # noqa: E731
+    adv, ret = K.gae(cu(r), cu(v), cu(st), cu(lv), cu(ld), 0.99, 0.95)
+    ra, rr = cref.gae(r, v, st, lv, ld, 0.99, 0.95)
+    np.testing.assert_array_equal(adv.cpu().numpy(), ra)
+    np.testing.assert_array_equal(ret.cpu().numpy(), rr)
+
+
+def test_policy_sample_distribution_and_logp():
+    from drone_rl_amd import ppo_kernels as K
+    n = 1 << 20
+    mean = torch.randn(n, 4, device="cuda")
+    log_std = torch.tensor([0.0, -0.5, 0.3, -1.0], device="cuda")
+    raw = torch.empty_like(mean)
+    clip = torch.empty_like(mean)
+    logp = torch.empty(n, device="cuda")
+    K.policy_sample(mean, log_std, seed=5, counter=17, lo=0.0, hi=7.3575,
+                    actions_raw=raw, actions_clipped=clip, logp=logp)
+    z = (raw - mean) / log_std.exp()
+    assert abs(z.mean().item()) < 5e-3 and abs(z.std().item() - 1) < 5e-3
+    assert abs(((z.abs() < 1).float().mean() - 0.6827).item()) < 3e-3
+    d = torch.distributions.Normal(mean, log_std.exp())
+    ref = d.log_prob(raw).sum(1)
+    assert torch.allclose(logp, ref, rtol=1e-5, atol=1e-5)
+    assert torch.equal(clip, raw.clamp(0.0, 7.3575))
+    # same (seed, counter) -> same draws; different counter -> different
+    raw2 = torch.empty_like(mean)
+    K.policy_sample(mean, log_std, 5, 17, 0.0, 7.3575, actions_raw=raw2)
+    assert torch.equal(raw, raw2)
+    K.policy_sample(mean, log_std, 5, 18, 0.0, 7.3575, actions_raw=raw2)
+    assert not torch.equal(raw, raw2)
+
+
+def test_permutation_valid_and_matches_philox_sort():
+    from drone_rl_amd import ppo_kernels as K
+    n = 5000
+    perm = K.Permuter(n, "cuda")(seed=9, counter=3).cpu().numpy()
+    assert np.array_equal(np.sort(perm), np.arange(n))
+    keys = np.zeros(n, np.uint64)
+    for i in range(n):
+        r = cref.philox([i, 0, 3, 0x50000000], [9, 0])
+        keys[i] = (np.uint64(r[0]) << np.uint64(32)) | np.uint64(r[1])
+    np.testing.assert_array_equal(perm, np.argsort(keys, kind="stable"))
+    big = K.Permuter(1 << 21, "cuda")(seed=1, counter=0)
+    assert torch.equal(torch.sort(big.long()).values,
+                       torch.arange(1 << 21, device="cuda"))
+
+
+def test_gather_rows_exact():
+    from drone_rl_amd import ppo_kernels as K
+    src = torch.randn(100_000, 15, device="cuda")
+    idx = torch.randint(0, 100_000, (4096,), device="cuda", dtype=torch.int32)
+    assert torch.equal(K.gather_rows(idx, src), src[idx.long()])
+
+
+@pytest.mark.parametrize("normalize", [True, False])
+def test_ppo_loss_vs_torch_autograd(normalize):
+    from drone_rl_amd import ppo_kernels as K
+    rng = np.random.default_rng(1)
+    m = 65536
+    mean = rng.normal(2.0, 1.0, (m, 4)).astype(np.float32)
+    log_std = np.array([0.1, -0.3, 0.0, 0.2], np.float32)
+    actions = (mean + np.exp(log_std) * rng.normal(size=(m, 4))).astype(np.float32)
+    old_logp = (rng.normal(-5.0, 1.0, m)).astype(np.float32)
+    # make the ratio land on both sides of the clip interval
+    d = torch.distributions.Normal(torch.from_numpy(mean), torch.from_numpy(np.exp(log_std)))
+    lp = d.log_prob(torch.from_numpy(actions)).sum(1).numpy()
+    old_logp = (lp - rng.normal(0, 0.2, m)).astype(np.float32)
+    adv = rng.normal(0.3, 2.0, m).astype(np.float32)
+    returns = rng.normal(size=m).astype(np.float32)
+    values = rng.normal(size=m).astype(np.float32)
+    stats, gm, gls, gv = ppo_ref.ppo_loss_torch(mean, log_std, values, actions, old_logp,
+                                                adv, returns, 0.2, 0.01, 0.5, normalize)
+    L = K.PPOLoss(m, "cuda", 0.2, 0.01, 0.5, normalize)
+    cu = lambda x: torch.from_numpy(x).cuda()  # noqa: E731
+    g_mean, g_ls, g_v, st = L(cu(mean), cu(log_std), cu(values), cu(actions), cu(old_logp),
+                              cu(adv), cu(returns))
+    st = st.cpu().numpy()
+    names = ["loss", "policy_loss", "value_loss", "entropy_loss", "clip_fraction", "approx_kl"]
+    for k, name in enumerate(names):
+        assert abs(st[k] - stats[name]) <= 1e-5 * max(1.0, abs(stats[name])), name
+    assert 0.05 < stats["clip_fraction"] < 0.95
+    scale = np.abs(gm).max()
+    np.testing.assert_allclose(g_mean.cpu().numpy(), gm, rtol=0, atol=1e-4 * scale)
+    np.testing.assert_allclose(g_v.cpu().numpy(), gv, rtol=0, atol=1e-6)
+    np.testing.assert_allclose(g_ls.cpu().numpy(), gls, rtol=1e-4, atol=1e-5)
+
+
+def test_clip_adam_vs_torch():
+    from drone_rl_amd import ppo_kernels as K
+    rng = np.random.default_rng(2)
+    n = 141_065
+    p = rng.normal(size=n).astype(np.float32)
+    for gscale, step in ((10.0, 1), (1e-4, 7)):   # clipped, and not clipped
+        g = (rng.normal(size=n) * gscale / np.sqrt(n)).astype(np.float32)
+        m = (rng.normal(size=n) * 1e-3).astype(np.float32)
+        v = (rng.random(n) * 1e-6).astype(np.float32)
+        rp, rm, rv, rg, rnorm = ppo_ref.clip_adam_torch(p, g, m, v, step)
+        opt = K.ClipAdam(torch.from_numpy(p.copy()).cuda())
+        opt.m.copy_(torch.from_numpy(m))
+        opt.v.copy_(torch.from_numpy(v))
+        opt.t = step - 1
+        gd = torch.from_numpy(g.copy()).cuda()
+        norm = opt.step(gd).item()
+        assert abs(norm - rnorm) <= 1e-5 * rnorm
+        # f32 norms summed in a different order -> clip coefficients agree to
+        # ~1e-6 relative; element tolerances are relative to each array's scale
+        def close(a, b, rel):
+            np.testing.assert_allclose(a, b, rtol=rel, atol=rel * np.abs(b).max())
+        close(gd.cpu().numpy(), rg, 1e-5)
+        close(opt.m.cpu().numpy(), rm, 1e-5)
+        close(opt.v.cpu().numpy(), rv, 1e-5)
+        close(opt.p.cpu().numpy() - p, rp - p, 1e-4)   # the update itself
+        np.testing.assert_allclose(opt.p.cpu().numpy(), rp, rtol=1e-6, atol=1e-7)
