@@ -74,6 +74,11 @@ __host__ __device__ inline double u01_f64(uint32_t a, uint32_t b) {
            (1.0 / 9007199254740992.0);
 }
 
+// Uniform double in [0,1) with 32 random bits (exact: w * 2^-32).
+__host__ __device__ inline double u01_w32(uint32_t w) {
+    return (double)w * (1.0 / 4294967296.0);
+}
+
 // 24-bit uniform float in [0,1).
 __host__ __device__ inline float u01_f32(uint32_t a) {
     return (float)(a >> 8) * (1.0f / 16777216.0f);

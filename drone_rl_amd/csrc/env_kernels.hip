@@ -97,13 +97,11 @@ __device__ inline void reset_uniforms(const EnvView<S> &v, int64_t i,
     const u32x4 r0 = philox4x32_10(c, v.seed_lo, v.seed_hi);
     c.w = TAG_RESET | 1u;
     const u32x4 r1 = philox4x32_10(c, v.seed_lo, v.seed_hi);
-    c.w = TAG_RESET | 2u;
-    const u32x4 r2 = philox4x32_10(c, v.seed_lo, v.seed_hi);
-    u[0] = u01_f64(r0.x, r0.y);
-    u[1] = u01_f64(r0.z, r0.w);
-    u[2] = u01_f64(r1.x, r1.y);
-    u[3] = u01_f64(r1.z, r1.w);
-    u[4] = u01_f64(r2.x, r2.y);
+    u[0] = u01_w32(r0.x);
+    u[1] = u01_w32(r0.y);
+    u[2] = u01_w32(r0.z);
+    u[3] = u01_w32(r0.w);
+    u[4] = u01_w32(r1.x);
 }
 
 // DroneEnv.reset (drone.py:48-75) on registers st[F_N]; updates ep_num/eps
@@ -265,8 +263,14 @@ __global__ __launch_bounds__(kBlock) void env_step_kernel(EnvView<S> v,
     float ob[OD];
     if (i < v.n) {
         S st[F_N];
+        // Issue order = landing order: euler and omega first so the three
+        // sincos range reductions start while pos / vel / target are still
+        // in flight (s_waitcnt vmcnt counts oldest-first).
 #pragma unroll
-        for (int k = 0; k < 12; ++k) st[k] = v.field(k)[i];
+        for (int k = F_EUL; k < F_EUL + 6; ++k) st[k] = v.field(k)[i];
+        const float4 act = reinterpret_cast<const float4 *>(io.actions)[i];
+#pragma unroll
+        for (int k = 0; k < F_EUL; ++k) st[k] = v.field(k)[i];
         if constexpr (VAR == DR_VARIANT_GYM) {
 #pragma unroll
             for (int k = F_TGT; k < F_N; ++k) st[k] = v.field(k)[i];
@@ -275,7 +279,6 @@ __global__ __launch_bounds__(kBlock) void env_step_kernel(EnvView<S> v,
             st[F_TGT + 1] = (S)0;
             st[F_TGT + 2] = (S)10.0;
         }
-        const float4 act = reinterpret_cast<const float4 *>(io.actions)[i];
         int32_t step = v.step[i];
 
         bool crash;
@@ -487,13 +490,13 @@ __global__ __launch_bounds__(kBlock) void env_step_quad_kernel(EnvView<S> v,
                     const uint64_t gid = (uint64_t)(v.env_id_offset + e);
                     const u32x4 rr = philox4x32_10(
                         u32x4{(uint32_t)ep_new, (uint32_t)gid, (uint32_t)(gid >> 32),
-                              TAG_RESET | (uint32_t)k},
+                              TAG_RESET | (uint32_t)(q & 1)},
                         v.seed_lo, v.seed_hi);
-                    u0 = u01_f64(qb<0>(rr.x), qb<0>(rr.y));
-                    u1 = u01_f64(qb<0>(rr.z), qb<0>(rr.w));
-                    u2 = u01_f64(qb<1>(rr.x), qb<1>(rr.y));
-                    u3 = u01_f64(qb<1>(rr.z), qb<1>(rr.w));
-                    u4 = u01_f64(qb<2>(rr.x), qb<2>(rr.y));
+                    u0 = u01_w32(qb<0>(rr.x));
+                    u1 = u01_w32(qb<0>(rr.y));
+                    u2 = u01_w32(qb<0>(rr.z));
+                    u3 = u01_w32(qb<0>(rr.w));
+                    u4 = u01_w32(qb<1>(rr.x));
                 }
                 double eps = v.eps[e];
                 const bool bump = (ep_new % 2000) == 0;

@@ -56,8 +56,10 @@ enum dr_state_dtype {
 };
 
 enum dr_rng_mode {
-    /* reset uniforms from counter-based Philox4x32-10 keyed by
-       (seed, global env id, episode number): reproducible, order-free   */
+    /* reset uniforms from counter-based Philox4x32-10 keyed by seed with
+       counter (episode number, global env id, tag|block): two blocks give
+       the five draws as 32-bit uniforms w * 2^-32.  Reproducible and
+       independent of how many other envs reset, or in which order.      */
     DR_RNG_PHILOX = 0,
     /* reset uniforms read from a caller-provided device buffer (N,5) f64,
        row i = the 5 draws env i's next reset consumes, in the reference's

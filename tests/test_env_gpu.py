@@ -254,8 +254,8 @@ def test_full_size_subset_parity_and_resets(dtype):
         ep_new = int(ep_pre[d][j]) + 1
         r0 = cref.philox([ep_new, i & 0xffffffff, i >> 32, 0x52000000],
                          [seed & 0xffffffff, seed >> 32])
-        u0 = ((int(r0[0]) >> 5) * 67108864.0 + (int(r0[1]) >> 6)) / 9007199254740992.0
-        u1 = ((int(r0[2]) >> 5) * 67108864.0 + (int(r0[3]) >> 6)) / 9007199254740992.0
+        u0 = int(r0[0]) / 4294967296.0
+        u1 = int(r0[1]) / 4294967296.0
         want = np.array([u0 - 0.5, u1 - 0.5, 1.0])
         if dtype == torch.float32:
             want = want.astype(np.float32).astype(np.float64)
