@@ -45,7 +45,10 @@ def parse():
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=1.5)
-    ap.add_argument("--ppo-updates", type=int, default=0)
+    ap.add_argument("--ppo-updates", type=int, default=3,
+                    help="timed PPO iterations for configs[2] (0 = skip)")
+    ap.add_argument("--ppo-epochs", type=int, default=10)
+    ap.add_argument("--ppo-steps", type=int, default=32, help="rollout length T")
     ap.add_argument("--extra", action="store_true",
                     help="also time the f32-state mode and the 4M-env size")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"))
@@ -121,6 +124,48 @@ def time_env(args, dtype_name, n_envs, rank, world, device, steps, warmup):
     return elapsed, gpu_ms, ep
 
 
+def time_ppo(args, rank, world, device):
+    """configs[2]/[3]: 65,536 envs per GPU + PPO (2x256 tanh MLP, GAE 0.95),
+    one PPO iteration = T-step rollout + GAE + n_epochs x minibatches."""
+    import torch
+    import torch.distributed as dist
+
+    from drone_rl_amd.ppo import PPOConfig, PPOTrainer
+    cfg = PPOConfig(num_envs=args.envs, n_steps=args.ppo_steps, batch_size=args.envs,
+                    n_epochs=args.ppo_epochs, state_dtype=args.state_dtype, seed=0)
+    tr = PPOTrainer(cfg, device=device, rank=rank, world_size=world)
+    tr.learn_step()                                   # warm-up iteration
+    torch.cuda.synchronize(device)
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.ppo_updates):
+        st = tr.learn_step()
+    torch.cuda.synchronize(device)
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([el], dtype=torch.float64, device=device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t[0])
+    es = tr.episode_stats()
+    stats = dict(zip(("loss", "policy_loss", "value_loss", "entropy_loss", "clip_fraction",
+                      "approx_kl"), [round(x, 5) for x in st.tolist()[:6]]))
+    tr.close()
+    K = args.ppo_updates
+    return {"updates_per_s": round(K / el, 4),
+            "env_steps_per_s": round(K * cfg.n_steps * cfg.num_envs * world / el, 1),
+            "s_per_update": round(el / K, 4),
+            "config": {"envs_per_gpu": cfg.num_envs, "n_steps": cfg.n_steps,
+                       "minibatch": cfg.batch_size, "n_epochs": cfg.n_epochs,
+                       "optimizer_steps_per_update": cfg.n_epochs * cfg.n_steps *
+                       cfg.num_envs // cfg.batch_size,
+                       "net_arch": list(cfg.net_arch), "mlp_dtype": "fp32",
+                       "grad_allreduce": "rccl" if world > 1 else "none"},
+            "last_update_stats": stats, "episodes": es}
+
+
 def main():
     args = parse()
     rank = int(os.environ.get("RANK", "0"))
@@ -180,6 +225,8 @@ def main():
     }
     if cpu is not None:
         out["cpu_baseline"] = cpu
+    if args.ppo_updates > 0:
+        out["ppo"] = time_ppo(args, rank, world, device)
     if args.extra and world == 1:
         ex = {}
         saved = os.environ.get("DRONERL_STEP_KERNEL")

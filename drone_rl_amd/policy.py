@@ -1,0 +1,114 @@
+"""Actor-critic MLP over ONE flat fp32 parameter buffer.
+
+Mirrors stable-baselines3's default `MlpPolicy` for a Box action space
+(called by the reference at /root/reference/train.py:36-43; SB3 is not
+vendored): Flatten features, separate pi / vf MLPs with
+Tanh, `action_net` Linear(h, 4) for the Gaussian mean, `value_net`
+Linear(h, 1), a state-independent `log_std` (init 0), orthogonal init with
+gains sqrt(2) (hidden), 0.01 (action), 1 (value) and zero biases.
+
+Every parameter is a view into `self.flat`, so autograd accumulates all
+gradients into one contiguous `flat.grad`: one RCCL all-reduce and one fused
+clip+Adam kernel per optimizer step (drone_rl_amd/ppo_kernels.py).  The
+GEMMs run through torch (hipBLASLt -> MFMA, fp32).  The layer order inside
+`flat` is pi layers, action head, vf layers, value head, log_std.
+"""
+from __future__ import annotations
+
+import math
+
+import numpy as np
+import torch
+import torch.nn.functional as F
+
+
+class ActorCritic:
+    def __init__(self, obs_dim: int = 15, act_dim: int = 4, net_arch=(256, 256),
+                 device=None, log_std_init: float = 0.0, seed: int = 0):
+        self.obs_dim, self.act_dim = obs_dim, act_dim
+        self.net_arch = tuple(net_arch)
+        self.device = torch.device(device) if device is not None else torch.device("cpu")
+        self.layout = []            # (name, shape, init gain or None)
+        dims = (obs_dim,) + self.net_arch
+        for pre in ("pi", "vf"):
+            for k in range(len(self.net_arch)):
+                self.layout.append((f"{pre}{k}.w", (dims[k + 1], dims[k]), math.sqrt(2)))
+                self.layout.append((f"{pre}{k}.b", (dims[k + 1],), None))
+            if pre == "pi":
+                self.layout.append(("action.w", (act_dim, dims[-1]), 0.01))
+                self.layout.append(("action.b", (act_dim,), None))
+            else:
+                self.layout.append(("value.w", (1, dims[-1]), 1.0))
+                self.layout.append(("value.b", (1,), None))
+        self.layout.append(("log_std", (act_dim,), "log_std"))
+        self.offsets = {}
+        off = 0
+        for name, shape, _ in self.layout:
+            n = int(np.prod(shape))
+            self.offsets[name] = (off, off + n, shape)
+            off += n
+        self.num_params = off
+        self.flat = torch.zeros(off, dtype=torch.float32, device=self.device)
+        self.reset_parameters(seed, log_std_init)
+        self.flat.requires_grad_(True)
+
+    def reset_parameters(self, seed: int, log_std_init: float = 0.0):
+        g = torch.Generator().manual_seed(seed)
+        host = torch.zeros(self.num_params, dtype=torch.float32)
+        for name, shape, gain in self.layout:
+            a, b, _ = self.offsets[name]
+            if gain == "log_std":
+                host[a:b] = log_std_init
+            elif gain is not None:
+                w = torch.empty(shape)
+                torch.nn.init.orthogonal_(w, gain=gain, generator=g)
+                host[a:b] = w.reshape(-1)
+        with torch.no_grad():
+            self.flat.copy_(host.to(self.device))
+
+    def p(self, name):
+        a, b, shape = self.offsets[name]
+        return self.flat[a:b].view(shape)
+
+    @property
+    def log_std(self):
+        return self.p("log_std")
+
+    def _mlp(self, x, pre):
+        for k in range(len(self.net_arch)):
+            x = torch.tanh(F.linear(x, self.p(f"{pre}{k}.w"), self.p(f"{pre}{k}.b")))
+        return x
+
+    def forward(self, obs):
+        """obs (M, obs_dim) f32 -> (mean (M, act_dim), value (M,))."""
+        mean = F.linear(self._mlp(obs, "pi"), self.p("action.w"), self.p("action.b"))
+        value = F.linear(self._mlp(obs, "vf"), self.p("value.w"), self.p("value.b"))
+        return mean, value.squeeze(-1)
+
+    __call__ = forward
+
+    def state_dict(self):
+        """SB3-style parameter names (policy.mlp_extractor.policy_net.0.weight
+        etc.) mapped to CPU tensors."""
+        out = {}
+        for name, _, _ in self.layout:
+            out[_sb3_name(name, len(self.net_arch))] = self.p(name).detach().cpu().clone()
+        return out
+
+    def load_state_dict(self, sd):
+        with torch.no_grad():
+            for name, _, _ in self.layout:
+                self.p(name).copy_(torch.as_tensor(sd[_sb3_name(name, len(self.net_arch))]))
+
+
+def _sb3_name(name: str, depth: int) -> str:
+    if name == "log_std":
+        return "log_std"
+    if name.startswith("action."):
+        return "action_net." + ("weight" if name.endswith("w") else "bias")
+    if name.startswith("value."):
+        return "value_net." + ("weight" if name.endswith("w") else "bias")
+    net = "policy_net" if name.startswith("pi") else "value_net"
+    k = int(name[2:name.index(".")])
+    # SB3 MlpExtractor: Sequential(Linear, Tanh, Linear, Tanh) -> indices 0, 2
+    return f"mlp_extractor.{net}.{2 * k}." + ("weight" if name.endswith("w") else "bias")

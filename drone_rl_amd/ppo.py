@@ -1,0 +1,220 @@
+"""GPU-resident PPO over the batched quadrotor env (SB3 PPO semantics).
+
+Replaces the reference's `PPO("MlpPolicy", env).learn(...)`
+(/root/reference/train.py:36-43, 63-68; SB3 recalled in SURVEY.md Appendix C)
+with a loop whose every byte stays in HBM:
+
+  rollout (T steps):  policy fwd (torch GEMMs, MFMA)  ->  dr_policy_sample
+                      (Gaussian action, log-prob, clip)  ->  dr_step_monitored
+                      (env physics + auto-reset + VecMonitor stats)
+  advantages:         dr_gae (reverse scan, one thread per env)
+  update (epochs):    dr_permutation  ->  dr_gather_rows (minibatch)  ->
+                      policy fwd/bwd (torch autograd over one flat buffer)
+                      with the loss head from dr_ppo_loss  ->  [RCCL
+                      all-reduce of the flat grad when world > 1]  ->
+                      dr_clip_adam (clip_grad_norm_ + Adam, fused)
+
+SB3-parity choices (documented deviations in DESIGN.md):
+  * no value bootstrap at the 200-step limit (the reference's env is wrapped
+    by shimmy's GymV21 compat, so SB3 sees terminated=True, not truncated);
+    `bootstrap_timeouts=True` is not offered yet;
+  * advantages normalised per minibatch (mean, unbiased std + 1e-8);
+  * the flat rollout index is t*N + n (SB3 uses n*T + t after
+    swap_and_flatten; a uniformly random permutation makes the two
+    statistically identical).
+"""
+from __future__ import annotations
+
+import dataclasses
+import time
+
+import torch
+
+from . import ppo_kernels as K
+from .env import MOTOR_MAX, DroneBatch
+from .policy import ActorCritic
+
+
+@dataclasses.dataclass
+class PPOConfig:
+    num_envs: int = 65536          # envs on this rank
+    n_steps: int = 32              # rollout length T per env
+    batch_size: int = 65536        # minibatch rows
+    n_epochs: int = 10
+    learning_rate: float = 3e-4
+    gamma: float = 0.99
+    gae_lambda: float = 0.95
+    clip_range: float = 0.2
+    ent_coef: float = 0.0
+    vf_coef: float = 0.5
+    max_grad_norm: float = 0.5
+    normalize_advantage: bool = True
+    net_arch: tuple = (256, 256)
+    log_std_init: float = 0.0
+    seed: int = 0
+    state_dtype: str = "f64"       # env state precision ("f64" = reference)
+    variant: str = "gym"
+
+    @classmethod
+    def sb3_defaults(cls, **kw):
+        """The reference's train.py configuration: SB3 PPO defaults, one env,
+        n_steps 2048, batch 64, 10 epochs, 64x64 tanh MLP."""
+        base = dict(num_envs=1, n_steps=2048, batch_size=64, n_epochs=10,
+                    net_arch=(64, 64))
+        base.update(kw)
+        return cls(**base)
+
+
+class PPOTrainer:
+    def __init__(self, cfg: PPOConfig, device=None, rank: int = 0, world_size: int = 1,
+                 process_group=None):
+        self.cfg = cfg
+        self.rank, self.world = rank, world_size
+        self.pg = process_group
+        self.device = torch.device("cuda", torch.cuda.current_device()) \
+            if device is None else torch.device(device)
+        N, T = cfg.num_envs, cfg.n_steps
+        if (N * T) % cfg.batch_size:
+            raise ValueError("num_envs * n_steps must be a multiple of batch_size")
+        dev = self.device
+        self.env = DroneBatch(N, cfg.variant, device=dev, seed=cfg.seed + 1000003 * rank,
+                              env_id_offset=rank * N, monitor=True,
+                              dtype=torch.float64 if cfg.state_dtype == "f64" else torch.float32)
+        od = self.env.obs_dim
+        # every rank starts from the same parameters (the seed is shared);
+        # with world > 1 rank 0's copy is also broadcast (sync_params)
+        self.policy = ActorCritic(od, 4, cfg.net_arch, dev, cfg.log_std_init, cfg.seed)
+        self.opt = K.ClipAdam(self.policy.flat.data, cfg.learning_rate, eps=1e-5,
+                              max_grad_norm=cfg.max_grad_norm)
+        f32 = dict(dtype=torch.float32, device=dev)
+        self.obs = torch.zeros(T + 1, N, od, **f32)           # obs[t] -> action[t]
+        self.dones = torch.ones(T + 1, N, dtype=torch.uint8, device=dev)
+        self.actions = torch.zeros(T, N, 4, **f32)              # unclipped (SB3)
+        self.act_env = torch.zeros(N, 4, **f32)                 # clipped, to the env
+        self.logp = torch.zeros(T, N, **f32)
+        self.values = torch.zeros(T, N, **f32)
+        self.rewards = torch.zeros(T, N, **f32)
+        self.ep_ret = torch.zeros(T, N, **f32)
+        self.ep_len = torch.zeros(T, N, dtype=torch.int32, device=dev)
+        self.adv = torch.zeros(T, N, **f32)
+        self.ret = torch.zeros(T, N, **f32)
+        self.aux = torch.zeros(T * N, 3, **f32)                 # (old logp, adv, return)
+        M = cfg.batch_size
+        self.perm = K.Permuter(T * N, dev)
+        self.mb_obs = torch.zeros(M, od, **f32)
+        self.mb_act = torch.zeros(M, 4, **f32)
+        self.mb_aux = torch.zeros(M, 3, **f32)
+        self.loss = K.PPOLoss(M, dev, cfg.clip_range, cfg.ent_coef, cfg.vf_coef,
+                              cfg.normalize_advantage)
+        self.num_updates = 0
+        self.num_timesteps = 0
+        self._rolled = False
+        self.env.reset(self.obs[0])
+        if self.world > 1:
+            self.sync_params()
+
+    # ------------------------------------------------------------ DP plumbing
+    def sync_params(self):
+        import torch.distributed as dist
+        dist.broadcast(self.policy.flat.data, src=0, group=self.pg)
+
+    def _allreduce_grad(self, g):
+        if self.world > 1:
+            import torch.distributed as dist
+            dist.all_reduce(g, op=dist.ReduceOp.SUM, group=self.pg)
+            g.mul_(1.0 / self.world)
+
+    # ---------------------------------------------------------------- phases
+    @torch.no_grad()
+    def collect_rollouts(self):
+        cfg, T = self.cfg, self.cfg.n_steps
+        if self._rolled:                              # continue where we stopped
+            self.obs[0].copy_(self.obs[T])
+        self.dones[0].copy_(self.dones[T])          # episode_starts of step 0
+        self._rolled = True
+        ls = self.policy.log_std
+        for t in range(T):
+            mean, value = self.policy(self.obs[t])
+            self.values[t].copy_(value)
+            K.policy_sample(mean, ls, seed=cfg.seed * 7919 + self.rank,
+                            counter=self.num_updates * T + t, lo=0.0, hi=MOTOR_MAX,
+                            actions_raw=self.actions[t], actions_clipped=self.act_env,
+                            logp=self.logp[t])
+            # VecMonitor outputs land in this step's slice (done rows only)
+            self.env.ep_ret = self.ep_ret[t]
+            self.env.ep_len = self.ep_len[t]
+            self.env.step(self.act_env, obs_out=self.obs[t + 1], rew_out=self.rewards[t],
+                          done_out=self.dones[t + 1])
+        _, last_values = self.policy(self.obs[T])
+        K.gae(self.rewards, self.values, self.dones[:T], last_values, self.dones[T],
+              cfg.gamma, cfg.gae_lambda, advantages=self.adv, returns=self.ret)
+        torch.stack([self.logp.reshape(-1), self.adv.reshape(-1), self.ret.reshape(-1)],
+                    dim=1, out=self.aux)
+        self.num_timesteps += T * cfg.num_envs * self.world
+
+    def train(self):
+        cfg = self.cfg
+        T, N, M = cfg.n_steps, cfg.num_envs, cfg.batch_size
+        flat = self.policy.flat
+        obs_flat = self.obs[:T].reshape(T * N, -1)
+        act_flat = self.actions.reshape(T * N, 4)
+        a, b, _ = self.policy.offsets["log_std"]
+        stats = []
+        for epoch in range(cfg.n_epochs):
+            perm = self.perm(seed=cfg.seed * 104729 + self.rank,
+                             counter=self.num_updates * cfg.n_epochs + epoch)
+            for k in range(T * N // M):
+                idx = perm[k * M:(k + 1) * M]
+                K.gather_rows(idx, obs_flat, out=self.mb_obs)
+                K.gather_rows(idx, act_flat, out=self.mb_act)
+                K.gather_rows(idx, self.aux, out=self.mb_aux)
+                mean, value = self.policy(self.mb_obs)
+                old_logp = self.mb_aux[:, 0].contiguous()
+                adv = self.mb_aux[:, 1].contiguous()
+                ret = self.mb_aux[:, 2].contiguous()
+                g_mean, g_ls, g_v, st = self.loss(mean.detach().contiguous(),
+                                                  self.policy.log_std.detach().contiguous(),
+                                                  value.detach().contiguous(), self.mb_act,
+                                                  old_logp, adv, ret)
+                flat.grad = None
+                torch.autograd.backward([mean, value], [g_mean, g_v])
+                flat.grad[a:b] += g_ls
+                self._allreduce_grad(flat.grad)
+                self.opt.step(flat.grad)
+                stats.append(st.clone())
+        self.num_updates += 1
+        return torch.stack(stats).mean(0) if stats else None
+
+    def learn_step(self):
+        """One PPO iteration: rollout + GAE + n_epochs of minibatch updates."""
+        self.collect_rollouts()
+        return self.train()
+
+    def episode_stats(self):
+        """Mean return / length of the episodes that ended in the last rollout
+        (VecMonitor's ep_info_buffer role; all-reduced over ranks)."""
+        done = self.dones[1:].bool()
+        s = torch.stack([torch.where(done, self.ep_ret, 0).sum(),
+                         torch.where(done, self.ep_len, 0).sum().float(),
+                         done.sum().float()])
+        if self.world > 1:
+            import torch.distributed as dist
+            dist.all_reduce(s, group=self.pg)
+        n = max(s[2].item(), 1.0)
+        return {"ep_rew_mean": s[0].item() / n, "ep_len_mean": s[1].item() / n,
+                "episodes": int(s[2].item())}
+
+    def learn(self, total_timesteps: int, log_every: int = 1, logger=print):
+        t0 = time.perf_counter()
+        while self.num_timesteps < total_timesteps:
+            st = self.learn_step()
+            if logger and self.rank == 0 and self.num_updates % log_every == 0:
+                es = self.episode_stats()
+                s = st.tolist()
+                logger({"update": self.num_updates, "timesteps": self.num_timesteps,
+                        "fps": int(self.num_timesteps / (time.perf_counter() - t0)),
+                        **es, **dict(zip(K.PPOLoss.STATS, s))})
+        return self
+
+    def close(self):
+        self.env.close()

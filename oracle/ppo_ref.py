@@ -82,3 +82,79 @@ def clip_adam_torch(params, grads, exp_avg, exp_avg_sq, step, lr=3e-4,
     opt.step()
     return (p.detach().numpy(), st["exp_avg"].numpy(), st["exp_avg_sq"].numpy(),
             p.grad.numpy(), norm)
+
+
+def sb3_policy_modules(state, net_arch):
+    """torch.nn modules shaped like SB3's MlpPolicy from an SB3-named
+    state dict (see drone_rl_amd.policy._sb3_name)."""
+    nn = torch.nn
+    d = len(net_arch)
+    pi, vf = [], []
+    for k in range(d):
+        for net, lst in (("policy_net", pi), ("value_net", vf)):
+            w = state[f"mlp_extractor.{net}.{2 * k}.weight"]
+            lin = nn.Linear(w.shape[1], w.shape[0])
+            lin.weight.data.copy_(w)
+            lin.bias.data.copy_(state[f"mlp_extractor.{net}.{2 * k}.bias"])
+            lst += [lin, nn.Tanh()]
+    act = nn.Linear(net_arch[-1], 4)
+    act.weight.data.copy_(state["action_net.weight"])
+    act.bias.data.copy_(state["action_net.bias"])
+    val = nn.Linear(net_arch[-1], 1)
+    val.weight.data.copy_(state["value_net.weight"])
+    val.bias.data.copy_(state["value_net.bias"])
+    log_std = nn.Parameter(state["log_std"].clone())
+    return nn.Sequential(*pi), nn.Sequential(*vf), act, val, log_std
+
+
+def sb3_train(state, net_arch, obs, actions, old_logp, adv, returns, perms, batch_size,
+              lr=3e-4, clip=0.2, ent_coef=0.0, vf_coef=0.5, max_grad_norm=0.5,
+              normalize=True):
+    """PPO.train() as SB3 runs it (CPU, f32), over a flat rollout and a given
+    list of per-epoch permutations.  Returns the updated SB3-named state."""
+    pi, vf, act, val, log_std = sb3_policy_modules(state, net_arch)
+    params = list(pi.parameters()) + list(act.parameters()) + list(vf.parameters()) + \
+        list(val.parameters()) + [log_std]
+    opt = torch.optim.Adam(params, lr=lr, eps=1e-5)
+    obs = torch.as_tensor(obs)
+    actions = torch.as_tensor(actions)
+    old_logp = torch.as_tensor(old_logp)
+    adv_all = torch.as_tensor(adv)
+    ret_all = torch.as_tensor(returns)
+    for perm in perms:
+        perm = torch.as_tensor(perm, dtype=torch.long)
+        for k in range(len(perm) // batch_size):
+            idx = perm[k * batch_size:(k + 1) * batch_size]
+            x = obs[idx]
+            mean = act(pi(x))
+            values = val(vf(x)).flatten()
+            dist = torch.distributions.Normal(mean, torch.ones_like(mean) * log_std.exp())
+            log_prob = dist.log_prob(actions[idx]).sum(dim=1)
+            entropy = dist.entropy().sum(dim=1)
+            a = adv_all[idx]
+            if normalize and len(a) > 1:
+                a = (a - a.mean()) / (a.std() + 1e-8)
+            ratio = torch.exp(log_prob - old_logp[idx])
+            l1 = a * ratio
+            l2 = a * torch.clamp(ratio, 1 - clip, 1 + clip)
+            policy_loss = -torch.min(l1, l2).mean()
+            value_loss = torch.nn.functional.mse_loss(ret_all[idx], values)
+            entropy_loss = -torch.mean(entropy)
+            loss = policy_loss + ent_coef * entropy_loss + vf_coef * value_loss
+            opt.zero_grad()
+            loss.backward()
+            torch.nn.utils.clip_grad_norm_(params, max_grad_norm)
+            opt.step()
+    d = len(net_arch)
+    out = {}
+    for k in range(d):
+        out[f"mlp_extractor.policy_net.{2 * k}.weight"] = pi[2 * k].weight.detach()
+        out[f"mlp_extractor.policy_net.{2 * k}.bias"] = pi[2 * k].bias.detach()
+        out[f"mlp_extractor.value_net.{2 * k}.weight"] = vf[2 * k].weight.detach()
+        out[f"mlp_extractor.value_net.{2 * k}.bias"] = vf[2 * k].bias.detach()
+    out["action_net.weight"] = act.weight.detach()
+    out["action_net.bias"] = act.bias.detach()
+    out["value_net.weight"] = val.weight.detach()
+    out["value_net.bias"] = val.bias.detach()
+    out["log_std"] = log_std.detach()
+    return out
