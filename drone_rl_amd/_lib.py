@@ -66,6 +66,7 @@ SIGNATURES = {
     "dr_get_state": (c_int, [_P, c_int, _P, _P]),
     "dr_set_state": (c_int, [_P, c_int, _P, _P]),
     "dr_set_reset_uniforms": (c_int, [_P, _P]),
+    "dr_set_seed": (c_int, [_P, c_uint64]),
     "dr_random_actions": (c_int, [c_int64, c_uint64, c_int64, c_int64, c_float,
                                   c_float, _P, _P]),
     "dr_last_error": (c_char_p, [_P]),

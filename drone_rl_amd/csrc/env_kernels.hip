@@ -960,6 +960,12 @@ int dr_set_reset_uniforms(dr_handle *h, const double *u_dev) {
     return DR_OK;
 }
 
+int dr_set_seed(dr_handle *h, uint64_t seed) {
+    if (!h) return fail(nullptr, DR_ERR_INVALID, "dr_set_seed: null handle");
+    h->cfg.seed = seed;
+    return DR_OK;
+}
+
 int dr_random_actions(int64_t n, uint64_t seed, int64_t env_id_offset,
                       int64_t step, float lo, float hi, float *out, void *stream) {
     if (n < 0 || !out) return fail(nullptr, DR_ERR_INVALID, "dr_random_actions: bad arguments");

@@ -175,6 +175,11 @@ class DroneBatch:
         check(self.L.dr_set_state(self.handle, fid, ptr(v), _stream(self.device)), self.handle)
         torch.cuda.current_stream(self.device).synchronize()   # v may be freed
 
+    def seed(self, seed: int) -> None:
+        """New Philox key for every later reset (order-free per env)."""
+        self.seed_value = int(seed)
+        check(self.L.dr_set_seed(self.handle, self.seed_value & (2**64 - 1)), self.handle)
+
     def set_reset_uniforms(self, u) -> None:
         """rng='host': (N,5) f64 uniforms consumed by the next resets."""
         t = torch.as_tensor(u, dtype=torch.float64).to(self.device).reshape(

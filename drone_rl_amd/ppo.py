@@ -30,6 +30,7 @@ import time
 
 import torch
 
+from . import dist as D
 from . import ppo_kernels as K
 from .env import MOTOR_MAX, DroneBatch
 from .policy import ActorCritic
@@ -77,8 +78,8 @@ class PPOTrainer:
         if (N * T) % cfg.batch_size:
             raise ValueError("num_envs * n_steps must be a multiple of batch_size")
         dev = self.device
-        self.env = DroneBatch(N, cfg.variant, device=dev, seed=cfg.seed + 1000003 * rank,
-                              env_id_offset=rank * N, monitor=True,
+        self.env = DroneBatch(N, cfg.variant, device=dev, seed=cfg.seed,
+                              env_id_offset=D.env_shard(rank, N)[0], monitor=True,
                               dtype=torch.float64 if cfg.state_dtype == "f64" else torch.float32)
         od = self.env.obs_dim
         # every rank starts from the same parameters (the seed is shared);
@@ -115,14 +116,10 @@ class PPOTrainer:
 
     # ------------------------------------------------------------ DP plumbing
     def sync_params(self):
-        import torch.distributed as dist
-        dist.broadcast(self.policy.flat.data, src=0, group=self.pg)
+        D.broadcast_params_(self.policy.flat.data, group=self.pg)
 
     def _allreduce_grad(self, g):
-        if self.world > 1:
-            import torch.distributed as dist
-            dist.all_reduce(g, op=dist.ReduceOp.SUM, group=self.pg)
-            g.mul_(1.0 / self.world)
+        D.allreduce_mean_(g, self.world, group=self.pg)
 
     # ---------------------------------------------------------------- phases
     @torch.no_grad()
@@ -197,9 +194,7 @@ class PPOTrainer:
         s = torch.stack([torch.where(done, self.ep_ret, 0).sum(),
                          torch.where(done, self.ep_len, 0).sum().float(),
                          done.sum().float()])
-        if self.world > 1:
-            import torch.distributed as dist
-            dist.all_reduce(s, group=self.pg)
+        D.allreduce_sum_(s, self.world, group=self.pg)
         n = max(s[2].item(), 1.0)
         return {"ep_rew_mean": s[0].item() / n, "ep_len_mean": s[1].item() / n,
                 "episodes": int(s[2].item())}

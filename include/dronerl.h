@@ -160,6 +160,10 @@ int dr_set_state(dr_handle *h, int field, const void *in, void *stream);
    in flight. */
 int dr_set_reset_uniforms(dr_handle *h, const double *u_dev);
 
+/* Replace the Philox key used by later resets (VecEnv.seed).  Takes effect
+   for work enqueued after the call. */
+int dr_set_seed(dr_handle *h, uint64_t seed);
+
 /* Synthetic random policy: out (n,4) f32 i.i.d. U[lo,hi) from Philox keyed
    by seed with counter (env_id_offset + i, step).  Not part of the
    reference; it generates the benchmark's action stream. */
