@@ -211,5 +211,50 @@ class PPOTrainer:
                         **es, **dict(zip(K.PPOLoss.STATS, s))})
         return self
 
+    # ------------------------------------------------------------ checkpoint
+    _ENV_FIELDS = ("pos", "vel", "euler", "omega", "target", "current_step", "ep_num", "eps",
+                   "ep_return", "ep_length")
+
+    def state_dict(self):
+        """Everything needed to resume bit-for-bit on the same device count:
+        parameters (SB3 names too), Adam moments and step, the env state
+        including the per-env curriculum (ep_num, eps) that the reference's
+        SB3 .zip does NOT save (drone.py:18,33), rollout continuation, and
+        the counters that key every Philox stream."""
+        T = self.cfg.n_steps
+        return {
+            "config": dataclasses.asdict(self.cfg),
+            "flat": self.policy.flat.detach().cpu().clone(),
+            "policy": self.policy.state_dict(),
+            "adam": {"exp_avg": self.opt.m.cpu().clone(), "exp_avg_sq": self.opt.v.cpu().clone(),
+                     "step": self.opt.t},
+            "env": {k: self.env.get(k).cpu() for k in self._ENV_FIELDS},
+            "last_obs": self.obs[T if self._rolled else 0].cpu().clone(),
+            "last_dones": self.dones[T].cpu().clone(),
+            "num_updates": self.num_updates, "num_timesteps": self.num_timesteps,
+            "rank": self.rank, "world_size": self.world,
+        }
+
+    def save(self, path):
+        torch.save(self.state_dict(), path)
+
+    def load_state_dict(self, sd):
+        T = self.cfg.n_steps
+        with torch.no_grad():
+            self.policy.flat.copy_(sd["flat"].to(self.device))
+            self.opt.m.copy_(sd["adam"]["exp_avg"].to(self.device))
+            self.opt.v.copy_(sd["adam"]["exp_avg_sq"].to(self.device))
+            self.opt.t = int(sd["adam"]["step"])
+            for k, v in sd["env"].items():
+                self.env.set(k, v)
+            self.obs[0].copy_(sd["last_obs"].to(self.device))
+            self.dones[T].copy_(sd["last_dones"].to(self.device))
+        self._rolled = False
+        self.num_updates = int(sd["num_updates"])
+        self.num_timesteps = int(sd["num_timesteps"])
+
+    def load(self, path):
+        self.load_state_dict(torch.load(path, map_location="cpu", weights_only=True))
+
     def close(self):
         self.env.close()

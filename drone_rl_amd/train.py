@@ -1,0 +1,67 @@
+"""Drop-in for the reference's train.py (/root/reference/train.py:1-70):
+PPO on the quadrotor env, here GPU-resident over N batched envs.
+
+  python -m drone_rl_amd.train                        # 65,536 envs, 2x256 MLP
+  python -m drone_rl_amd.train --sb3-defaults --envs 1 # the reference's config
+  torchrun --nproc-per-node 8 --master-addr 127.0.0.1 -m drone_rl_amd.train
+
+Like the reference it resumes from a checkpoint when one exists
+(train.py:10-31; ours also restores the env curriculum), trains for
+--total-steps (train.py:11,63-68) and saves at the end (train.py:70).
+Logs are JSON lines on stdout (SB3's logger keys: ep_rew_mean, ep_len_mean,
+fps, loss terms) instead of TensorBoard.
+"""
+import argparse
+import json
+import os
+
+import torch
+import torch.distributed as dist
+
+from .ppo import PPOConfig, PPOTrainer
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--envs", type=int, default=65536, help="envs per GPU")
+    ap.add_argument("--total-steps", type=float, default=2e6 * 64)
+    ap.add_argument("--n-steps", type=int, default=32)
+    ap.add_argument("--batch-size", type=int, default=65536)
+    ap.add_argument("--epochs", type=int, default=10)
+    ap.add_argument("--lr", type=float, default=3e-4)
+    ap.add_argument("--net", type=int, nargs="+", default=[256, 256])
+    ap.add_argument("--state-dtype", choices=["f64", "f32"], default="f64")
+    ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--sb3-defaults", action="store_true",
+                    help="SB3 PPO defaults of the reference (n_steps 2048, batch 64, 64x64)")
+    ap.add_argument("--checkpoint", default="./dd_gpu.pt")
+    ap.add_argument("--log-every", type=int, default=1)
+    a = ap.parse_args(argv)
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    if a.sb3_defaults:
+        cfg = PPOConfig.sb3_defaults(num_envs=a.envs, seed=a.seed, state_dtype=a.state_dtype)
+    else:
+        cfg = PPOConfig(num_envs=a.envs, n_steps=a.n_steps, batch_size=a.batch_size,
+                        n_epochs=a.epochs, learning_rate=a.lr, net_arch=tuple(a.net),
+                        seed=a.seed, state_dtype=a.state_dtype)
+    tr = PPOTrainer(cfg, rank=rank, world_size=world)
+    ck = a.checkpoint if world == 1 else f"{a.checkpoint}.rank{rank}"
+    if os.path.exists(ck):
+        tr.load(ck)
+        if rank == 0:
+            print(json.dumps({"resumed": ck, "num_timesteps": tr.num_timesteps}), flush=True)
+    tr.learn(int(a.total_steps), log_every=a.log_every,
+             logger=lambda d: print(json.dumps(d), flush=True))
+    tr.save(ck)
+    tr.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()
