@@ -56,3 +56,20 @@ def test_config_defaults():
     assert (c.n_steps, c.batch_size, c.n_epochs, c.net_arch) == (2048, 64, 10, (64, 64))
     assert c.gamma == 0.99 and c.gae_lambda == 0.95 and c.clip_range == 0.2
     assert c.ent_coef == 0.0 and c.vf_coef == 0.5 and c.max_grad_norm == 0.5
+
+
+def test_splitk_linear_matches_autograd():
+    from drone_rl_amd.policy import _SplitKLinear
+    torch.manual_seed(0)
+    x = torch.randn(8192, 33, requires_grad=True)
+    w = torch.randn(17, 33, requires_grad=True)
+    b = torch.randn(17, requires_grad=True)
+    g = torch.randn(8192, 17)
+    y = _SplitKLinear.apply(x, w, b, 64)
+    y.backward(g)
+    x2, w2, b2 = x.detach().clone().requires_grad_(), w.detach().clone().requires_grad_(), \
+        b.detach().clone().requires_grad_()
+    torch.nn.functional.linear(x2, w2, b2).backward(g)
+    assert torch.allclose(y, torch.nn.functional.linear(x2, w2, b2), atol=1e-5)
+    for a, r in ((x.grad, x2.grad), (w.grad, w2.grad), (b.grad, b2.grad)):
+        assert torch.allclose(a, r, rtol=1e-4, atol=1e-3)
