@@ -40,10 +40,49 @@ constexpr double kFactor = kArm / 1.4142135623730951;  // L / np.sqrt(2)
 constexpr float kKyaw32 = 0.01f;  // python float * np.float32 -> f32 (NEP 50)
 constexpr double kDt = 0.02;
 
+// DR_ABLATE (diagnostic builds only, scripts/micro/ablate.sh; never set in
+// the product build): 1 = f32 trig, 2 = no auto-reset, 3 = no LDS obs
+// staging, 4 = divides by reciprocal multiplies.
+#ifndef DR_ABLATE
+#define DR_ABLATE 0
+#endif
+// 1: load eps with the state (a reset never waits on a dependent load)
+#ifndef DR_STRIDE_PAD
+#define DR_STRIDE_PAD 0
+#endif
+// 1: obs staged per wave (no block barrier); 0: per block
+#ifndef DR_WAVE_STAGE
+#define DR_WAVE_STAGE 1
+#endif
+#ifndef DR_PREFETCH_EPS
+#define DR_PREFETCH_EPS 0
+#endif
+#if DR_ABLATE == 1
+__device__ inline void m_sincos(double x, double *s, double *c) {
+    float fs, fc;
+    __sincosf((float)x, &fs, &fc);
+    *s = fs;
+    *c = fc;
+}
+#else
 __device__ inline void m_sincos(double x, double *s, double *c) { sincos(x, s, c); }
+#endif
 __device__ inline void m_sincos(float x, float *s, float *c) { sincosf(x, s, c); }
 __device__ inline double m_sqrt(double x) { return sqrt(x); }
 __device__ inline float m_sqrt(float x) { return sqrtf(x); }
+
+__device__ inline double m_fma(double a, double b, double c) { return fma(a, b, c); }
+__device__ inline float m_fma(float a, float b, float c) { return fmaf(a, b, c); }
+
+// x / d given rd = RN(1/d): q = RN(x*rd), then one Markstein correction with
+// the exact FMA remainder, giving the correctly rounded quotient (up to
+// rare 1-ulp cases) in 3 instructions instead of the ~10 of an IEEE divide.
+template <typename S>
+__device__ inline S div_rcp(S x, S d, S rd) {
+    const S q = x * rd;
+    const S r = m_fma(-q, d, x);
+    return m_fma(r, rd, q);
+}
 
 enum : int { F_POS = 0, F_VEL = 3, F_EUL = 6, F_OMG = 9, F_TGT = 12, F_N = 15 };
 
@@ -108,11 +147,11 @@ __device__ inline void reset_uniforms(const EnvView<S> &v, int64_t i,
 // in memory, returns the new step counter (0).
 template <typename S>
 __device__ inline void gym_reset_regs(const EnvView<S> &v, int64_t i, int mode,
-                                      S st[F_N]) {
-    const int32_t ep_new = v.ep_num[i] + 1;   // ep_num += 1          (61)
+                                      S st[F_N], int32_t ep_old, double eps) {
+    const int32_t ep_new = ep_old + 1;        // ep_num += 1          (61)
     double u[5];
     reset_uniforms(v, i, ep_new, mode, u);
-    double eps = v.eps[i];
+    if (!DR_PREFETCH_EPS) eps = v.eps[i];
     if (ep_new % 2000 == 0) {                 // curriculum bump      (68-70)
         eps += 0.1;
         v.eps[i] = eps;
@@ -190,12 +229,13 @@ __device__ inline S physics_step(S st[F_N], float4 act, S dt, bool &crash) {
     const S w0 = st[F_OMG + 0], w1 = st[F_OMG + 1], w2 = st[F_OMG + 2];
     // tan(theta) from the shared sincos (np.tan rounds once; this rounds the
     // quotient once more: <= 2 ulp apart, far inside the parity bar).
-    const S tth = sth / cth;
+    const S sec = (S)1 / cth;        // the only IEEE divide; also vd:116
+    const S tth = div_rcp(sth, cth, sec);
     S ed2;
     if constexpr (VAR == DR_VARIANT_GYM) {
-        ed2 = ((S)0 * w0 + (sph / cth) * w1) + (cph / cth) * w2;      // (184)
+        ed2 = ((S)0 * w0 + div_rcp(sph, cth, sec) * w1) +
+              div_rcp(cph, cth, sec) * w2;                             // (184)
     } else {
-        const S sec = (S)1 / cth;                                      // vd:116
         ed2 = ((S)0 * w0 + (sph * sec) * w1) + (cph * sec) * w2;
     }
     const S ed0 = ((S)1 * w0 + (sph * tth) * w1) + (cph * tth) * w2;
@@ -205,9 +245,15 @@ __device__ inline S physics_step(S st[F_N], float4 act, S dt, bool &crash) {
     st[F_EUL + 2] += ed2 * dt;
 
     // Angular dynamics, diagonal inertia, old omega (135-139).
-    const S wd0 = (tau_phi - (S)(kIyy - kIzz) * w1 * w2) / (S)kIxx;
-    const S wd1 = (tau_theta - (S)(kIzz - kIxx) * w0 * w2) / (S)kIyy;
-    const S wd2 = ((S)tau_psi - (S)(kIxx - kIyy) * w0 * w1) / (S)kIzz;
+#if DR_ABLATE == 4
+    const S wd0 = (tau_phi - (S)(kIyy - kIzz) * w1 * w2) * (S)(1.0 / kIxx);
+    const S wd1 = (tau_theta - (S)(kIzz - kIxx) * w0 * w2) * (S)(1.0 / kIyy);
+    const S wd2 = ((S)tau_psi - (S)(kIxx - kIyy) * w0 * w1) * (S)(1.0 / kIzz);
+#else
+    const S wd0 = div_rcp(tau_phi - (S)(kIyy - kIzz) * w1 * w2, (S)kIxx, (S)(1.0 / kIxx));
+    const S wd1 = div_rcp(tau_theta - (S)(kIzz - kIxx) * w0 * w2, (S)kIyy, (S)(1.0 / kIyy));
+    const S wd2 = div_rcp((S)tau_psi - (S)(kIxx - kIyy) * w0 * w1, (S)kIzz, (S)(1.0 / kIzz));
+#endif
     st[F_OMG + 0] += wd0 * dt;
     st[F_OMG + 1] += wd1 * dt;
     st[F_OMG + 2] += wd2 * dt;
@@ -230,6 +276,33 @@ __device__ inline S physics_step(S st[F_N], float4 act, S dt, bool &crash) {
     const S pn = m_sqrt((px * px + py * py) + pz * pz);
     crash = (pz < (S)0) || (pn > (S)50);
     return r;
+}
+
+// Per-wave variant: each wave stages its own 64 rows (3,840 B) and writes
+// them out with no workgroup barrier, so a wave delayed by a reset or a late
+// load does not hold back the other three waves of its block.
+template <int OD>
+__device__ inline void store_obs_wave(float *sh_block, const float ob[OD],
+                                      float *dst_all, int64_t n) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    float *sh = sh_block + w * 64 * OD;
+#pragma unroll
+    for (int k = 0; k < OD; ++k) sh[lane * OD + k] = ob[k];
+    // DS ops of one wave execute in order; the barrier only pins the
+    // compiler's schedule (no workgroup s_barrier is emitted)
+    __builtin_amdgcn_wave_barrier();
+    const int64_t wbase = (int64_t)blockIdx.x * kBlock + w * 64;
+    const int64_t nvalid = (n - wbase) < 64 ? (n - wbase) : 64;
+    if (nvalid <= 0) return;
+    float *dst = dst_all + wbase * OD;
+    if (nvalid == 64 && (((uintptr_t)dst) & 15) == 0) {
+        const float4 *s4 = reinterpret_cast<const float4 *>(sh);
+        float4 *d4 = reinterpret_cast<float4 *>(dst);
+#pragma unroll
+        for (int q = lane; q < 64 * OD / 4; q += 64) d4[q] = s4[q];
+    } else {
+        for (int q = lane; q < (int)nvalid * OD; q += 64) dst[q] = sh[q];
+    }
 }
 
 template <int OD>
@@ -280,6 +353,15 @@ __global__ __launch_bounds__(kBlock) void env_step_kernel(EnvView<S> v,
             st[F_TGT + 2] = (S)10.0;
         }
         int32_t step = v.step[i];
+        // needed only if this env resets; loaded up front so a reset does
+        // not stall the wave on a dependent global load (+12 B per step,
+        // counted in the measured traffic, not in the 305 B algorithmic)
+        int32_t ep_old = 0;
+        double eps_old = 0.0;
+        if constexpr (VAR == DR_VARIANT_GYM) {
+            ep_old = v.ep_num[i];
+            if (DR_PREFETCH_EPS) eps_old = v.eps[i];
+        }
 
         bool crash;
         const S r = physics_step<S, VAR>(st, act, v.dt, crash);
@@ -297,13 +379,13 @@ __global__ __launch_bounds__(kBlock) void env_step_kernel(EnvView<S> v,
             len = v.ep_len[i] + 1;
         }
         if constexpr (VAR == DR_VARIANT_GYM) {
-            if (done && io.auto_reset) {
+            if (done && io.auto_reset && DR_ABLATE != 2) {
                 // DummyVecEnv: keep the terminal obs, reset in the same step.
                 if (io.term_obs) {
 #pragma unroll
                     for (int k = 0; k < OD; ++k) io.term_obs[i * OD + k] = ob[k];
                 }
-                gym_reset_regs(v, i, v.host_u ? 1 : 0, st);
+                gym_reset_regs(v, i, v.host_u ? 1 : 0, st, ep_old, eps_old);
                 step = 0;
 #pragma unroll
                 for (int k = F_TGT; k < F_N; ++k) v.field(k)[i] = st[k];
@@ -327,7 +409,17 @@ __global__ __launch_bounds__(kBlock) void env_step_kernel(EnvView<S> v,
 #pragma unroll
         for (int k = 0; k < OD; ++k) ob[k] = 0.f;
     }
+#if DR_ABLATE == 3
+    if (i < v.n) {
+#pragma unroll
+        for (int k = 0; k < OD; ++k) io.obs[i * OD + k] = ob[k];
+    }
+    (void)sh4;
+#elif DR_WAVE_STAGE
+    store_obs_wave<OD>(reinterpret_cast<float *>(sh4), ob, io.obs, v.n);
+#else
     store_obs_block<OD>(reinterpret_cast<float *>(sh4), ob, io.obs, base, v.n);
+#endif
 }
 
 // ----------------------------------------------------------------------------
@@ -422,12 +514,12 @@ __global__ __launch_bounds__(kBlock) void env_step_quad_kernel(EnvView<S> v,
 
         // ---- Euler-angle rates, row k of W(old phi, theta) (131-132, 176-186)
         S c1, c2;
-        const S tth = sth / cth;
+        const S sec = (S)1 / cth;                          // also vd:116
+        const S tth = div_rcp(sth, cth, sec);
         if constexpr (VAR == DR_VARIANT_GYM) {
-            c1 = sel3(k, sph * tth, cph, sph / cth);
-            c2 = sel3(k, cph * tth, -sph, cph / cth);
+            c1 = sel3(k, sph * tth, cph, div_rcp(sph, cth, sec));
+            c2 = sel3(k, cph * tth, -sph, div_rcp(cph, cth, sec));
         } else {
-            const S sec = (S)1 / cth;                      // vd:116
             c1 = sel3(k, sph * tth, cph, sph * sec);
             c2 = sel3(k, cph * tth, -sph, cph * sec);
         }
@@ -440,7 +532,8 @@ __global__ __launch_bounds__(kBlock) void env_step_quad_kernel(EnvView<S> v,
         const S Ik = (S)sel3(k, kIxx, kIyy, kIzz);
         const S wa = k == 0 ? w1 : w0;
         const S wb = k == 2 ? w1 : w2;
-        const S wd = (tau - dI * wa * wb) / Ik;
+        const S rIk = (S)sel3(k, 1.0 / kIxx, 1.0 / kIyy, 1.0 / kIzz);
+        const S wd = div_rcp(tau - dI * wa * wb, Ik, rIk);
         w += wd * v.dt;
 
         // ---- reward / termination on the new position (142-157)
@@ -583,7 +676,7 @@ __global__ __launch_bounds__(kBlock) void env_reset_kernel(EnvView<S> v,
         const bool doit = (mask == nullptr) || mask[i];
         if (doit) {
             if constexpr (VAR == DR_VARIANT_GYM) {
-                gym_reset_regs(v, i, mode, st);
+                gym_reset_regs(v, i, mode, st, v.ep_num[i], v.eps[i]);
             } else {
                 vec_reset_regs(st);
             }
@@ -816,7 +909,10 @@ int dr_create(const dr_config *cfg_in, dr_handle **out) {
     if (!h) return fail(nullptr, DR_ERR_NOMEM, "dr_create: host allocation failed");
     h->cfg = cfg;
     h->n = cfg.num_envs;
-    h->stride = (cfg.num_envs + 63) / 64 * 64;
+    // SoA arrays are `stride` elements apart.  A pure power-of-two spacing
+    // would put the 17 concurrently streamed arrays at congruent addresses
+    // (same HBM channel bits); DR_STRIDE_PAD elements of skew break that.
+    h->stride = (cfg.num_envs + 63) / 64 * 64 + DR_STRIDE_PAD;
     h->obs_dim = cfg.variant == DR_VARIANT_GYM ? 15 : 12;
     // Step kernel choice: one lane per env unless DRONERL_STEP_KERNEL=quad
     // (4 lanes per env; fewer serial f64 ops per lane, more total VALU work:
