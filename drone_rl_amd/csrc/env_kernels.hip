@@ -42,13 +42,37 @@ constexpr double kDt = 0.02;
 
 // DR_ABLATE (diagnostic builds only, scripts/micro/ablate.sh; never set in
 // the product build): 1 = f32 trig, 2 = no auto-reset, 3 = no LDS obs
-// staging, 4 = divides by reciprocal multiplies.
+// staging, 4 = divides by reciprocal multiplies, 5 = constant reset draws.
 #ifndef DR_ABLATE
 #define DR_ABLATE 0
 #endif
 // 1: load eps with the state (a reset never waits on a dependent load)
 #ifndef DR_STRIDE_PAD
 #define DR_STRIDE_PAD 0
+#endif
+// DR_STAMPS (diagnostic builds only): per-wave s_memrealtime / s_memtime
+// stamps at phase boundaries of env_step_kernel into a module-scope array,
+// read back by dr_diag_stamps (scripts/micro/stamps.py).  Never set in the
+// product build; no output element is computed from a stamp.
+#ifndef DR_STAMPS
+#define DR_STAMPS 0
+#endif
+#if DR_STAMPS
+__device__ unsigned long long g_stamps[16384 * 8];
+#define DR_STAMP(k)                                                            \
+    do {                                                                       \
+        __builtin_amdgcn_sched_barrier(0);                                     \
+        const unsigned long long t__ = __builtin_amdgcn_s_memrealtime();       \
+        const unsigned w__ = blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6);   \
+        const unsigned long long m__ = __ballot(1);                          \
+        if ((int)(threadIdx.x & 63) == __ffsll((long long)m__) - 1 && w__ < 16384) \
+            g_stamps[w__ * 8 + (k)] = t__;                                     \
+        __builtin_amdgcn_sched_barrier(0);                                     \
+    } while (0)
+#else
+#define DR_STAMP(k) \
+    do {            \
+    } while (0)
 #endif
 // 1: obs staged per wave (no block barrier); 0: per block
 #ifndef DR_WAVE_STAGE
@@ -126,7 +150,7 @@ __device__ inline void reset_uniforms(const EnvView<S> &v, int64_t i,
         for (int k = 0; k < 5; ++k) u[k] = v.host_u[i * 5 + k];
         return;
     }
-    if (mode == 2) {
+    if (mode == 2 || DR_ABLATE == 5) {
 #pragma unroll
         for (int k = 0; k < 5; ++k) u[k] = 0.5;
         return;
@@ -151,6 +175,7 @@ __device__ inline void gym_reset_regs(const EnvView<S> &v, int64_t i, int mode,
     const int32_t ep_new = ep_old + 1;        // ep_num += 1          (61)
     double u[5];
     reset_uniforms(v, i, ep_new, mode, u);
+    DR_STAMP(6);
     if (!DR_PREFETCH_EPS) eps = v.eps[i];
     if (ep_new % 2000 == 0) {                 // curriculum bump      (68-70)
         eps += 0.1;
@@ -165,6 +190,7 @@ __device__ inline void gym_reset_regs(const EnvView<S> &v, int64_t i, int mode,
     st[F_TGT + 0] = (S)(eps * u[2]);          // (73)
     st[F_TGT + 1] = (S)(eps * u[3]);
     st[F_TGT + 2] = (S)(eps * u[4] + 1.0 + 0.0);
+    DR_STAMP(7);
 }
 
 template <typename S>
@@ -209,6 +235,7 @@ __device__ inline S physics_step(S st[F_N], float4 act, S dt, bool &crash) {
     const S theta = st[F_EUL + 1];
     S sph, cph, sth, cth, sps, cps;
     m_sincos(st[F_EUL + 0], &sph, &cph);
+    DR_STAMP(1);
     m_sincos(theta, &sth, &cth);
     m_sincos(st[F_EUL + 2], &sps, &cps);
     // R(old euler) column 2 (drone.py:169-173): thrust is body-z only.
@@ -333,6 +360,7 @@ __global__ __launch_bounds__(kBlock) void env_step_kernel(EnvView<S> v,
     __shared__ float4 sh4[kBlock * OD / 4];
     const int64_t base = (int64_t)blockIdx.x * kBlock;
     const int64_t i = base + threadIdx.x;
+    DR_STAMP(0);
     float ob[OD];
     if (i < v.n) {
         S st[F_N];
@@ -365,6 +393,7 @@ __global__ __launch_bounds__(kBlock) void env_step_kernel(EnvView<S> v,
 
         bool crash;
         const S r = physics_step<S, VAR>(st, act, v.dt, crash);
+        DR_STAMP(2);
         step += 1;                                         // (155)
         bool done = crash || (step >= v.max_steps);        // (156-157)
         const float rf = (float)r;                         // SB3 f32 buffer
@@ -402,9 +431,11 @@ __global__ __launch_bounds__(kBlock) void env_step_kernel(EnvView<S> v,
             v.ep_ret[i] = ret;
             v.ep_len[i] = len;
         }
+        DR_STAMP(3);
 #pragma unroll
         for (int k = 0; k < 12; ++k) v.field(k)[i] = st[k];
         v.step[i] = step;
+        DR_STAMP(4);
     } else {
 #pragma unroll
         for (int k = 0; k < OD; ++k) ob[k] = 0.f;
@@ -420,6 +451,7 @@ __global__ __launch_bounds__(kBlock) void env_step_kernel(EnvView<S> v,
 #else
     store_obs_block<OD>(reinterpret_cast<float *>(sh4), ob, io.obs, base, v.n);
 #endif
+    DR_STAMP(5);
 }
 
 // ----------------------------------------------------------------------------
@@ -1076,6 +1108,14 @@ int dr_random_actions(int64_t n, uint64_t seed, int64_t env_id_offset,
         return fail(nullptr, DR_ERR_HIP, std::string("random_actions: ") + hipGetErrorString(e));
     return DR_OK;
 }
+
+#if DR_STAMPS
+int dr_diag_stamps(void *host_out, size_t bytes) {
+    hipError_t e = hipMemcpyFromSymbol(host_out, HIP_SYMBOL(g_stamps), bytes, 0,
+                                       hipMemcpyDeviceToHost);
+    return e == hipSuccess ? DR_OK : DR_ERR_HIP;
+}
+#endif
 
 const char *dr_last_error(const dr_handle *h) {
     return h ? h->err.c_str() : global_error();
