@@ -77,6 +77,8 @@ SIGNATURES = {
     "dr_permutation_workspace_bytes": (c_size_t, [c_int64]),
     "dr_permutation": (c_int, [c_int64, c_uint64, c_uint64, _P, _P, c_size_t, _P]),
     "dr_gather_rows": (c_int, [c_int64, c_int64, _P, _P, _P, _P]),
+    "dr_tanh_backward_workspace_bytes": (c_size_t, [c_int64, c_int64]),
+    "dr_tanh_backward": (c_int, [c_int64, c_int64, _P, _P, _P, _P, _P, c_size_t, _P]),
     "dr_ppo_loss_workspace_bytes": (c_size_t, [c_int64]),
     "dr_ppo_loss": (c_int, [c_int64, _P, _P, _P, _P, _P, _P, _P, c_float,
                             c_float, c_float, c_int, _P, _P, _P, _P, _P,

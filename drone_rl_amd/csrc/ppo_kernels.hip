@@ -138,6 +138,73 @@ __global__ __launch_bounds__(kBlock) void gather_rows_kernel(
 }
 
 // --------------------------------------------------------------------------
+// Tanh backward + bias gradient.  Block b owns rows [b*R, (b+1)*R); thread t
+// owns 4 columns (float4) of one of 256/(n/4) row lanes; per-thread column
+// partial sums are combined across the block's row lanes in LDS, giving one
+// partial row per block; a second kernel sums the partial rows.
+// --------------------------------------------------------------------------
+constexpr int kTanhRows = 256;
+
+__global__ __launch_bounds__(kBlock) void tanh_bwd_kernel(
+    int64_t m, int n4, const float4 *__restrict__ gh, const float4 *__restrict__ h,
+    float4 *__restrict__ gz, float4 *__restrict__ part) {
+    __shared__ float4 red[kBlock];
+    const int lanes = kBlock / n4;               // row lanes per block
+    const int c = threadIdx.x % n4, rl = threadIdx.x / n4;
+    const int64_t r0 = (int64_t)blockIdx.x * kTanhRows;
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+    constexpr int U = 8;                         // row pairs in flight per thread
+    if (rl < lanes) {
+        for (int r = rl; r < kTanhRows; r += U * lanes) {
+            float4 g[U], y[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int64_t row = r0 + r + u * lanes;
+                const bool ok = (r + u * lanes < kTanhRows) && row < m;
+                g[u] = ok ? gh[row * n4 + c] : make_float4(0.f, 0.f, 0.f, 0.f);
+                y[u] = ok ? h[row * n4 + c] : make_float4(0.f, 0.f, 0.f, 0.f);
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int64_t row = r0 + r + u * lanes;
+                float4 z;
+                z.x = g[u].x * (1.0f - y[u].x * y[u].x);
+                z.y = g[u].y * (1.0f - y[u].y * y[u].y);
+                z.z = g[u].z * (1.0f - y[u].z * y[u].z);
+                z.w = g[u].w * (1.0f - y[u].w * y[u].w);
+                if ((r + u * lanes < kTanhRows) && row < m) gz[row * n4 + c] = z;
+                acc.x += z.x;
+                acc.y += z.y;
+                acc.z += z.z;
+                acc.w += z.w;
+            }
+        }
+    }
+    red[threadIdx.x] = acc;
+    __syncthreads();
+    if (rl == 0) {
+        for (int k = 1; k < lanes; ++k) {
+            const float4 v = red[k * n4 + c];
+            acc.x += v.x;
+            acc.y += v.y;
+            acc.z += v.z;
+            acc.w += v.w;
+        }
+        part[(int64_t)blockIdx.x * n4 + c] = acc;
+    }
+}
+
+__global__ void colsum_kernel(int nb, int n, const float *__restrict__ part,
+                              float *__restrict__ out) {
+    const int j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= n) return;
+    float s = 0.f;
+#pragma unroll 16
+    for (int b = 0; b < nb; ++b) s += part[(int64_t)b * n + j];
+    out[j] = s;
+}
+
+// --------------------------------------------------------------------------
 // Block reductions (wave64 shuffles, then LDS across the 4 waves).
 // --------------------------------------------------------------------------
 __device__ inline float wave_sum(float x) {
@@ -471,6 +538,34 @@ int dr_gather_rows(int64_t m, int64_t width, const int32_t *idx, const float *sr
     hipLaunchKernelGGL(gather_rows_kernel, dim3(grid_for(m * width)), dim3(kBlock), 0,
                        as_stream(stream), m, width, idx, src, dst);
     return check_launch("dr_gather_rows");
+}
+
+size_t dr_tanh_backward_workspace_bytes(int64_t m, int64_t n) {
+    const int64_t nb = (m + kTanhRows - 1) / kTanhRows;
+    return align_up(sizeof(float) * (size_t)(nb * n));
+}
+
+int dr_tanh_backward(int64_t m, int64_t n, const float *grad_h, const float *h,
+                     float *grad_z, float *bias_grad, void *workspace, size_t workspace_bytes,
+                     void *stream) {
+    if (m < 1 || n < 4 || n % 4 || n > 4 * kBlock || !grad_h || !h || !grad_z || !bias_grad)
+        return fail0(DR_ERR_INVALID, "dr_tanh_backward: bad arguments (n % 4, n <= 1024)");
+    if ((((uintptr_t)grad_h) | ((uintptr_t)h) | ((uintptr_t)grad_z)) & 15)
+        return fail0(DR_ERR_INVALID, "dr_tanh_backward: buffers must be 16-byte aligned");
+    if (!workspace || workspace_bytes < dr_tanh_backward_workspace_bytes(m, n))
+        return fail0(DR_ERR_INVALID, "dr_tanh_backward: workspace too small");
+    const int nb = (int)((m + kTanhRows - 1) / kTanhRows);
+    float *part = static_cast<float *>(workspace);
+    hipStream_t st = as_stream(stream);
+    hipLaunchKernelGGL(tanh_bwd_kernel, dim3(nb), dim3(kBlock), 0, st, m, (int)(n / 4),
+                       reinterpret_cast<const float4 *>(grad_h),
+                       reinterpret_cast<const float4 *>(h), reinterpret_cast<float4 *>(grad_z),
+                       reinterpret_cast<float4 *>(part));
+    int rc = check_launch("dr_tanh_backward");
+    if (rc) return rc;
+    hipLaunchKernelGGL(colsum_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, nb,
+                       (int)n, part, bias_grad);
+    return check_launch("dr_tanh_backward colsum");
 }
 
 size_t dr_ppo_loss_workspace_bytes(int64_t m) {

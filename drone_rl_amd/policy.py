@@ -145,3 +145,92 @@ def _sb3_name(name: str, depth: int) -> str:
     k = int(name[2:name.index(".")])
     # SB3 MlpExtractor: Sequential(Linear, Tanh, Linear, Tanh) -> indices 0, 2
     return f"mlp_extractor.{net}.{2 * k}." + ("weight" if name.endswith("w") else "bias")
+
+
+class FusedTrainStep:
+    """Forward + hand-written backward of the actor-critic for one minibatch,
+    writing every parameter gradient straight into a flat buffer (no
+    autograd graph, no per-view gradient accumulation kernels).
+
+    Per hidden layer the backward is: the fused HIP `dr_tanh_backward`
+    (grad_z = grad_h * (1 - h^2) and the bias gradient in one pass), a
+    split-K weight gradient (batched GEMM over C row chunks, then one sum
+    into the flat-gradient view) and, below the top layer, grad_h = grad_z W.
+    GEMMs are fp32 (hipBLASLt, MFMA).  Numerically this is the same
+    computation autograd performs (checked in tests/test_ppo_gpu.py against
+    the SB3 restatement)."""
+
+    def __init__(self, policy: ActorCritic, m: int, chunks: int = 64):
+        from . import ppo_kernels as K
+        self.K = K
+        self.pol = policy
+        self.m = m
+        self.C = chunks if m % chunks == 0 else 1
+        dev = policy.device
+        wmax = max(policy.net_arch)
+        f32 = dict(dtype=torch.float32, device=dev)
+        self.grad = torch.zeros(policy.num_params, **f32)
+        # flat storage, viewed per layer width so every view is contiguous
+        self._g = torch.empty(m * wmax, **f32)
+        self._gz = torch.empty(m * wmax, **f32)
+        dims = (policy.obs_dim,) + policy.net_arch
+        self._ws = torch.empty(self.C * wmax * max(dims), **f32)
+        self.tanh_ws = torch.empty(
+            max(K.tanh_backward_workspace_bytes(m, n) for n in policy.net_arch) // 4 + 1, **f32)
+
+    def gview(self, name):
+        a, b, shape = self.pol.offsets[name]
+        return self.grad[a:b].view(shape)
+
+    @torch.no_grad()
+    def forward(self, obs):
+        pol = self.pol
+        cache = {}
+        outs = {}
+        for pre, head in (("pi", "action"), ("vf", "value")):
+            x, hs = obs, []
+            for k in range(len(pol.net_arch)):
+                h = torch.addmm(pol.p(f"{pre}{k}.b"), x, pol.p(f"{pre}{k}.w").t())
+                torch.tanh_(h)
+                hs.append(h)
+                x = h
+            outs[head] = torch.addmm(pol.p(f"{head}.b"), x, pol.p(f"{head}.w").t())
+            cache[pre] = hs
+        return outs["action"], outs["value"].squeeze(-1), cache
+
+    def _wgrad(self, g, x, out):
+        """out (N,K) = g^T x over M rows, split into C chunks."""
+        M, N = g.shape
+        Kd = x.shape[1]
+        C = self.C
+        ws = self._ws[:C * N * Kd].view(C, N, Kd)
+        if C == 1:
+            torch.mm(g.t(), x, out=out)
+            return
+        torch.bmm(g.reshape(C, M // C, N).transpose(1, 2), x.reshape(C, M // C, Kd),
+                  out=ws)
+        torch.sum(ws, dim=0, out=out)
+
+    @torch.no_grad()
+    def backward(self, obs, cache, g_mean, g_value, g_log_std):
+        pol = self.pol
+        M = obs.shape[0]
+        for pre, head, gout in (("pi", "action", g_mean), ("vf", "value", g_value.view(M, 1))):
+            hs = cache[pre]
+            self._wgrad(gout, hs[-1], self.gview(f"{head}.w"))
+            torch.sum(gout, dim=0, out=self.gview(f"{head}.b"))
+            n = hs[-1].shape[1]
+            g = self._g[:M * n].view(M, n)
+            torch.mm(gout, pol.p(f"{head}.w"), out=g)
+            for k in reversed(range(len(pol.net_arch))):
+                h = hs[k]
+                n = h.shape[1]
+                gz = self._gz[:M * n].view(M, n)
+                self.K.tanh_backward(g, h, gz, self.gview(f"{pre}{k}.b"), self.tanh_ws)
+                x = hs[k - 1] if k > 0 else obs
+                self._wgrad(gz, x, self.gview(f"{pre}{k}.w"))
+                if k > 0:
+                    g = self._g[:M * x.shape[1]].view(M, x.shape[1])
+                    torch.mm(gz, pol.p(f"{pre}{k}.w"), out=g)
+        self.gview("log_std").copy_(g_log_std)
+        return self.grad

@@ -33,7 +33,7 @@ import torch
 from . import dist as D
 from . import ppo_kernels as K
 from .env import MOTOR_MAX, DroneBatch
-from .policy import ActorCritic
+from .policy import ActorCritic, FusedTrainStep
 
 
 @dataclasses.dataclass
@@ -107,6 +107,7 @@ class PPOTrainer:
         self.mb_aux = torch.zeros(M, 3, **f32)
         self.loss = K.PPOLoss(M, dev, cfg.clip_range, cfg.ent_coef, cfg.vf_coef,
                               cfg.normalize_advantage)
+        self.fused = FusedTrainStep(self.policy, M)
         self.num_updates = 0
         self.num_timesteps = 0
         self._rolled = False
@@ -149,38 +150,37 @@ class PPOTrainer:
                     dim=1, out=self.aux)
         self.num_timesteps += T * cfg.num_envs * self.world
 
+    @torch.no_grad()
     def train(self):
         cfg = self.cfg
         T, N, M = cfg.n_steps, cfg.num_envs, cfg.batch_size
-        flat = self.policy.flat
         obs_flat = self.obs[:T].reshape(T * N, -1)
         act_flat = self.actions.reshape(T * N, 4)
-        a, b, _ = self.policy.offsets["log_std"]
-        stats = []
+        log_std = self.policy.log_std.detach()
+        nmb = T * N // M
+        stats = torch.zeros(cfg.n_epochs * nmb, 8, dtype=torch.float32, device=self.device)
+        j = 0
         for epoch in range(cfg.n_epochs):
             perm = self.perm(seed=cfg.seed * 104729 + self.rank,
                              counter=self.num_updates * cfg.n_epochs + epoch)
-            for k in range(T * N // M):
+            for k in range(nmb):
                 idx = perm[k * M:(k + 1) * M]
                 K.gather_rows(idx, obs_flat, out=self.mb_obs)
                 K.gather_rows(idx, act_flat, out=self.mb_act)
                 K.gather_rows(idx, self.aux, out=self.mb_aux)
-                mean, value = self.policy(self.mb_obs)
+                mean, value, cache = self.fused.forward(self.mb_obs)
                 old_logp = self.mb_aux[:, 0].contiguous()
                 adv = self.mb_aux[:, 1].contiguous()
                 ret = self.mb_aux[:, 2].contiguous()
-                g_mean, g_ls, g_v, st = self.loss(mean.detach().contiguous(),
-                                                  self.policy.log_std.detach().contiguous(),
-                                                  value.detach().contiguous(), self.mb_act,
-                                                  old_logp, adv, ret)
-                flat.grad = None
-                torch.autograd.backward([mean, value], [g_mean, g_v])
-                flat.grad[a:b] += g_ls
-                self._allreduce_grad(flat.grad)
-                self.opt.step(flat.grad)
-                stats.append(st.clone())
+                g_mean, g_ls, g_v, st = self.loss(mean, log_std, value.contiguous(),
+                                                  self.mb_act, old_logp, adv, ret)
+                grad = self.fused.backward(self.mb_obs, cache, g_mean, g_v, g_ls)
+                self._allreduce_grad(grad)
+                self.opt.step(grad)
+                stats[j].copy_(st)
+                j += 1
         self.num_updates += 1
-        return torch.stack(stats).mean(0) if stats else None
+        return stats.mean(0)
 
     def learn_step(self):
         """One PPO iteration: rollout + GAE + n_epochs of minibatch updates."""

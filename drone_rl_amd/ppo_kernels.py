@@ -74,6 +74,22 @@ def gather_rows(idx, src, out=None):
     return o
 
 
+def tanh_backward_workspace_bytes(m: int, n: int) -> int:
+    return int(_lib.lib().dr_tanh_backward_workspace_bytes(m, n))
+
+
+def tanh_backward(grad_h, h, grad_z, bias_grad, workspace):
+    """grad_z = grad_h * (1 - h^2); bias_grad = grad_z.sum(0) (one pass).
+    grad_h / h / grad_z: contiguous (m, n) f32; bias_grad: contiguous (n,)."""
+    m, n = h.shape
+    for t in (grad_h, h, grad_z):
+        assert t.is_contiguous() and t.dtype == torch.float32
+    check(_lib.lib().dr_tanh_backward(m, n, ptr(grad_h), ptr(h), ptr(grad_z), ptr(bias_grad),
+                                      ptr(workspace), workspace.numel() * workspace.element_size(),
+                                      _s(h)))
+    return grad_z
+
+
 class PPOLoss:
     """Fused PPO minibatch loss and its gradient w.r.t. the policy head
     outputs (mean (m,4), log_std (4,), values (m,))."""

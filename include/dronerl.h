@@ -212,6 +212,15 @@ int dr_permutation(int64_t n, uint64_t seed, uint64_t counter, int32_t *out,
 int dr_gather_rows(int64_t m, int64_t width, const int32_t *idx,
                    const float *src, float *dst, void *stream);
 
+/* Tanh-layer backward fused with the bias gradient (the MLP backward of
+   PPO.train): grad_z = grad_h * (1 - h^2) for an (m, n) activation h =
+   tanh(z), and bias_grad[j] = sum_i grad_z[i, j].  n must be a multiple of
+   4 and <= 1024.  `workspace` >= dr_tanh_backward_workspace_bytes(m, n). */
+size_t dr_tanh_backward_workspace_bytes(int64_t m, int64_t n);
+int dr_tanh_backward(int64_t m, int64_t n, const float *grad_h, const float *h,
+                     float *grad_z, float *bias_grad, void *workspace,
+                     size_t workspace_bytes, void *stream);
+
 /* Fused PPO loss + gradient of the loss w.r.t. the policy head outputs
    (PPO.train: normalised advantage, ratio/clip surrogate, value MSE,
    entropy).  Inputs for a minibatch of m rows:
