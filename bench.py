@@ -32,6 +32,8 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 BYTES_PER_ENV_STEP = {"f64": 305, "f32": 197}
+# moving-target variant: + 9 f32 motion params read, + 3 f32 obs written
+BYTES_PER_ENV_STEP_MOVING = {"f64": 353, "f32": 245}
 HBM_PEAK_GBS = 8000.0      # MI355X HBM3E spec (MI355X_MICROARCH.md)
 
 
@@ -67,13 +69,13 @@ def cpu_baseline(seconds):
                        f"SubprocVecEnv-equivalent without pipe IPC; CPU: {cpu_model()}")}
 
 
-def time_env(args, dtype_name, n_envs, rank, world, device, steps, warmup):
+def time_env(args, dtype_name, n_envs, rank, world, device, steps, warmup, variant="gym"):
     import torch
     import torch.distributed as dist
 
     from drone_rl_amd import DroneBatch, random_actions
     dtype = torch.float64 if dtype_name == "f64" else torch.float32
-    b = DroneBatch(n_envs, "gym", dtype=dtype, device=device, seed=2025,
+    b = DroneBatch(n_envs, variant, dtype=dtype, device=device, seed=2025,
                    env_id_offset=rank * n_envs, auto_reset=True)
     b.reset()
     total = warmup + steps
@@ -240,6 +242,16 @@ def main():
                     "env_steps_per_s": round(n * k / el, 1),
                     "avg_launch_us": round(pl * 1e6, 3),
                     "achieved_GBs": round(n * BYTES_PER_ENV_STEP[dn] / pl / 1e9, 1)}
+        os.environ["DRONERL_STEP_KERNEL"] = "lane"
+        # configs[4]: the moving-target curriculum, 1M envs over 8 GPUs
+        for dn, n in (("f64", 1 << 17), ("f64", 1 << 20)):
+            k = 200 if n > N else args.steps
+            el, gm, _ = time_env(args, dn, n, 0, 1, device, k, 20, variant="moving")
+            pl = gm / 1e3 / k
+            ex[f"moving_{dn}_{n}"] = {
+                "env_steps_per_s": round(n * k / el, 1),
+                "avg_launch_us": round(pl * 1e6, 3),
+                "achieved_GBs": round(n * BYTES_PER_ENV_STEP_MOVING[dn] / pl / 1e9, 1)}
         if saved is None:
             os.environ.pop("DRONERL_STEP_KERNEL", None)
         else:

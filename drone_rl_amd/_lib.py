@@ -25,6 +25,7 @@ DR_ERR_UNSUPPORTED = -4
 
 DR_VARIANT_GYM = 0
 DR_VARIANT_VECTORIZED = 1
+DR_VARIANT_MOVING = 2
 DR_STATE_F64 = 0
 DR_STATE_F32 = 1
 DR_RNG_PHILOX = 0
@@ -32,7 +33,7 @@ DR_RNG_HOST_UNIFORMS = 1
 
 FIELDS = {"pos": 0, "vel": 1, "euler": 2, "omega": 3, "target": 4,
           "current_step": 5, "ep_num": 6, "eps": 7, "ep_return": 8,
-          "ep_length": 9}
+          "ep_length": 9, "motion": 10}
 
 
 class dr_config(ctypes.Structure):

@@ -119,6 +119,7 @@ struct EnvView {
     double *eps;
     float *ep_ret;
     int32_t *ep_len;
+    float *mot;       // moving variant: 9 f32 arrays (a xyz, w xyz, ph xyz)
     int64_t n;
     int64_t env_id_offset;
     const double *host_u;  // DR_RNG_HOST_UNIFORMS buffer, else nullptr
@@ -142,29 +143,33 @@ struct StepIO {
 // The five reset draws of env i starting episode `ep_new`, in the reference
 // order: pos x, pos y, target x, y, z (drone.py:57,73).  mode: 0 Philox,
 // 1 host buffer, 2 constant 0.5 (constructor reset in host-uniform mode).
-template <typename S>
+// NU = 5 (gym) or 14 (moving: the 5 gym draws, then 9 motion draws; the
+// first 5 are the gym variant's, so eps = 0 reproduces it exactly).
+template <int NU, typename S>
 __device__ inline void reset_uniforms(const EnvView<S> &v, int64_t i,
-                                      int32_t ep_new, int mode, double u[5]) {
+                                      int32_t ep_new, int mode, double u[NU]) {
     if (mode == 1) {
 #pragma unroll
-        for (int k = 0; k < 5; ++k) u[k] = v.host_u[i * 5 + k];
+        for (int k = 0; k < NU; ++k) u[k] = v.host_u[i * NU + k];
         return;
     }
     if (mode == 2 || DR_ABLATE == 5) {
 #pragma unroll
-        for (int k = 0; k < 5; ++k) u[k] = 0.5;
+        for (int k = 0; k < NU; ++k) u[k] = 0.5;
         return;
     }
     const uint64_t gid = (uint64_t)(v.env_id_offset + i);
-    u32x4 c{(uint32_t)ep_new, (uint32_t)gid, (uint32_t)(gid >> 32), TAG_RESET};
-    const u32x4 r0 = philox4x32_10(c, v.seed_lo, v.seed_hi);
-    c.w = TAG_RESET | 1u;
-    const u32x4 r1 = philox4x32_10(c, v.seed_lo, v.seed_hi);
-    u[0] = u01_w32(r0.x);
-    u[1] = u01_w32(r0.y);
-    u[2] = u01_w32(r0.z);
-    u[3] = u01_w32(r0.w);
-    u[4] = u01_w32(r1.x);
+#pragma unroll
+    for (int b = 0; b < (NU + 3) / 4; ++b) {
+        const u32x4 r = philox4x32_10(
+            u32x4{(uint32_t)ep_new, (uint32_t)gid, (uint32_t)(gid >> 32),
+                  TAG_RESET | (uint32_t)b},
+            v.seed_lo, v.seed_hi);
+        const uint32_t w[4] = {r.x, r.y, r.z, r.w};
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            if (4 * b + k < NU) u[4 * b + k] = u01_w32(w[k]);
+    }
 }
 
 // DroneEnv.reset (drone.py:48-75) on registers st[F_N]; updates ep_num/eps
@@ -174,7 +179,7 @@ __device__ inline void gym_reset_regs(const EnvView<S> &v, int64_t i, int mode,
                                       S st[F_N], int32_t ep_old, double eps) {
     const int32_t ep_new = ep_old + 1;        // ep_num += 1          (61)
     double u[5];
-    reset_uniforms(v, i, ep_new, mode, u);
+    reset_uniforms<5>(v, i, ep_new, mode, u);
     DR_STAMP(6);
     if (!DR_PREFETCH_EPS) eps = v.eps[i];
     if (ep_new % 2000 == 0) {                 // curriculum bump      (68-70)
@@ -206,14 +211,67 @@ __device__ inline void vec_reset_regs(S st[F_N]) {
     st[F_TGT + 2] = (S)10.0;
 }
 
+// ---- moving-target variant (DR_VARIANT_MOVING) ----
+// target_k(s) = c_k + a_k sin(w_k s dt + ph_k), velocity a_k w_k cos(...),
+// evaluated in f32 (the motion is this build's spec, not the reference's).
+template <typename S>
+__device__ inline void moving_target(const S c[3], const float mp[9], int32_t s,
+                                     float dt, S tgt[3], float tvel[3]) {
+    const float t = (float)s * dt;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        float sn, cs;
+        sincosf(mp[3 + k] * t + mp[6 + k], &sn, &cs);
+        tgt[k] = c[k] + (S)(mp[k] * sn);
+        tvel[k] = mp[k] * mp[3 + k] * cs;
+    }
+}
+
+// DroneEnv.reset plus the motion draws: pos / zeroed rates / centre exactly
+// as gym_reset_regs (centre = the gym target), a = eps * U, w = 0.5 + 1.5 U
+// rad/s, ph = 2 pi U.
+template <typename S>
+__device__ inline void moving_reset_regs(const EnvView<S> &v, int64_t i, int mode,
+                                         S st[F_N], S c[3], float mp[9],
+                                         int32_t ep_old, double eps) {
+    const int32_t ep_new = ep_old + 1;
+    double u[14];
+    reset_uniforms<14>(v, i, ep_new, mode, u);
+    if (!DR_PREFETCH_EPS) eps = v.eps[i];
+    if (ep_new % 2000 == 0) {
+        eps += 0.1;
+        v.eps[i] = eps;
+    }
+    v.ep_num[i] = ep_new;
+    st[F_POS + 0] = (S)(u[0] - 0.5);
+    st[F_POS + 1] = (S)(u[1] - 0.5);
+    st[F_POS + 2] = (S)1.0;
+#pragma unroll
+    for (int k = 3; k < 12; ++k) st[k] = (S)0;
+    c[0] = (S)(eps * u[2]);
+    c[1] = (S)(eps * u[3]);
+    c[2] = (S)(eps * u[4] + 1.0 + 0.0);
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        mp[k] = (float)(eps * u[5 + k]);
+        mp[3 + k] = (float)(0.5 + 1.5 * u[8 + k]);
+        mp[6 + k] = (float)(6.283185307179586 * u[11 + k]);
+    }
+}
+
 template <typename S, int OD>
-__device__ inline void make_obs(const S st[F_N], float ob[OD]) {
+__device__ inline void make_obs(const S st[F_N], float ob[OD],
+                                const float *tvel = nullptr) {
     // _get_obs: f32(concat(pos, vel, euler, omega[, target - pos]))  (79)
 #pragma unroll
     for (int k = 0; k < 12; ++k) ob[k] = (float)st[k];
-    if constexpr (OD == 15) {
+    if constexpr (OD >= 15) {
 #pragma unroll
         for (int k = 0; k < 3; ++k) ob[12 + k] = (float)(st[F_TGT + k] - st[F_POS + k]);
+    }
+    if constexpr (OD == 18) {
+#pragma unroll
+        for (int k = 0; k < 3; ++k) ob[15 + k] = tvel[k];
     }
 }
 
@@ -259,7 +317,7 @@ __device__ inline S physics_step(S st[F_N], float4 act, S dt, bool &crash) {
     const S sec = (S)1 / cth;        // the only IEEE divide; also vd:116
     const S tth = div_rcp(sth, cth, sec);
     S ed2;
-    if constexpr (VAR == DR_VARIANT_GYM) {
+    if constexpr (VAR != DR_VARIANT_VECTORIZED) {
         ed2 = ((S)0 * w0 + div_rcp(sph, cth, sec) * w1) +
               div_rcp(cph, cth, sec) * w2;                             // (184)
     } else {
@@ -291,7 +349,7 @@ __device__ inline S physics_step(S st[F_N], float4 act, S dt, bool &crash) {
     const S dz = st[F_POS + 2] - st[F_TGT + 2];
     const S d = m_sqrt((dx * dx + dy * dy) + dz * dz);
     S r;
-    if constexpr (VAR == DR_VARIANT_GYM) {
+    if constexpr (VAR != DR_VARIANT_VECTORIZED) {
         r = (S)0.01 * -d;
         if (d < (S)0.05) r += (S)1;
     } else {
@@ -356,7 +414,8 @@ __device__ inline void store_obs_block(float *sh, const float ob[OD],
 template <typename S, int VAR, bool MON>
 __global__ __launch_bounds__(kBlock) void env_step_kernel(EnvView<S> v,
                                                           StepIO io) {
-    constexpr int OD = (VAR == DR_VARIANT_GYM) ? 15 : 12;
+    constexpr int OD = VAR == DR_VARIANT_GYM ? 15 : (VAR == DR_VARIANT_MOVING ? 18 : 12);
+    constexpr bool GYMLIKE = VAR != DR_VARIANT_VECTORIZED;
     __shared__ float4 sh4[kBlock * OD / 4];
     const int64_t base = (int64_t)blockIdx.x * kBlock;
     const int64_t i = base + threadIdx.x;
@@ -372,21 +431,32 @@ __global__ __launch_bounds__(kBlock) void env_step_kernel(EnvView<S> v,
         const float4 act = reinterpret_cast<const float4 *>(io.actions)[i];
 #pragma unroll
         for (int k = 0; k < F_EUL; ++k) st[k] = v.field(k)[i];
+        S cen[3];
+        float mp[9], tvel[3];
         if constexpr (VAR == DR_VARIANT_GYM) {
 #pragma unroll
             for (int k = F_TGT; k < F_N; ++k) st[k] = v.field(k)[i];
+        } else if constexpr (VAR == DR_VARIANT_MOVING) {
+#pragma unroll
+            for (int k = 0; k < 3; ++k) cen[k] = v.field(F_TGT + k)[i];
+#pragma unroll
+            for (int k = 0; k < 9; ++k) mp[k] = v.mot[k * v.stride + i];
         } else {
             st[F_TGT + 0] = (S)0;
             st[F_TGT + 1] = (S)0;
             st[F_TGT + 2] = (S)10.0;
         }
         int32_t step = v.step[i];
+        if constexpr (VAR == DR_VARIANT_MOVING) {
+            // the reward and obs of this step see the target at the NEW step
+            moving_target(cen, mp, step + 1, (float)v.dt, &st[F_TGT], tvel);
+        }
         // needed only if this env resets; loaded up front so a reset does
         // not stall the wave on a dependent global load (+12 B per step,
         // counted in the measured traffic, not in the 305 B algorithmic)
         int32_t ep_old = 0;
         double eps_old = 0.0;
-        if constexpr (VAR == DR_VARIANT_GYM) {
+        if constexpr (GYMLIKE) {
             ep_old = v.ep_num[i];
             if (DR_PREFETCH_EPS) eps_old = v.eps[i];
         }
@@ -399,7 +469,7 @@ __global__ __launch_bounds__(kBlock) void env_step_kernel(EnvView<S> v,
         const float rf = (float)r;                         // SB3 f32 buffer
         io.rew[i] = rf;
         io.done[i] = (uint8_t)done;
-        make_obs<S, OD>(st, ob);
+        make_obs<S, OD>(st, ob, tvel);
 
         float ret = 0.f;
         int32_t len = 0;
@@ -407,18 +477,27 @@ __global__ __launch_bounds__(kBlock) void env_step_kernel(EnvView<S> v,
             ret = v.ep_ret[i] + rf;                        // VecMonitor
             len = v.ep_len[i] + 1;
         }
-        if constexpr (VAR == DR_VARIANT_GYM) {
+        if constexpr (GYMLIKE) {
             if (done && io.auto_reset && DR_ABLATE != 2) {
                 // DummyVecEnv: keep the terminal obs, reset in the same step.
                 if (io.term_obs) {
 #pragma unroll
                     for (int k = 0; k < OD; ++k) io.term_obs[i * OD + k] = ob[k];
                 }
-                gym_reset_regs(v, i, v.host_u ? 1 : 0, st, ep_old, eps_old);
                 step = 0;
+                if constexpr (VAR == DR_VARIANT_GYM) {
+                    gym_reset_regs(v, i, v.host_u ? 1 : 0, st, ep_old, eps_old);
 #pragma unroll
-                for (int k = F_TGT; k < F_N; ++k) v.field(k)[i] = st[k];
-                make_obs<S, OD>(st, ob);
+                    for (int k = F_TGT; k < F_N; ++k) v.field(k)[i] = st[k];
+                } else {
+                    moving_reset_regs(v, i, v.host_u ? 1 : 0, st, cen, mp, ep_old, eps_old);
+#pragma unroll
+                    for (int k = 0; k < 3; ++k) v.field(F_TGT + k)[i] = cen[k];
+#pragma unroll
+                    for (int k = 0; k < 9; ++k) v.mot[k * v.stride + i] = mp[k];
+                    moving_target(cen, mp, 0, (float)v.dt, &st[F_TGT], tvel);
+                }
+                make_obs<S, OD>(st, ob, tvel);
             }
         }
         if constexpr (MON) {
@@ -692,7 +771,7 @@ __global__ __launch_bounds__(kBlock) void env_reset_kernel(EnvView<S> v,
                                                            const uint8_t *mask,
                                                            float *obs, int mode,
                                                            int init) {
-    constexpr int OD = (VAR == DR_VARIANT_GYM) ? 15 : 12;
+    constexpr int OD = VAR == DR_VARIANT_GYM ? 15 : (VAR == DR_VARIANT_MOVING ? 18 : 12);
     __shared__ float4 sh4[kBlock * OD / 4];
     const int64_t base = (int64_t)blockIdx.x * kBlock;
     const int64_t i = base + threadIdx.x;
@@ -705,10 +784,16 @@ __global__ __launch_bounds__(kBlock) void env_reset_kernel(EnvView<S> v,
             v.ep_len[i] = 0;
         }
         S st[F_N];
+        float tvel[3] = {0.f, 0.f, 0.f};
         const bool doit = (mask == nullptr) || mask[i];
         if (doit) {
             if constexpr (VAR == DR_VARIANT_GYM) {
                 gym_reset_regs(v, i, mode, st, v.ep_num[i], v.eps[i]);
+            } else if constexpr (VAR == DR_VARIANT_MOVING) {
+                float mp[9];
+                moving_reset_regs(v, i, mode, st, &st[F_TGT], mp, v.ep_num[i], v.eps[i]);
+#pragma unroll
+                for (int k = 0; k < 9; ++k) v.mot[k * v.stride + i] = mp[k];
             } else {
                 vec_reset_regs(st);
             }
@@ -719,7 +804,15 @@ __global__ __launch_bounds__(kBlock) void env_reset_kernel(EnvView<S> v,
 #pragma unroll
             for (int k = 0; k < F_N; ++k) st[k] = v.field(k)[i];
         }
-        make_obs<S, OD>(st, ob);
+        if constexpr (VAR == DR_VARIANT_MOVING) {
+            // stored target = the centre; the obs sees the target at `step`
+            S cen[3] = {st[F_TGT], st[F_TGT + 1], st[F_TGT + 2]};
+            float mp[9];
+#pragma unroll
+            for (int k = 0; k < 9; ++k) mp[k] = v.mot[k * v.stride + i];
+            moving_target(cen, mp, v.step[i], (float)v.dt, &st[F_TGT], tvel);
+        }
+        make_obs<S, OD>(st, ob, tvel);
     } else {
 #pragma unroll
         for (int k = 0; k < OD; ++k) ob[k] = 0.f;
@@ -745,6 +838,9 @@ __global__ void get_field_kernel(EnvView<S> v, int field, void *out) {
         static_cast<float *>(out)[i] = v.ep_ret[i];
     } else if (field == DR_FIELD_EP_LENGTH) {
         static_cast<int32_t *>(out)[i] = v.ep_len[i];
+    } else if (field == DR_FIELD_MOTION) {
+#pragma unroll
+        for (int k = 0; k < 9; ++k) static_cast<float *>(out)[i * 9 + k] = v.mot[k * v.stride + i];
     }
 }
 
@@ -766,6 +862,9 @@ __global__ void set_field_kernel(EnvView<S> v, int field, const void *in) {
         v.ep_ret[i] = static_cast<const float *>(in)[i];
     } else if (field == DR_FIELD_EP_LENGTH) {
         v.ep_len[i] = static_cast<const int32_t *>(in)[i];
+    } else if (field == DR_FIELD_MOTION) {
+#pragma unroll
+        for (int k = 0; k < 9; ++k) v.mot[k * v.stride + i] = static_cast<const float *>(in)[i * 9 + k];
     }
 }
 
@@ -835,6 +934,8 @@ EnvView<S> view_of(const dr_handle *h) {
     v.ep_ret = reinterpret_cast<float *>(m);
     m += sp * sizeof(float);
     v.ep_len = reinterpret_cast<int32_t *>(m);
+    m += sp * sizeof(int32_t);
+    v.mot = h->cfg.variant == DR_VARIANT_MOVING ? reinterpret_cast<float *>(m) : nullptr;
     v.n = h->n;
     v.env_id_offset = h->cfg.env_id_offset;
     v.host_u = h->host_u;
@@ -845,9 +946,10 @@ EnvView<S> view_of(const dr_handle *h) {
     return v;
 }
 
-size_t state_bytes(int64_t stride, int dtype) {
+size_t state_bytes(int64_t stride, int dtype, int variant) {
     const size_t s = dtype == DR_STATE_F64 ? sizeof(double) : sizeof(float);
-    return (size_t)F_N * stride * s + (size_t)stride * (8 + 4 + 4 + 4 + 4);
+    const size_t mot = variant == DR_VARIANT_MOVING ? 9 * sizeof(float) : 0;
+    return (size_t)F_N * stride * s + (size_t)stride * (8 + 4 + 4 + 4 + 4 + mot);
 }
 
 inline hipStream_t as_stream(void *s) { return static_cast<hipStream_t>(s); }
@@ -870,6 +972,9 @@ int dispatch_reset(dr_handle *h, const uint8_t *mask, float *obs, int mode,
     if (h->cfg.variant == DR_VARIANT_GYM)
         return f64 ? launch_reset<double, DR_VARIANT_GYM>(h, mask, obs, mode, init, st)
                    : launch_reset<float, DR_VARIANT_GYM>(h, mask, obs, mode, init, st);
+    if (h->cfg.variant == DR_VARIANT_MOVING)
+        return f64 ? launch_reset<double, DR_VARIANT_MOVING>(h, mask, obs, mode, init, st)
+                   : launch_reset<float, DR_VARIANT_MOVING>(h, mask, obs, mode, init, st);
     return f64 ? launch_reset<double, DR_VARIANT_VECTORIZED>(h, mask, obs, mode, init, st)
                : launch_reset<float, DR_VARIANT_VECTORIZED>(h, mask, obs, mode, init, st);
 }
@@ -877,10 +982,15 @@ int dispatch_reset(dr_handle *h, const uint8_t *mask, float *obs, int mode,
 template <typename S, int VAR, bool MON>
 int launch_step(dr_handle *h, const StepIO &io, hipStream_t st) {
     EnvView<S> v = view_of<S>(h);
-    if (h->quad)
-        hipLaunchKernelGGL((env_step_quad_kernel<S, VAR, MON>),
-                           dim3(grid_for(h->n, kBlock / 4)), dim3(kBlock), 0, st, v, io);
-    else
+    bool launched = false;
+    if constexpr (VAR != DR_VARIANT_MOVING) {  // the quad A/B kernel has no moving form
+        if (h->quad) {
+            hipLaunchKernelGGL((env_step_quad_kernel<S, VAR, MON>),
+                               dim3(grid_for(h->n, kBlock / 4)), dim3(kBlock), 0, st, v, io);
+            launched = true;
+        }
+    }
+    if (!launched)
         hipLaunchKernelGGL((env_step_kernel<S, VAR, MON>), dim3(grid_for(h->n)),
                            dim3(kBlock), 0, st, v, io);
     hipError_t e = hipGetLastError();
@@ -895,13 +1005,16 @@ int dispatch_step(dr_handle *h, const StepIO &io, hipStream_t st) {
     if (h->cfg.variant == DR_VARIANT_GYM)
         return f64 ? launch_step<double, DR_VARIANT_GYM, MON>(h, io, st)
                    : launch_step<float, DR_VARIANT_GYM, MON>(h, io, st);
+    if (h->cfg.variant == DR_VARIANT_MOVING)
+        return f64 ? launch_step<double, DR_VARIANT_MOVING, MON>(h, io, st)
+                   : launch_step<float, DR_VARIANT_MOVING, MON>(h, io, st);
     return f64 ? launch_step<double, DR_VARIANT_VECTORIZED, MON>(h, io, st)
                : launch_step<float, DR_VARIANT_VECTORIZED, MON>(h, io, st);
 }
 
 int check_rng(dr_handle *h) {
     if (h->cfg.rng_mode == DR_RNG_HOST_UNIFORMS && h->host_u == nullptr &&
-        h->cfg.variant == DR_VARIANT_GYM)
+        h->cfg.variant != DR_VARIANT_VECTORIZED)
         return fail(h, DR_ERR_INVALID,
                     "rng_mode DR_RNG_HOST_UNIFORMS: call dr_set_reset_uniforms first");
     return DR_OK;
@@ -918,7 +1031,8 @@ int dr_create(const dr_config *cfg_in, dr_handle **out) {
     *out = nullptr;
     dr_config cfg = *cfg_in;
     if (cfg.num_envs < 1) return fail(nullptr, DR_ERR_INVALID, "dr_create: num_envs must be >= 1");
-    if (cfg.variant != DR_VARIANT_GYM && cfg.variant != DR_VARIANT_VECTORIZED)
+    if (cfg.variant != DR_VARIANT_GYM && cfg.variant != DR_VARIANT_VECTORIZED &&
+        cfg.variant != DR_VARIANT_MOVING)
         return fail(nullptr, DR_ERR_INVALID, "dr_create: unknown variant");
     if (cfg.state_dtype != DR_STATE_F64 && cfg.state_dtype != DR_STATE_F32)
         return fail(nullptr, DR_ERR_INVALID, "dr_create: unknown state_dtype");
@@ -926,7 +1040,7 @@ int dr_create(const dr_config *cfg_in, dr_handle **out) {
         return fail(nullptr, DR_ERR_INVALID, "dr_create: unknown rng_mode");
     if (cfg.num_envs > (int64_t)1 << 31)
         return fail(nullptr, DR_ERR_INVALID, "dr_create: num_envs above 2^31 per handle");
-    if (cfg.max_steps == 0) cfg.max_steps = cfg.variant == DR_VARIANT_GYM ? 200 : 1000;
+    if (cfg.max_steps == 0) cfg.max_steps = cfg.variant == DR_VARIANT_VECTORIZED ? 1000 : 200;
     if (cfg.max_steps < 0) return fail(nullptr, DR_ERR_INVALID, "dr_create: max_steps < 0");
     if (cfg.dt == 0.0) cfg.dt = kDt;
     if (cfg.variant == DR_VARIANT_VECTORIZED) cfg.auto_reset = 0;
@@ -945,7 +1059,7 @@ int dr_create(const dr_config *cfg_in, dr_handle **out) {
     // would put the 17 concurrently streamed arrays at congruent addresses
     // (same HBM channel bits); DR_STRIDE_PAD elements of skew break that.
     h->stride = (cfg.num_envs + 63) / 64 * 64 + DR_STRIDE_PAD;
-    h->obs_dim = cfg.variant == DR_VARIANT_GYM ? 15 : 12;
+    h->obs_dim = cfg.variant == DR_VARIANT_GYM ? 15 : (cfg.variant == DR_VARIANT_MOVING ? 18 : 12);
     // Step kernel choice: one lane per env unless DRONERL_STEP_KERNEL=quad
     // (4 lanes per env; fewer serial f64 ops per lane, more total VALU work:
     // slower on MI355X at every measured size, kept for A/B measurement).
@@ -953,7 +1067,7 @@ int dr_create(const dr_config *cfg_in, dr_handle **out) {
         h->quad = std::strcmp(kk, "quad") == 0;
 
     DeviceGuard g(cfg.device);
-    const size_t bytes = state_bytes(h->stride, cfg.state_dtype);
+    const size_t bytes = state_bytes(h->stride, cfg.state_dtype, cfg.variant);
     hipError_t e = hipMalloc(&h->mem, bytes);
     if (e != hipSuccess) {
         delete h;
@@ -1003,7 +1117,7 @@ int dr_reset(dr_handle *h, float *obs_out, void *stream) {
 int dr_reset_masked(dr_handle *h, const uint8_t *mask, float *obs_out, void *stream) {
     if (!h) return fail(nullptr, DR_ERR_INVALID, "dr_reset_masked: null handle");
     if (!mask) return fail(h, DR_ERR_INVALID, "dr_reset_masked: mask is null");
-    if (h->cfg.variant != DR_VARIANT_GYM)
+    if (h->cfg.variant == DR_VARIANT_VECTORIZED)
         return fail(h, DR_ERR_UNSUPPORTED, "dr_reset_masked: vectorized variant resets globally");
     int rc = check_rng(h);
     if (rc) return rc;
@@ -1049,8 +1163,10 @@ int dr_step_monitored(dr_handle *h, const float *actions, float *obs_out,
 int dr_get_state(dr_handle *h, int field, void *out, void *stream) {
     if (!h) return fail(nullptr, DR_ERR_INVALID, "dr_get_state: null handle");
     if (!out) return fail(h, DR_ERR_INVALID, "dr_get_state: out is null");
-    if (field < DR_FIELD_POS || field > DR_FIELD_EP_LENGTH)
+    if (field < DR_FIELD_POS || field > DR_FIELD_MOTION)
         return fail(h, DR_ERR_INVALID, "dr_get_state: unknown field");
+    if (field == DR_FIELD_MOTION && h->cfg.variant != DR_VARIANT_MOVING)
+        return fail(h, DR_ERR_INVALID, "dr_get_state: motion exists only for DR_VARIANT_MOVING");
     DeviceGuard g(h->cfg.device);
     if (h->cfg.state_dtype == DR_STATE_F64)
         hipLaunchKernelGGL(get_field_kernel<double>, dim3(grid_for(h->n)), dim3(kBlock), 0,
@@ -1066,8 +1182,10 @@ int dr_get_state(dr_handle *h, int field, void *out, void *stream) {
 int dr_set_state(dr_handle *h, int field, const void *in, void *stream) {
     if (!h) return fail(nullptr, DR_ERR_INVALID, "dr_set_state: null handle");
     if (!in) return fail(h, DR_ERR_INVALID, "dr_set_state: in is null");
-    if (field < DR_FIELD_POS || field > DR_FIELD_EP_LENGTH)
+    if (field < DR_FIELD_POS || field > DR_FIELD_MOTION)
         return fail(h, DR_ERR_INVALID, "dr_set_state: unknown field");
+    if (field == DR_FIELD_MOTION && h->cfg.variant != DR_VARIANT_MOVING)
+        return fail(h, DR_ERR_INVALID, "dr_set_state: motion exists only for DR_VARIANT_MOVING");
     DeviceGuard g(h->cfg.device);
     if (h->cfg.state_dtype == DR_STATE_F64)
         hipLaunchKernelGGL(set_field_kernel<double>, dim3(grid_for(h->n)), dim3(kBlock), 0,

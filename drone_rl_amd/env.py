@@ -25,7 +25,11 @@ ARM_LENGTH = 0.5
 K_YAW = 0.01
 MAX_STEPS = 200
 MOTOR_MAX = 3 * MASS * G / 4.0          # 7.3575, action_space.high
-OBS_DIM = {"gym": 15, "vectorized": 12}
+OBS_DIM = {"gym": 15, "vectorized": 12, "moving": 18}
+# reset uniforms per env and reset for rng="host" 
+RESET_UNIFORMS = {"gym": 5, "vectorized": 5, "moving": 14}
+_VARIANT_ID = {"gym": _lib.DR_VARIANT_GYM, "vectorized": _lib.DR_VARIANT_VECTORIZED,
+               "moving": _lib.DR_VARIANT_MOVING}
 
 _VEC_FIELDS = ("pos", "vel", "euler", "omega", "target")
 
@@ -37,8 +41,9 @@ def _stream(device):
 class DroneBatch:
     """N independent quadrotor envs in HBM (struct of arrays).
 
-    variant    "gym" (DroneGymEnv, drone.py) or "vectorized"
-               (VectorizedDroneEnv, vectorized_drone.py)
+    variant    "gym" (DroneGymEnv, drone.py), "vectorized"
+               (VectorizedDroneEnv, vectorized_drone.py) or "moving" (the
+               moving-target curriculum of BASELINE configs[4]; 18-d obs)
     dtype      torch.float64 (reference precision) or torch.float32 state
     rng        "philox" (counter-based, seeded) or "host" (caller supplies
                the reset uniforms: numpy-MT19937 replay for parity tests)
@@ -68,13 +73,13 @@ class DroneBatch:
         self.variant = variant
         self.dtype = dtype
         self.obs_dim = OBS_DIM[variant]
-        self.auto_reset = bool(auto_reset) and variant == "gym"
+        self.auto_reset = bool(auto_reset) and variant != "vectorized"
         self.monitor = monitor
         self.seed_value = int(seed)
         self.env_id_offset = int(env_id_offset)
         cfg = _lib.dr_config(
             num_envs=self.num_envs,
-            variant=_lib.DR_VARIANT_GYM if variant == "gym" else _lib.DR_VARIANT_VECTORIZED,
+            variant=_VARIANT_ID[variant],
             state_dtype=_lib.DR_STATE_F64 if dtype == torch.float64 else _lib.DR_STATE_F32,
             rng_mode=_lib.DR_RNG_PHILOX if rng == "philox" else _lib.DR_RNG_HOST_UNIFORMS,
             auto_reset=int(self.auto_reset), device=self.device.index,
@@ -83,7 +88,7 @@ class DroneBatch:
         h = ctypes.c_void_p()
         check(self.L.dr_create(ctypes.byref(cfg), ctypes.byref(h)))
         self.handle = h
-        self.max_steps = int(max_steps or (MAX_STEPS if variant == "gym" else 1000))
+        self.max_steps = int(max_steps or (1000 if variant == "vectorized" else MAX_STEPS))
         n, od, dev = self.num_envs, self.obs_dim, self.device
         self.obs = torch.zeros(n, od, dtype=torch.float32, device=dev)
         self.rew = torch.zeros(n, dtype=torch.float32, device=dev)
@@ -156,6 +161,8 @@ class DroneBatch:
             out = torch.empty(n, dtype=torch.float64, device=self.device)
         elif field == "ep_return":
             out = torch.empty(n, dtype=torch.float32, device=self.device)
+        elif field == "motion":
+            out = torch.empty(n, 9, dtype=torch.float32, device=self.device)
         else:
             out = torch.empty(n, dtype=torch.int32, device=self.device)
         check(self.L.dr_get_state(self.handle, fid, ptr(out), _stream(self.device)), self.handle)
@@ -169,6 +176,8 @@ class DroneBatch:
             dt, shape = torch.float64, (self.num_envs,)
         elif field == "ep_return":
             dt, shape = torch.float32, (self.num_envs,)
+        elif field == "motion":
+            dt, shape = torch.float32, (self.num_envs, 9)
         else:
             dt, shape = torch.int32, (self.num_envs,)
         v = torch.as_tensor(value, dtype=dt).to(self.device).reshape(shape).contiguous()
@@ -181,9 +190,10 @@ class DroneBatch:
         check(self.L.dr_set_seed(self.handle, self.seed_value & (2**64 - 1)), self.handle)
 
     def set_reset_uniforms(self, u) -> None:
-        """rng='host': (N,5) f64 uniforms consumed by the next resets."""
+        """rng='host': (N,5) f64 uniforms ((N,14) for "moving") consumed by
+        the next resets."""
         t = torch.as_tensor(u, dtype=torch.float64).to(self.device).reshape(
-            self.num_envs, 5).contiguous()
+            self.num_envs, RESET_UNIFORMS[self.variant]).contiguous()
         self._uniforms = t          # keep alive while kernels may read it
         check(self.L.dr_set_reset_uniforms(self.handle, ptr(t)), self.handle)
 

@@ -215,6 +215,9 @@ class PPOTrainer:
     _ENV_FIELDS = ("pos", "vel", "euler", "omega", "target", "current_step", "ep_num", "eps",
                    "ep_return", "ep_length")
 
+    def _env_fields(self):
+        return self._ENV_FIELDS + (("motion",) if self.cfg.variant == "moving" else ())
+
     def state_dict(self):
         """Everything needed to resume bit-for-bit on the same device count:
         parameters (SB3 names too), Adam moments and step, the env state
@@ -228,7 +231,7 @@ class PPOTrainer:
             "policy": self.policy.state_dict(),
             "adam": {"exp_avg": self.opt.m.cpu().clone(), "exp_avg_sq": self.opt.v.cpu().clone(),
                      "step": self.opt.t},
-            "env": {k: self.env.get(k).cpu() for k in self._ENV_FIELDS},
+            "env": {k: self.env.get(k).cpu() for k in self._env_fields()},
             "last_obs": self.obs[T if self._rolled else 0].cpu().clone(),
             "last_dones": self.dones[T].cpu().clone(),
             "num_updates": self.num_updates, "num_timesteps": self.num_timesteps,

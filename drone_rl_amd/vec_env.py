@@ -46,7 +46,7 @@ class BatchedDroneVecEnv(_VecEnvBase):
         if seed is None:
             seed = int(np.random.randint(0, 2**31 - 1))
         self.batch = DroneBatch(num_envs, variant, dtype=dtype, device=device, seed=seed,
-                                auto_reset=(variant == "gym"), rng=rng,
+                                auto_reset=(variant != "vectorized"), rng=rng,
                                 env_id_offset=env_id_offset, keep_terminal_obs=True,
                                 monitor=True)
         self._monitor = monitor
@@ -84,7 +84,7 @@ class BatchedDroneVecEnv(_VecEnvBase):
         idx = np.nonzero(done_np)[0]
         if len(idx):
             it = torch.as_tensor(idx, device=self.batch.device)
-            if self.batch.variant == "gym":
+            if self.batch.auto_reset:
                 term = self.batch.term_obs[it].cpu().numpy()
             else:
                 term = obs_np[idx]
@@ -93,7 +93,7 @@ class BatchedDroneVecEnv(_VecEnvBase):
                 ln = self.batch.ep_len[it].cpu().numpy()
                 t = round(time.time() - self._t_start, 6)
             for j, i in enumerate(idx):
-                if self.batch.variant == "gym":
+                if self.batch.auto_reset:
                     infos[i]["terminal_observation"] = term[j]
                 if self._monitor:
                     infos[i]["episode"] = {"r": np.float32(ret[j]), "l": int(ln[j]), "t": t}

@@ -47,7 +47,14 @@ enum dr_status {
 
 enum dr_variant {
     DR_VARIANT_GYM = 0,        /* DroneGymEnv, drone.py:13-274             */
-    DR_VARIANT_VECTORIZED = 1  /* VectorizedDroneEnv, vectorized_drone.py  */
+    DR_VARIANT_VECTORIZED = 1, /* VectorizedDroneEnv, vectorized_drone.py  */
+    /* Moving-target trajectory tracking (BASELINE.json configs[4]; an
+       extension with no reference oracle, spec in DESIGN.md section 11):
+       gym physics, reset and curriculum; the target moves per axis k as
+       c_k + a_k sin(w_k t + ph_k) with per-episode (a, w, ph), a = eps * U,
+       so eps = 0 reproduces DR_VARIANT_GYM exactly; obs (N,18) = gym obs +
+       target velocity; reward = the gym reward against the moving target. */
+    DR_VARIANT_MOVING = 2
 };
 
 enum dr_state_dtype {
@@ -78,7 +85,9 @@ enum dr_field {   /* dr_get_state / dr_set_state, all device buffers      */
     DR_FIELD_EP_NUM = 6,    /* (N,)  i32  ep_num (drone.py:18,61)            */
     DR_FIELD_EPS = 7,       /* (N,)  f64  curriculum eps (drone.py:33,70)    */
     DR_FIELD_EP_RETURN = 8, /* (N,)  f32  running episode return (monitor)   */
-    DR_FIELD_EP_LENGTH = 9  /* (N,)  i32  running episode length (monitor)   */
+    DR_FIELD_EP_LENGTH = 9, /* (N,)  i32  running episode length (monitor)   */
+    DR_FIELD_MOTION = 10    /* (N,9) f32  moving variant: a xyz, w xyz, ph xyz
+                               (DR_FIELD_TARGET is then the motion centre)  */
 };
 
 typedef struct dr_config {
@@ -114,7 +123,7 @@ int dr_create(const dr_config *cfg, dr_handle **out);
 int dr_destroy(dr_handle *h);
 
 int64_t dr_num_envs(const dr_handle *h);
-int dr_obs_dim(const dr_handle *h);   /* 15 gym, 12 vectorized */
+int dr_obs_dim(const dr_handle *h);   /* 15 gym, 12 vectorized, 18 moving */
 
 /* Reset every env and write (N,obs_dim) obs.  Replaces DroneEnv.reset
    (drone.py:48-75) called on each env by VecEnv.reset, and
@@ -155,7 +164,8 @@ int dr_step_monitored(dr_handle *h, const float *actions, float *obs_out,
 int dr_get_state(dr_handle *h, int field, void *out, void *stream);
 int dr_set_state(dr_handle *h, int field, const void *in, void *stream);
 
-/* DR_RNG_HOST_UNIFORMS: device pointer to (N,5) f64 read by every later
+/* DR_RNG_HOST_UNIFORMS: device pointer to (N,5) f64 ((N,14) for the moving
+   variant: the 5 gym draws, then a xyz, w xyz, ph xyz) read by every later
    reset until replaced.  The buffer must stay alive while work using it is
    in flight. */
 int dr_set_reset_uniforms(dr_handle *h, const double *u_dev);

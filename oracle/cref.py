@@ -61,6 +61,41 @@ def gym_reset(state, u):
     return obs
 
 
+def moving_step(state, action):
+    """One step of the moving-target variant (drone_ref.c oracle_moving_step).
+    state: gym_step's dict with "target" = the reset centre (n,3) f64 and
+    "motion" (n,9) f32; mutated in place.  Returns obs (n,18), reward, done."""
+    n = len(action)
+    action = np.ascontiguousarray(action, np.float32)
+    for k in ("pos", "vel", "euler", "omega"):
+        assert state[k].dtype == np.float64 and state[k].flags.c_contiguous
+    state["step"] = np.ascontiguousarray(state["step"], np.int32)
+    cen = np.ascontiguousarray(state["target"], np.float64)
+    mot = np.ascontiguousarray(state["motion"], np.float32)
+    obs = np.zeros((n, 18), np.float32)
+    rew = np.zeros(n)
+    done = np.zeros(n, np.uint8)
+    lib().oracle_moving_step(ctypes.c_int64(n), _p(state["pos"]), _p(state["vel"]),
+                             _p(state["euler"]), _p(state["omega"]), _p(cen), _p(mot),
+                             _p(state["step"]), _p(action), _p(obs), _p(rew), _p(done))
+    return obs, rew, done.astype(bool)
+
+
+def moving_reset(state, u):
+    """Moving-variant reset given (n,14) uniforms; fills state["motion"]."""
+    n = len(u)
+    u = np.ascontiguousarray(u, np.float64)
+    state["ep_num"] = np.ascontiguousarray(state["ep_num"], np.int64)
+    state["step"] = np.ascontiguousarray(state["step"], np.int32)
+    state["motion"] = np.zeros((n, 9), np.float32)
+    obs = np.zeros((n, 18), np.float32)
+    lib().oracle_moving_reset(ctypes.c_int64(n), _p(state["pos"]), _p(state["vel"]),
+                              _p(state["euler"]), _p(state["omega"]), _p(state["target"]),
+                              _p(state["motion"]), _p(state["step"]), _p(state["ep_num"]),
+                              _p(state["eps"]), _p(u), _p(obs))
+    return obs
+
+
 def vec_step(state, action, shared_step):
     """VectorizedDroneEnv.step; returns obs, reward, done, new shared step."""
     n = len(action)

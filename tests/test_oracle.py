@@ -209,3 +209,37 @@ def test_gae_matches_sb3_numpy_restatement():
     a2, r2 = ppo_ref.gae_numpy(r, v, starts, lv, ld, 0.99, 0.95)
     np.testing.assert_array_equal(a1, a2)
     np.testing.assert_array_equal(r1, r2)
+
+
+def test_c_oracle_moving_reduces_to_gym(golden):
+    """The moving-target restatement with zero motion
+    amplitude IS the gym env: same state, reward, done and obs[:15] on the
+    reference's golden step vectors, zero target velocity; and its reset
+    with u[:5] = the gym draws reproduces the golden reset."""
+    g = golden("gym_step.npz")
+    ref_obs, _, _ = cref.gym_step({k: np.array(v) for k, v in _state(g).items()}, g["action"])
+    s = {k: np.array(v) for k, v in _state(g).items()}
+    n = len(g["action"])
+    rng = np.random.default_rng(0)
+    s["motion"] = np.concatenate([np.zeros((n, 3)), rng.uniform(0.5, 2, (n, 3)),
+                                  rng.uniform(0, 6.3, (n, 3))], 1).astype(np.float32)
+    obs, rew, done = cref.moving_step(s, g["action"])
+    np.testing.assert_array_equal(done, g["o_done"])
+    assert _rel(s["pos"], g["o_pos"]) <= REL and _rel(rew, g["o_rew"]) <= REL
+    assert (obs[:, 15:] == 0).all()
+    np.testing.assert_array_equal(obs[:, :15], ref_obs)
+
+    r = golden("gym_reset.npz")
+    m = len(r["u"])
+    s = {k: np.zeros((m, 3)) for k in ("pos", "vel", "euler", "omega", "target")}
+    s["step"] = np.full(m, 7, np.int32)
+    s["ep_num"] = r["ep_num"].astype(np.int64).copy()
+    s["eps"] = r["eps"].copy()
+    u = np.concatenate([r["u"], rng.uniform(0, 1, (m, 9))], 1)
+    obs = cref.moving_reset(s, u)
+    np.testing.assert_array_equal(s["target"], r["o_target"])
+    np.testing.assert_array_equal(obs[:, :12], r["o_obs"][:, :12])
+    # obs target-pos at s=0 uses the moved target: c + a sin(ph)
+    want = s["target"] + (s["motion"][:, :3] * np.sin(s["motion"][:, 6:])).astype(np.float32)
+    assert _rel(obs[:, 12:15].astype(np.float64), want - s["pos"]) < 1e-6
+    assert _rel(s["motion"][:, :3].astype(np.float64), s["eps"][:, None] * u[:, 5:8]) < 1e-6
