@@ -25,6 +25,7 @@
 #include <string>
 
 #include "common.h"
+#include "trig.h"
 
 #pragma clang fp contract(off)
 
@@ -81,6 +82,10 @@ __device__ unsigned long long g_stamps[16384 * 8];
 #ifndef DR_PREFETCH_EPS
 #define DR_PREFETCH_EPS 0
 #endif
+// 1 (A/B builds only): the device library's sincos(double) instead of trig.h
+#ifndef DR_LIB_TRIG
+#define DR_LIB_TRIG 0
+#endif
 #if DR_ABLATE == 1
 __device__ inline void m_sincos(double x, double *s, double *c) {
     float fs, fc;
@@ -88,10 +93,52 @@ __device__ inline void m_sincos(double x, double *s, double *c) {
     *s = fs;
     *c = fc;
 }
-#else
+#elif DR_LIB_TRIG
 __device__ inline void m_sincos(double x, double *s, double *c) { sincos(x, s, c); }
+#else
+// trig.h: 3-FMA reduction + shared polynomials (<= 1 ulp); the library
+// sincos only for |x| >= 2^19 rad, inf and NaN (a branch no lane usually takes)
+__device__ inline void m_sincos(double x, double *s, double *c) {
+    if (sincos_fast_range(x)) {
+        const SinCos t = sincos_medium(x);
+        *s = t.s;
+        *c = t.c;
+    } else {
+        sincos(x, s, c);
+    }
+}
+#define DR_SINCOS3 1
 #endif
+#ifndef DR_SINCOS3
+#define DR_SINCOS3 0
+#endif
+
 __device__ inline void m_sincos(float x, float *s, float *c) { sincosf(x, s, c); }
+
+// The three Euler angles at once: the fast path runs unconditionally for
+// all three (independent chains interleave; the polynomial constants are
+// materialised once), the library path only for out-of-range lanes.
+template <typename S>
+__device__ inline void m_sincos3(const S x[3], S s[3], S c[3]) {
+    if constexpr (DR_SINCOS3 && sizeof(S) == 8) {
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            const SinCos t = sincos_medium(x[k]);
+            s[k] = t.s;
+            c[k] = t.c;
+        }
+        const bool fast = (int)sincos_fast_range(x[0]) & (int)sincos_fast_range(x[1]) &
+                          (int)sincos_fast_range(x[2]);
+        if (!fast) {
+#pragma unroll
+            for (int k = 0; k < 3; ++k)
+                if (!sincos_fast_range(x[k])) sincos(x[k], &s[k], &c[k]);
+        }
+    } else {
+#pragma unroll
+        for (int k = 0; k < 3; ++k) m_sincos(x[k], &s[k], &c[k]);
+    }
+}
 __device__ inline double m_sqrt(double x) { return sqrt(x); }
 __device__ inline float m_sqrt(float x) { return sqrtf(x); }
 
@@ -290,12 +337,10 @@ __device__ inline S physics_step(S st[F_N], float4 act, S dt, bool &crash) {
 
     // One sincos per angle: a shared range reduction yields exactly the
     // separate sin() and cos() results at half the instructions.
-    const S theta = st[F_EUL + 1];
-    S sph, cph, sth, cth, sps, cps;
-    m_sincos(st[F_EUL + 0], &sph, &cph);
+    S sn[3], cs[3];
+    m_sincos3(&st[F_EUL], sn, cs);
     DR_STAMP(1);
-    m_sincos(theta, &sth, &cth);
-    m_sincos(st[F_EUL + 2], &sps, &cps);
+    const S sph = sn[0], cph = cs[0], sth = sn[1], cth = cs[1], sps = sn[2], cps = cs[2];
     // R(old euler) column 2 (drone.py:169-173): thrust is body-z only.
     const S r02 = cps * sth * cph + sps * sph;
     const S r12 = sps * sth * cph - cps * sph;
@@ -358,8 +403,11 @@ __device__ inline S physics_step(S st[F_N], float4 act, S dt, bool &crash) {
     }
     // Termination (154; vectorized_drone.py:211).  NaN compares false.
     const S px = st[F_POS + 0], py = st[F_POS + 1], pz = st[F_POS + 2];
-    const S pn = m_sqrt((px * px + py * py) + pz * pz);
-    crash = (pz < (S)0) || (pn > (S)50);
+    // norm(p) > 50  <=>  |p|^2 > 2500 exactly: sqrt is correctly rounded and
+    // the next representable square above 2500 already rounds above 50
+    // (f64 and f32 alike); NaN compares false either way.
+    const S pn2 = (px * px + py * py) + pz * pz;
+    crash = (pz < (S)0) || (pn2 > (S)2500);
     return r;
 }
 
@@ -447,18 +495,23 @@ __global__ __launch_bounds__(kBlock) void env_step_kernel(EnvView<S> v,
             st[F_TGT + 2] = (S)10.0;
         }
         int32_t step = v.step[i];
-        if constexpr (VAR == DR_VARIANT_MOVING) {
-            // the reward and obs of this step see the target at the NEW step
-            moving_target(cen, mp, step + 1, (float)v.dt, &st[F_TGT], tvel);
-        }
         // needed only if this env resets; loaded up front so a reset does
-        // not stall the wave on a dependent global load (+12 B per step,
+        // not stall the wave on a dependent global load (+4 B per step,
         // counted in the measured traffic, not in the 305 B algorithmic)
         int32_t ep_old = 0;
         double eps_old = 0.0;
         if constexpr (GYMLIKE) {
             ep_old = v.ep_num[i];
             if (DR_PREFETCH_EPS) eps_old = v.eps[i];
+        }
+        // Every load is issued before any arithmetic: without this the
+        // scheduler interleaves the first sincos with the loads and its
+        // s_waitcnt holds back the issue of the remaining ones by a full
+        // memory latency.
+        __builtin_amdgcn_sched_barrier(0);
+        if constexpr (VAR == DR_VARIANT_MOVING) {
+            // the reward and obs of this step see the target at the NEW step
+            moving_target(cen, mp, step + 1, (float)v.dt, &st[F_TGT], tvel);
         }
 
         bool crash;

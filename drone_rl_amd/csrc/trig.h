@@ -1,0 +1,80 @@
+// trig.h -- f64 sincos for the env step's Euler angles.
+//
+// The device library's sincos(double) spends ~95 VALU instructions per call
+// on a double-double range reduction (plus a Payne-Hanek path for huge
+// arguments).  The env step evaluates three of them per env on a
+// latency-bound critical path (one wave per SIMD at 65,536 envs), so this
+// version does the medium-range reduction with three FMAs (|x| < 2^19 rad;
+// k*P1 is exact there, so r carries <= 0.5 ulp of rounding) and evaluates
+// one shared pair of minimax polynomials on [-pi/4, pi/4] (the classic
+// fdlibm k_sin/k_cos coefficient sets, with k_cos's compensated 1 - z/2).
+// Error <= 1 ulp vs a correctly rounded sin/cos (checked against numpy on
+// the host by tests/test_trig_host.py).  Arguments outside the fast range,
+// infinities and NaN go to the library sincos.
+#pragma once
+
+#include <cmath>
+
+#ifndef __HIP__
+#define DR_HD
+#else
+#define DR_HD __host__ __device__
+#endif
+
+namespace dr {
+
+struct SinCos {
+    double s, c;
+};
+
+// r in [-pi/4, pi/4] (slightly beyond by rounding of k): sin(r), cos(r).
+DR_HD inline SinCos sincos_kernel(double r) {
+    const double z = r * r;
+    const double S1 = -1.66666666666666324348e-01, S2 = 8.33333333332248946124e-03,
+                 S3 = -1.98412698298579493134e-04, S4 = 2.75573137070700676789e-06,
+                 S5 = -2.50507602534068634195e-08, S6 = 1.58969099521155010221e-10;
+    const double C1 = 4.16666666666666019037e-02, C2 = -1.38888888888741095749e-03,
+                 C3 = 2.48015872894767294178e-05, C4 = -2.75573143513906633035e-07,
+                 C5 = 2.08757232129817482790e-09, C6 = -1.13596475577881948265e-11;
+    // sin: r + r^3 (S1 + z (S2 + ... ))
+    double ps = fma(z, S6, S5);
+    ps = fma(z, ps, S4);
+    ps = fma(z, ps, S3);
+    ps = fma(z, ps, S2);
+    const double rz = r * z;
+    const double s = fma(rz, fma(z, ps, S1), r);
+    // cos: (1 - z/2) + z^2 (C1 + z (C2 + ...)), 1 - z/2 compensated
+    double pc = fma(z, C6, C5);
+    pc = fma(z, pc, C4);
+    pc = fma(z, pc, C3);
+    pc = fma(z, pc, C2);
+    pc = fma(z, pc, C1);
+    const double hz = 0.5 * z;
+    const double w = 1.0 - hz;
+    const double corr = (1.0 - w) - hz;  // exact rounding error of w
+    const double c = w + fma(z * z, pc, corr);
+    return {s, c};
+}
+
+DR_HD inline bool sincos_fast_range(double x) { return fabs(x) < 524288.0; }
+
+// Precondition: sincos_fast_range(x).
+DR_HD inline SinCos sincos_medium(double x) {
+    const double kInvPio2 = 6.36619772367581382433e-01;
+    const double P1 = 1.57079632679489655800e+00;   // RN(pi/2)
+    const double P2 = 6.12323399573676603587e-17;   // RN(pi/2 - P1)
+    const double P3 = -1.49738490485916983053e-33;  // RN(pi/2 - P1 - P2)
+    const double k = rint(x * kInvPio2);
+    double r = fma(-k, P1, x);  // exact: |k| < 2^19
+    r = fma(-k, P2, r);
+    r = fma(-k, P3, r);
+    const SinCos t = sincos_kernel(r);
+    const int q = (int)k & 3;
+    const double s0 = (q & 1) ? t.c : t.s;
+    const double c0 = (q & 1) ? t.s : t.c;
+    const double s = (q & 2) ? -s0 : s0;
+    const double c = ((q + 1) & 2) ? -c0 : c0;
+    return {s, c};
+}
+
+}  // namespace dr

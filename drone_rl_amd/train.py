@@ -32,6 +32,8 @@ def main(argv=None):
     ap.add_argument("--net", type=int, nargs="+", default=[256, 256])
     ap.add_argument("--state-dtype", choices=["f64", "f32"], default="f64")
     ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--variant", choices=["gym", "moving"], default="gym",
+                    help="gym = DroneGymEnv; moving = the moving-target curriculum")
     ap.add_argument("--sb3-defaults", action="store_true",
                     help="SB3 PPO defaults of the reference (n_steps 2048, batch 64, 64x64)")
     ap.add_argument("--checkpoint", default="./dd_gpu.pt")
@@ -44,11 +46,12 @@ def main(argv=None):
     if world > 1:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     if a.sb3_defaults:
-        cfg = PPOConfig.sb3_defaults(num_envs=a.envs, seed=a.seed, state_dtype=a.state_dtype)
+        cfg = PPOConfig.sb3_defaults(num_envs=a.envs, seed=a.seed, state_dtype=a.state_dtype,
+                                     variant=a.variant)
     else:
         cfg = PPOConfig(num_envs=a.envs, n_steps=a.n_steps, batch_size=a.batch_size,
                         n_epochs=a.epochs, learning_rate=a.lr, net_arch=tuple(a.net),
-                        seed=a.seed, state_dtype=a.state_dtype)
+                        seed=a.seed, state_dtype=a.state_dtype, variant=a.variant)
     tr = PPOTrainer(cfg, rank=rank, world_size=world)
     ck = a.checkpoint if world == 1 else f"{a.checkpoint}.rank{rank}"
     if os.path.exists(ck):
