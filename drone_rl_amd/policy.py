@@ -120,6 +120,25 @@ class ActorCritic:
 
     __call__ = forward
 
+    @torch.no_grad()
+    def predict(self, obs, deterministic: bool = True, generator=None):
+        """SB3 ``BasePolicy.predict`` (test.py:13): the distribution's mode
+        (or a sample) clipped to the action space [0, 7.3575].  Accepts one
+        observation (obs_dim,) or a batch (N, obs_dim), numpy or tensor;
+        returns the same kind it was given."""
+        is_np = not isinstance(obs, torch.Tensor)
+        x = torch.as_tensor(np.asarray(obs, np.float32) if is_np else obs,
+                            dtype=torch.float32, device=self.device)
+        single = x.dim() == 1
+        x = x.reshape(-1, self.obs_dim)
+        mean, _ = self.forward(x)
+        if not deterministic:
+            z = torch.randn(mean.shape, generator=generator, device=self.device)
+            mean = mean + self.log_std.exp() * z
+        a = mean.clamp(0.0, 3 * 1.0 * 9.81 / 4.0)
+        a = a[0] if single else a
+        return (a.cpu().numpy(), None) if is_np else (a, None)
+
     def state_dict(self):
         """SB3-style parameter names (policy.mlp_extractor.policy_net.0.weight
         etc.) mapped to CPU tensors."""

@@ -259,5 +259,21 @@ class PPOTrainer:
     def load(self, path):
         self.load_state_dict(torch.load(path, map_location="cpu", weights_only=True))
 
+    def save_sb3(self, path):
+        """stable-baselines3 PPO .zip (train.py:70 ``model.save``); see sb3_zip."""
+        from . import sb3_zip
+        sb3_zip.save(self, path)
+
+    def load_sb3(self, path):
+        """Resume from an SB3 PPO .zip (train.py:10-31 ``PPO.load``): params,
+        Adam state, timesteps (+ curriculum when written by save_sb3)."""
+        from . import sb3_zip
+        ck = sb3_zip.load_into(self, path)
+        self._rolled = False
+        self.dones[self.cfg.n_steps].fill_(1)
+        with torch.no_grad():
+            self.env.reset(self.obs[0])
+        return ck
+
     def close(self):
         self.env.close()

@@ -4,6 +4,7 @@ PPO on the quadrotor env, here GPU-resident over N batched envs.
   python -m drone_rl_amd.train                        # 65,536 envs, 2x256 MLP
   python -m drone_rl_amd.train --sb3-defaults --envs 1 # the reference's config
   torchrun --nproc-per-node 8 --master-addr 127.0.0.1 -m drone_rl_amd.train
+  python -m drone_rl_amd.train --checkpoint dd.zip     # SB3 .zip in and out
 
 Like the reference it resumes from a checkpoint when one exists
 (train.py:10-31; ours also restores the env curriculum), trains for
@@ -54,13 +55,16 @@ def main(argv=None):
                         seed=a.seed, state_dtype=a.state_dtype, variant=a.variant)
     tr = PPOTrainer(cfg, rank=rank, world_size=world)
     ck = a.checkpoint if world == 1 else f"{a.checkpoint}.rank{rank}"
+    # *.zip = stable-baselines3 PPO checkpoint (the reference's dd.zip,
+    # train.py:10-31 / 70); anything else = this trainer's bit-exact resume file
+    sb3 = ck.endswith(".zip")
     if os.path.exists(ck):
-        tr.load(ck)
+        tr.load_sb3(ck) if sb3 else tr.load(ck)
         if rank == 0:
             print(json.dumps({"resumed": ck, "num_timesteps": tr.num_timesteps}), flush=True)
     tr.learn(int(a.total_steps), log_every=a.log_every,
              logger=lambda d: print(json.dumps(d), flush=True))
-    tr.save(ck)
+    tr.save_sb3(ck) if sb3 else tr.save(ck)
     tr.close()
     if world > 1:
         dist.destroy_process_group()

@@ -102,3 +102,22 @@ def test_checkpoint_resume_is_bitexact(tmp_path):
     assert a.num_timesteps == b.num_timesteps
     a.close()
     b.close()
+
+
+def test_sb3_zip_roundtrip_on_gpu(tmp_path):
+    """save_sb3 -> load_sb3 restores parameters, Adam state and the per-env
+    curriculum, and training continues (SB3 itself: parity unpinned)."""
+    a = _trainer()
+    a.learn_step()
+    a.env.set("eps", np.full(a.env.num_envs, 0.3))
+    path = tmp_path / "dd.zip"
+    a.save_sb3(path)
+    b = _trainer()
+    b.load_sb3(path)
+    assert torch.equal(a.policy.flat.detach(), b.policy.flat.detach())
+    assert torch.equal(a.opt.m, b.opt.m) and torch.equal(a.opt.v, b.opt.v)
+    assert b.opt.t == a.opt.t and b.num_timesteps == a.num_timesteps
+    assert (b.env.get("eps").cpu().numpy() == 0.3).all()
+    assert torch.isfinite(b.learn_step()).all()
+    a.close()
+    b.close()
