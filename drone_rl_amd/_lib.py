@@ -23,6 +23,7 @@ DR_ERR_HIP = -2
 DR_ERR_NOMEM = -3
 DR_ERR_UNSUPPORTED = -4
 
+ABI_VERSION = 2                 # DR_ABI_VERSION in include/dronerl.h
 DR_VARIANT_GYM = 0
 DR_VARIANT_VECTORIZED = 1
 DR_VARIANT_MOVING = 2
@@ -81,7 +82,7 @@ SIGNATURES = {
     "dr_tanh_backward_workspace_bytes": (c_size_t, [c_int64, c_int64]),
     "dr_tanh_backward": (c_int, [c_int64, c_int64, _P, _P, _P, _P, _P, c_size_t, _P]),
     "dr_ppo_loss_workspace_bytes": (c_size_t, [c_int64]),
-    "dr_ppo_loss": (c_int, [c_int64, _P, _P, _P, _P, _P, _P, _P, c_float,
+    "dr_ppo_loss": (c_int, [c_int64, _P, _P, _P, _P, _P, _P, _P, c_int64, c_float,
                             c_float, c_float, c_int, _P, _P, _P, _P, _P,
                             c_size_t, _P]),
     "dr_adam_workspace_bytes": (c_size_t, [c_int64]),
@@ -107,7 +108,7 @@ def lib() -> ctypes.CDLL:
         fn = getattr(l, name)  # AttributeError = missing export: loud
         fn.restype = res
         fn.argtypes = args
-    if l.dr_abi_version() != 1:
+    if l.dr_abi_version() != ABI_VERSION:
         raise ImportError("libdronerl.so ABI version mismatch")
     _lib = l
     return l

@@ -232,14 +232,15 @@ __device__ inline void block_sum(float (&x)[K], float *sh /* K*4 */) {
 // Pass 1 of the advantage normalisation: per-block (count, mean, M2)
 // (Chan et al. parallel variance) -> partials[3*b].
 __global__ __launch_bounds__(kBlock) void adv_stats_kernel(
-    int64_t m, const float *__restrict__ adv, float *__restrict__ part) {
+    int64_t m, const float *__restrict__ adv, int64_t stride, float *__restrict__ part) {
     __shared__ float sh[8];
     const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     const int64_t cnt = min((int64_t)kBlock, m - (int64_t)blockIdx.x * kBlock);
-    float x[1] = {i < m ? adv[i] : 0.f};
+    const float ai = i < m ? adv[i * stride] : 0.f;
+    float x[1] = {ai};
     block_sum<1>(x, sh);
     const float mean = x[0] / (float)cnt;
-    float d = i < m ? adv[i] - mean : 0.f;
+    float d = i < m ? ai - mean : 0.f;
     float y[1] = {d * d};
     block_sum<1>(y, sh);
     if (threadIdx.x == 0) {
@@ -249,21 +250,44 @@ __global__ __launch_bounds__(kBlock) void adv_stats_kernel(
     }
 }
 
-// Combine the per-block (n, mean, M2) partials in a fixed order.
-__device__ inline void merge_stats(const float *part, int nb, float &mean,
-                                   float &m2, float &count) {
+// Chan et al. merge of (n, mean, M2) b into a.
+__device__ inline void chan_merge(double &n, double &mu, double &M2, double nb_, double mb,
+                                  double m2b) {
+    const double tot = n + nb_;
+    if (tot == 0.0) return;
+    const double dl = mb - mu;
+    mu += dl * nb_ / tot;
+    M2 += m2b + dl * dl * n * nb_ / tot;
+    n = tot;
+}
+
+// Combine the per-block (n, mean, M2) partials with the whole block: strided
+// per-thread merges, then a fixed-shape tree in LDS (deterministic).  Every
+// thread returns the result.  Needs blockDim.x == kBlock.
+__device__ inline void merge_stats_block(const float *part, int nb, float &mean,
+                                         float &m2, float &count) {
+    __shared__ double sn[kBlock], smu[kBlock], sm2[kBlock];
+    const int t = threadIdx.x;
     double n = 0.0, mu = 0.0, M2 = 0.0;
-    for (int b = 0; b < nb; ++b) {
-        const double nb_ = part[3 * b], mb = part[3 * b + 1], m2b = part[3 * b + 2];
-        const double tot = n + nb_;
-        const double dl = mb - mu;
-        mu += dl * nb_ / tot;
-        M2 += m2b + dl * dl * n * nb_ / tot;
-        n = tot;
+    for (int b = t; b < nb; b += kBlock)
+        chan_merge(n, mu, M2, part[3 * b], part[3 * b + 1], part[3 * b + 2]);
+    sn[t] = n;
+    smu[t] = mu;
+    sm2[t] = M2;
+    __syncthreads();
+    for (int h = kBlock / 2; h > 0; h >>= 1) {
+        if (t < h) {
+            double a = sn[t], am = smu[t], a2 = sm2[t];
+            chan_merge(a, am, a2, sn[t + h], smu[t + h], sm2[t + h]);
+            sn[t] = a;
+            smu[t] = am;
+            sm2[t] = a2;
+        }
+        __syncthreads();
     }
-    mean = (float)mu;
-    m2 = (float)M2;
-    count = (float)n;
+    mean = (float)smu[0];
+    m2 = (float)sm2[0];
+    count = (float)sn[0];
 }
 
 // Fused PPO loss over a minibatch: per row the Gaussian log-prob of the
@@ -281,6 +305,7 @@ struct LossArgs {
     const float *old_logp;
     const float *adv;
     const float *ret;
+    int64_t stride;  // element stride of old_logp / adv / ret
     float clip, ent_coef, vf_coef;
     int normalize;
     const float *adv_part;  // 3 * nb partials from adv_stats_kernel
@@ -294,21 +319,14 @@ constexpr int kLossK = 9;  // pl, vl, clipcnt, kl, g_ls[4], (spare)
 
 __global__ __launch_bounds__(kBlock) void ppo_loss_kernel(LossArgs a) {
     __shared__ float sh[kLossK * 4];
-    __shared__ float stat_sh[2];
     const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-    if (threadIdx.x == 0) {
-        float mean = 0.f, std = 1.f;
-        if (a.normalize) {
-            float m2, cnt;
-            merge_stats(a.adv_part, a.nb, mean, m2, cnt);
-            // torch.std: unbiased (n-1); SB3 adds 1e-8 to std
-            std = sqrtf(m2 / (cnt - 1.0f));
-        }
-        stat_sh[0] = mean;
-        stat_sh[1] = std;
+    float amean = 0.f, astd = 1.f;
+    if (a.normalize) {
+        float m2, cnt;
+        merge_stats_block(a.adv_part, a.nb, amean, m2, cnt);
+        // torch.std: unbiased (n-1); SB3 adds 1e-8 to std
+        astd = sqrtf(m2 / (cnt - 1.0f));
     }
-    __syncthreads();
-    const float amean = stat_sh[0], astd = stat_sh[1];
     float acc[kLossK] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
     if (i < a.m) {
         const float ls[4] = {a.log_std[0], a.log_std[1], a.log_std[2], a.log_std[3]};
@@ -324,9 +342,9 @@ __global__ __launch_bounds__(kBlock) void ppo_loss_kernel(LossArgs a) {
             zz[j] = d / var;             // d logp / d mu_j
             lp += (-(d * d) / (2.0f * var) - logf(sd)) - kLogSqrt2Pi;
         }
-        float A = a.adv[i];
+        float A = a.adv[i * a.stride];
         if (a.normalize) A = (A - amean) / (astd + 1e-8f);
-        const float logr = lp - a.old_logp[i];
+        const float logr = lp - a.old_logp[i * a.stride];
         const float r = expf(logr);
         const float lo = 1.0f - a.clip, hi = 1.0f + a.clip;
         const float rc = fminf(fmaxf(r, lo), hi);
@@ -341,9 +359,10 @@ __global__ __launch_bounds__(kBlock) void ppo_loss_kernel(LossArgs a) {
         const float dlp = dr * r;                              // dL/dlogp
         // value loss: vf_coef * mean((R - V)^2)
         const float v = a.values[i];
-        const float e = a.ret[i] - v;
+        const float R = a.ret[i * a.stride];
+        const float e = R - v;
         acc[1] = e * e;
-        a.grad_values[i] = a.vf_coef * (2.0f * (v - a.ret[i])) * inv_m;
+        a.grad_values[i] = a.vf_coef * (2.0f * (v - R)) * inv_m;
         acc[2] = (fabsf(r - 1.0f) > a.clip) ? 1.f : 0.f;
         acc[3] = (r - 1.0f) - logr;                       // approx_kl term
         a.grad_mean[i] = make_float4(dlp * zz[0], dlp * zz[1], dlp * zz[2], dlp * zz[3]);
@@ -424,18 +443,21 @@ __global__ __launch_bounds__(kBlock) void clip_adam_kernel(
     float *__restrict__ m, float *__restrict__ v, const float *__restrict__ part,
     int nb, float max_norm, float w1, float beta2, float one_m_b2,
     float step_size, float bc2_sqrt, float eps, float *norm_out) {
-    __shared__ float coef_sh;
-    if (threadIdx.x == 0) {
-        double s = 0.0;
-        for (int b = 0; b < nb; ++b) s += part[b];
-        const float total = (float)sqrt(s);
-        float c = max_norm / (total + 1e-6f);
-        c = c < 1.0f ? c : 1.0f;
-        coef_sh = c;
-        if (blockIdx.x == 0 && norm_out) *norm_out = total;
-    }
+    // total squared norm: strided per-thread sums of the sumsq partials, then
+    // a fixed-shape LDS tree (deterministic; every block gets the same value)
+    __shared__ double ssum[kBlock];
+    double s = 0.0;
+    for (int b = threadIdx.x; b < nb; b += kBlock) s += part[b];
+    ssum[threadIdx.x] = s;
     __syncthreads();
-    const float c = coef_sh;
+    for (int h = kBlock / 2; h > 0; h >>= 1) {
+        if ((int)threadIdx.x < h) ssum[threadIdx.x] += ssum[threadIdx.x + h];
+        __syncthreads();
+    }
+    const float total = (float)sqrt(ssum[0]);
+    float c = max_norm / (total + 1e-6f);
+    c = c < 1.0f ? c : 1.0f;
+    if (blockIdx.x == 0 && threadIdx.x == 0 && norm_out) *norm_out = total;
     for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n;
          i += (int64_t)gridDim.x * kBlock) {
         const float gi = g[i] * c;
@@ -575,13 +597,14 @@ size_t dr_ppo_loss_workspace_bytes(int64_t m) {
 
 int dr_ppo_loss(int64_t m, const float *mean, const float *log_std, const float *values,
                 const float *actions, const float *old_logp, const float *advantages,
-                const float *returns, float clip_range, float ent_coef, float vf_coef,
+                const float *returns, int64_t aux_stride, float clip_range, float ent_coef, float vf_coef,
                 int normalize_advantage, float *grad_mean, float *grad_values,
                 float *grad_log_std, float *stats, void *workspace, size_t workspace_bytes,
                 void *stream) {
     if (m < 1 || !mean || !log_std || !values || !actions || !old_logp || !advantages ||
         !returns || !grad_mean || !grad_values || !grad_log_std || !stats)
         return fail0(DR_ERR_INVALID, "dr_ppo_loss: bad arguments");
+    if (aux_stride < 1) return fail0(DR_ERR_INVALID, "dr_ppo_loss: aux_stride must be >= 1");
     if ((((uintptr_t)mean) | ((uintptr_t)actions) | ((uintptr_t)grad_mean)) & 15)
         return fail0(DR_ERR_INVALID, "dr_ppo_loss: (m,4) buffers must be 16-byte aligned");
     if (!workspace || workspace_bytes < dr_ppo_loss_workspace_bytes(m))
@@ -595,13 +618,13 @@ int dr_ppo_loss(int64_t m, const float *mean, const float *log_std, const float 
     hipStream_t st = as_stream(stream);
     if (norm) {
         hipLaunchKernelGGL(adv_stats_kernel, dim3(nb), dim3(kBlock), 0, st, m, advantages,
-                           adv_part);
+                           aux_stride, adv_part);
         int rc = check_launch("dr_ppo_loss stats");
         if (rc) return rc;
     }
     LossArgs a{m, reinterpret_cast<const float4 *>(mean), log_std, values,
                reinterpret_cast<const float4 *>(actions), old_logp, advantages, returns,
-               clip_range, ent_coef, vf_coef, norm, adv_part, nb,
+               aux_stride, clip_range, ent_coef, vf_coef, norm, adv_part, nb,
                reinterpret_cast<float4 *>(grad_mean), grad_values, part};
     hipLaunchKernelGGL(ppo_loss_kernel, dim3(nb), dim3(kBlock), 0, st, a);
     int rc = check_launch("dr_ppo_loss");

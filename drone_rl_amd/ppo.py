@@ -169,11 +169,8 @@ class PPOTrainer:
                 K.gather_rows(idx, act_flat, out=self.mb_act)
                 K.gather_rows(idx, self.aux, out=self.mb_aux)
                 mean, value, cache = self.fused.forward(self.mb_obs)
-                old_logp = self.mb_aux[:, 0].contiguous()
-                adv = self.mb_aux[:, 1].contiguous()
-                ret = self.mb_aux[:, 2].contiguous()
-                g_mean, g_ls, g_v, st = self.loss(mean, log_std, value.contiguous(),
-                                                  self.mb_act, old_logp, adv, ret)
+                g_mean, g_ls, g_v, st = self.loss(mean, log_std, value, self.mb_act,
+                                                  aux=self.mb_aux)
                 grad = self.fused.backward(self.mb_obs, cache, g_mean, g_v, g_ls)
                 self._allreduce_grad(grad)
                 self.opt.step(grad)

@@ -109,12 +109,24 @@ class PPOLoss:
         self.grad_log_std = torch.empty(4, dtype=torch.float32, device=device)
         self.stats = torch.empty(8, dtype=torch.float32, device=device)
 
-    def __call__(self, mean, log_std, values, actions, old_logp, advantages, returns):
+    def __call__(self, mean, log_std, values, actions, old_logp=None, advantages=None,
+                 returns=None, aux=None):
+        """Either old_logp / advantages / returns as three (m,) arrays, or
+        aux = one contiguous (m,3) array of (old_logp, advantage, return)
+        rows (read in place with stride 3)."""
         m = mean.shape[0]
         assert m == self.m
+        if aux is not None:
+            assert aux.shape == (m, 3)
+            base = _f32(aux)
+            p_lp, p_adv, p_ret = ptr(base), ptr(base) + 4, ptr(base) + 8
+            stride = 3
+        else:
+            p_lp, p_adv, p_ret = ptr(_f32(old_logp)), ptr(_f32(advantages)), ptr(_f32(returns))
+            stride = 1
         check(_lib.lib().dr_ppo_loss(
             m, ptr(_f32(mean)), ptr(_f32(log_std)), ptr(_f32(values)), ptr(_f32(actions)),
-            ptr(_f32(old_logp)), ptr(_f32(advantages)), ptr(_f32(returns)),
+            p_lp, p_adv, p_ret, stride,
             float(self.clip), float(self.ent), float(self.vf), self.norm,
             ptr(self.grad_mean), ptr(self.grad_values), ptr(self.grad_log_std),
             ptr(self.stats), ptr(self.ws), self.ws.numel(), _s(mean)))

@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define DR_ABI_VERSION 1
+#define DR_ABI_VERSION 2
 
 enum dr_status {
     DR_OK = 0,
@@ -235,7 +235,10 @@ int dr_tanh_backward(int64_t m, int64_t n, const float *grad_h, const float *h,
    (PPO.train: normalised advantage, ratio/clip surrogate, value MSE,
    entropy).  Inputs for a minibatch of m rows:
      mean (m,4), log_std (4), values (m), actions (m,4), old_logp (m),
-     advantages (m), returns (m).
+     advantages (m), returns (m); old_logp / advantages / returns are read
+     with element stride aux_stride (1: three arrays; 3: one interleaved
+     (m,3) array of rows (old_logp, advantage, return), the rollout
+     buffer's gathered minibatch, no repacking copies).
    Outputs:
      grad_mean (m,4), grad_values (m), grad_log_std (4): dLoss/d(.)
      stats (8) f32: [loss, policy_loss, value_loss, entropy_loss,
@@ -245,7 +248,8 @@ size_t dr_ppo_loss_workspace_bytes(int64_t m);
 int dr_ppo_loss(int64_t m, const float *mean, const float *log_std,
                 const float *values, const float *actions,
                 const float *old_logp, const float *advantages,
-                const float *returns, float clip_range, float ent_coef,
+                const float *returns, int64_t aux_stride, float clip_range,
+                float ent_coef,
                 float vf_coef, int normalize_advantage, float *grad_mean,
                 float *grad_values, float *grad_log_std, float *stats,
                 void *workspace, size_t workspace_bytes, void *stream);

@@ -106,6 +106,13 @@ def test_ppo_loss_vs_torch_autograd(normalize):
     np.testing.assert_allclose(g_mean.cpu().numpy(), gm, rtol=0, atol=1e-4 * scale)
     np.testing.assert_allclose(g_v.cpu().numpy(), gv, rtol=0, atol=1e-6)
     np.testing.assert_allclose(g_ls.cpu().numpy(), gls, rtol=1e-4, atol=1e-5)
+    # the interleaved (m,3) aux form (the trainer's gathered rollout rows)
+    # reads the same numbers: identical outputs
+    keep = [t.clone() for t in (g_mean, g_ls, g_v, L.stats)]
+    aux = cu(np.stack([old_logp, adv, returns], 1).copy())
+    out = L(cu(mean), cu(log_std), cu(values), cu(actions), aux=aux)
+    for a, b in zip(keep, out):
+        assert torch.equal(a, b)
 
 
 def test_clip_adam_vs_torch():
