@@ -81,6 +81,12 @@ SIGNATURES = {
     "dr_gather_rows": (c_int, [c_int64, c_int64, _P, _P, _P, _P]),
     "dr_tanh_backward_workspace_bytes": (c_size_t, [c_int64, c_int64]),
     "dr_tanh_backward": (c_int, [c_int64, c_int64, _P, _P, _P, _P, _P, c_size_t, _P]),
+    "dr_linear_tanh": (c_int, [c_int64, c_int64, c_int64, _P, _P, _P, _P, _P]),
+    "dr_policy_heads": (c_int, [c_int64, c_int64, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
+    "dr_ppo_head_workspace_bytes": (c_size_t, [c_int64, c_int64]),
+    "dr_ppo_head_loss_backward": (c_int, [c_int64, c_int64] + [_P] * 9 +
+                                  [c_float, c_float, c_float, c_int] + [_P] * 10 +
+                                  [_P, c_size_t, _P]),
     "dr_ppo_loss_workspace_bytes": (c_size_t, [c_int64]),
     "dr_ppo_loss": (c_int, [c_int64, _P, _P, _P, _P, _P, _P, _P, c_int64, c_float,
                             c_float, c_float, c_int, _P, _P, _P, _P, _P,

@@ -317,6 +317,73 @@ struct LossArgs {
 
 constexpr int kLossK = 9;  // pl, vl, clipcnt, kl, g_ls[4], (spare)
 
+// Per-row PPO loss terms and gradient, shared by ppo_loss_kernel and the
+// fused head kernel so both compute bit-identical rows.
+struct RowLossConst {
+    float var[4], logsd[4];
+    float lo, hi, clip, inv_m, vf_coef, amean, astd;
+    int normalize;
+};
+
+__device__ inline RowLossConst row_loss_const(const float *log_std, float clip, float vf_coef,
+                                              int64_t m, int normalize, float amean,
+                                              float astd) {
+    RowLossConst c;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const float sd = expf(log_std[j]);
+        c.var[j] = sd * sd;
+        c.logsd[j] = logf(sd);
+    }
+    c.lo = 1.0f - clip;
+    c.hi = 1.0f + clip;
+    c.clip = clip;
+    c.inv_m = 1.0f / (float)m;
+    c.vf_coef = vf_coef;
+    c.amean = amean;
+    c.astd = astd;
+    c.normalize = normalize;
+    return c;
+}
+
+// acc[0..8] += (-min(l1,l2), (R-V)^2, clipped, kl term, dL/dlog_std[4]);
+// gm = dL/dmean (4), gv = dL/dvalue.  Gradient conventions follow torch
+// autograd of PPO.train's expression: a min() tie sends half the gradient
+// to each branch; clamp passes gradient inside the closed interval.
+__device__ inline void ppo_row(const RowLossConst &c, const float mu[4], const float ac[4],
+                               float old_lp, float A, float R, float v, float gm[4],
+                               float &gv, float acc[kLossK]) {
+    float lp = 0.f, zz[4], dd[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const float d = ac[j] - mu[j];
+        dd[j] = d;
+        zz[j] = d / c.var[j];             // d logp / d mu_j
+        lp += (-(d * d) / (2.0f * c.var[j]) - c.logsd[j]) - kLogSqrt2Pi;
+    }
+    if (c.normalize) A = (A - c.amean) / (c.astd + 1e-8f);
+    const float logr = lp - old_lp;
+    const float r = expf(logr);
+    const float rc = fminf(fmaxf(r, c.lo), c.hi);
+    const float l1 = A * r, l2 = A * rc;
+    acc[0] += -fminf(l1, l2);                          // policy_loss = -mean(min)
+    const float g1 = l1 < l2 ? 1.f : (l1 == l2 ? 0.5f : 0.f);
+    const float g2 = l2 < l1 ? 1.f : (l1 == l2 ? 0.5f : 0.f);
+    const float dclamp = (r >= c.lo && r <= c.hi) ? 1.f : 0.f;
+    const float dr = -(g1 * A + g2 * A * dclamp) * c.inv_m;  // dL/dratio
+    const float dlp = dr * r;                                // dL/dlogp
+    const float e = R - v;                                   // vf_coef * mean((R-V)^2)
+    acc[1] += e * e;
+    gv = c.vf_coef * (2.0f * (v - R)) * c.inv_m;
+    acc[2] += (fabsf(r - 1.0f) > c.clip) ? 1.f : 0.f;
+    acc[3] += (r - 1.0f) - logr;                             // approx_kl term
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        gm[j] = dlp * zz[j];
+        acc[4 + j] += dlp * ((dd[j] * dd[j]) / c.var[j] - 1.0f);  // d/dlog_std_j
+    }
+}
+
 __global__ __launch_bounds__(kBlock) void ppo_loss_kernel(LossArgs a) {
     __shared__ float sh[kLossK * 4];
     const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
@@ -327,52 +394,18 @@ __global__ __launch_bounds__(kBlock) void ppo_loss_kernel(LossArgs a) {
         // torch.std: unbiased (n-1); SB3 adds 1e-8 to std
         astd = sqrtf(m2 / (cnt - 1.0f));
     }
+    const RowLossConst c = row_loss_const(a.log_std, a.clip, a.vf_coef, a.m, a.normalize,
+                                          amean, astd);
     float acc[kLossK] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
     if (i < a.m) {
-        const float ls[4] = {a.log_std[0], a.log_std[1], a.log_std[2], a.log_std[3]};
         const float4 mu4 = a.mean[i], ac4 = a.actions[i];
         const float mu[4] = {mu4.x, mu4.y, mu4.z, mu4.w};
         const float ac[4] = {ac4.x, ac4.y, ac4.z, ac4.w};
-        float lp = 0.f, zz[4];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const float sd = expf(ls[j]);
-            const float d = ac[j] - mu[j];
-            const float var = sd * sd;
-            zz[j] = d / var;             // d logp / d mu_j
-            lp += (-(d * d) / (2.0f * var) - logf(sd)) - kLogSqrt2Pi;
-        }
-        float A = a.adv[i * a.stride];
-        if (a.normalize) A = (A - amean) / (astd + 1e-8f);
-        const float logr = lp - a.old_logp[i * a.stride];
-        const float r = expf(logr);
-        const float lo = 1.0f - a.clip, hi = 1.0f + a.clip;
-        const float rc = fminf(fmaxf(r, lo), hi);
-        const float l1 = A * r, l2 = A * rc;
-        const float inv_m = 1.0f / (float)a.m;
-        // policy_loss = -mean(min(l1, l2))
-        acc[0] = -fminf(l1, l2);
-        float g1 = l1 < l2 ? 1.f : (l1 == l2 ? 0.5f : 0.f);
-        float g2 = l2 < l1 ? 1.f : (l1 == l2 ? 0.5f : 0.f);
-        const float dclamp = (r >= lo && r <= hi) ? 1.f : 0.f;
-        const float dr = -(g1 * A + g2 * A * dclamp) * inv_m;  // dL/dratio
-        const float dlp = dr * r;                              // dL/dlogp
-        // value loss: vf_coef * mean((R - V)^2)
-        const float v = a.values[i];
-        const float R = a.ret[i * a.stride];
-        const float e = R - v;
-        acc[1] = e * e;
-        a.grad_values[i] = a.vf_coef * (2.0f * (v - R)) * inv_m;
-        acc[2] = (fabsf(r - 1.0f) > a.clip) ? 1.f : 0.f;
-        acc[3] = (r - 1.0f) - logr;                       // approx_kl term
-        a.grad_mean[i] = make_float4(dlp * zz[0], dlp * zz[1], dlp * zz[2], dlp * zz[3]);
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const float d = ac[j] - mu[j];
-            const float sd = expf(ls[j]);
-            // d logp / d log_std_j = d^2 / var - 1
-            acc[4 + j] = dlp * ((d * d) / (sd * sd) - 1.0f);
-        }
+        float gm[4], gv;
+        ppo_row(c, mu, ac, a.old_logp[i * a.stride], a.adv[i * a.stride],
+                a.ret[i * a.stride], a.values[i], gm, gv, acc);
+        a.grad_values[i] = gv;
+        a.grad_mean[i] = make_float4(gm[0], gm[1], gm[2], gm[3]);
     }
     block_sum<kLossK>(acc, sh);
     if (threadIdx.x == 0) {
@@ -418,6 +451,280 @@ __global__ void ppo_loss_finish_kernel(int64_t m, int nb, const float *part,
         stats[6] = part[kLossK * nb + 0];
         stats[7] = part[kLossK * nb + 1];
     }
+}
+
+// ---------------------------------------------------------------------------
+// Actor-critic MLP pieces around the hidden-layer GEMMs (which stay on
+// hipBLASLt / MFMA).  One wave per row, lane l owning hidden columns
+// [4l, 4l+4): a row of activations is one coalesced 16 B-per-lane access.
+// ---------------------------------------------------------------------------
+template <int CTRL>
+__device__ inline float dpp_mov(float x) {
+    return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), CTRL, 0xF, 0xF, true));
+}
+
+// Sum over the 64 lanes, returned wave-uniform.  Fixed butterfly order:
+// quad xor 1, quad xor 2, half-row mirror, row mirror (DPP), xor 16
+// (ds_swizzle), then lane 0 + lane 32.
+__device__ inline float wave_allsum(float x) {
+    x = x + dpp_mov<0xB1>(x);
+    x = x + dpp_mov<0x4E>(x);
+    x = x + dpp_mov<0x141>(x);
+    x = x + dpp_mov<0x140>(x);
+    x = x + __int_as_float(__builtin_amdgcn_ds_swizzle(__float_as_int(x), 0x401F));
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(x), 0)) +
+           __int_as_float(__builtin_amdgcn_readlane(__float_as_int(x), 32));
+}
+
+__device__ inline float4 ld4(const float *p) { return *reinterpret_cast<const float4 *>(p); }
+__device__ inline float dot4(float4 a, float4 b) {
+    return fmaf(a.w, b.w, fmaf(a.z, b.z, fmaf(a.y, b.y, a.x * b.x)));
+}
+
+// h = tanh(x W^T + b) for a narrow input (the first layer: K = obs_dim),
+// x (m,K), W (n,K), b (n), h (m,n), n % 4 == 0, n <= 256.  Memory-bound on
+// the h write; replaces an addmm + a separate tanh pass over h.
+template <int K>
+__global__ __launch_bounds__(kBlock) void linear_tanh_kernel(int64_t m, int n,
+                                                             const float *__restrict__ x,
+                                                             const float *__restrict__ w,
+                                                             const float *__restrict__ b,
+                                                             float *__restrict__ h) {
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const int c0 = 4 * lane;
+    const bool act = c0 < n;
+    float wr[4][K], bb[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        bb[q] = act ? b[c0 + q] : 0.f;
+#pragma unroll
+        for (int k = 0; k < K; ++k) wr[q][k] = act ? w[(c0 + q) * K + k] : 0.f;
+    }
+    for (int64_t r = (int64_t)blockIdx.x * 4 + wid; r < m; r += (int64_t)gridDim.x * 4) {
+        const float xv = lane < K ? x[r * K + lane] : 0.f;
+        float acc[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            const float xk = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(xv), k));
+#pragma unroll
+            for (int q = 0; q < 4; ++q) acc[q] = fmaf(xk, wr[q][k], acc[q]);
+        }
+        if (act)
+            *reinterpret_cast<float4 *>(h + r * n + c0) =
+                make_float4(tanhf(acc[0] + bb[0]), tanhf(acc[1] + bb[1]),
+                            tanhf(acc[2] + bb[2]), tanhf(acc[3] + bb[3]));
+    }
+}
+
+// Policy heads for inference (rollouts): mean = h_pi Wa^T + ba (m,4),
+// value = h_vf Wv^T + bv (m).
+__global__ __launch_bounds__(kBlock) void policy_heads_kernel(
+    int64_t m, int hd, const float *__restrict__ h_pi, const float *__restrict__ h_vf,
+    const float *__restrict__ w_act, const float *__restrict__ b_act,
+    const float *__restrict__ w_val, const float *__restrict__ b_val,
+    float4 *__restrict__ mean, float *__restrict__ value) {
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const int c0 = 4 * lane;
+    const bool act = c0 < hd;
+    const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
+    float4 wa[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) wa[j] = act ? ld4(w_act + j * hd + c0) : z4;
+    const float4 wv = act ? ld4(w_val + c0) : z4;
+    for (int64_t r = (int64_t)blockIdx.x * 4 + wid; r < m; r += (int64_t)gridDim.x * 4) {
+        const float4 hp = act ? ld4(h_pi + r * hd + c0) : z4;
+        const float4 hv = act ? ld4(h_vf + r * hd + c0) : z4;
+        float d[5];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) d[j] = wave_allsum(dot4(hp, wa[j]));
+        d[4] = wave_allsum(dot4(hv, wv));
+        if (lane == 0) {
+            mean[r] = make_float4(d[0] + b_act[0], d[1] + b_act[1], d[2] + b_act[2],
+                                  d[3] + b_act[3]);
+            value[r] = d[4] + b_val[0];
+        }
+    }
+}
+
+// Fused heads + PPO loss + backward through the heads and the top tanh, for
+// one minibatch.  Per row (one wave): mean / value from the top hidden
+// activations, the PPO row loss (ppo_row) and its gradient, then
+//   gz_pi = (g_mean Wa) * (1 - h_pi^2),  gz_vf = (g_v Wv) * (1 - h_vf^2)
+// written for the hidden-layer backward, and per-block partial sums of every
+// head parameter gradient, the top hidden biases and the loss terms.
+// Partial layout per block (P = 14 + 7 h floats):
+//   [0,9) loss terms, [9,13) d b_act, 13 d b_val, then d b_pi (h),
+//   d b_vf (h), d W_act (4h, row-major), d W_val (h).
+constexpr int kHeadFixed = 14;
+
+struct HeadArgs {
+    int64_t m;
+    int hd;
+    const float *h_pi, *h_vf;
+    const float *w_act, *b_act, *w_val, *b_val, *log_std;
+    const float4 *actions;
+    const float *aux;  // (m,3): old_logp, advantage, return
+    float clip, ent_coef, vf_coef;
+    int normalize;
+    const float *adv_part;
+    int adv_nb;
+    float *gz_pi, *gz_vf;
+    float *part;
+    int P;
+};
+
+__global__ __launch_bounds__(kBlock) void ppo_head_kernel(HeadArgs a) {
+    extern __shared__ float sh_part[];  // 4 * P
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const int hd = a.hd, c0 = 4 * lane;
+    const bool act = c0 < hd;
+    float amean = 0.f, astd = 1.f;
+    if (a.normalize) {
+        float m2, cnt;
+        merge_stats_block(a.adv_part, a.adv_nb, amean, m2, cnt);
+        astd = sqrtf(m2 / (cnt - 1.0f));
+    }
+    const RowLossConst c = row_loss_const(a.log_std, a.clip, a.vf_coef, a.m, a.normalize,
+                                          amean, astd);
+    const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
+    float4 wa[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) wa[j] = act ? ld4(a.w_act + j * hd + c0) : z4;
+    const float4 wv = act ? ld4(a.w_val + c0) : z4;
+    const float ba[4] = {a.b_act[0], a.b_act[1], a.b_act[2], a.b_act[3]};
+    const float bv = a.b_val[0];
+    float u[kHeadFixed];
+#pragma unroll
+    for (int k = 0; k < kHeadFixed; ++k) u[k] = 0.f;
+    float sbp[4] = {0.f, 0.f, 0.f, 0.f}, sbv[4] = {0.f, 0.f, 0.f, 0.f};
+    float swa[4][4] = {}, swv[4] = {0.f, 0.f, 0.f, 0.f};
+    for (int64_t r = (int64_t)blockIdx.x * 4 + wid; r < a.m; r += (int64_t)gridDim.x * 4) {
+        const float4 hp4 = act ? ld4(a.h_pi + r * hd + c0) : z4;
+        const float4 hv4 = act ? ld4(a.h_vf + r * hd + c0) : z4;
+        float mu[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) mu[j] = wave_allsum(dot4(hp4, wa[j])) + ba[j];
+        const float v = wave_allsum(dot4(hv4, wv)) + bv;
+        const float4 ac4 = a.actions[r];
+        const float ac[4] = {ac4.x, ac4.y, ac4.z, ac4.w};
+        float gm[4], gv;
+        ppo_row(c, mu, ac, a.aux[3 * r], a.aux[3 * r + 1], a.aux[3 * r + 2], v, gm, gv, u);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) u[9 + j] += gm[j];
+        u[13] += gv;
+        const float hp[4] = {hp4.x, hp4.y, hp4.z, hp4.w};
+        const float hv[4] = {hv4.x, hv4.y, hv4.z, hv4.w};
+        const float wq[4][4] = {{wa[0].x, wa[0].y, wa[0].z, wa[0].w},
+                                {wa[1].x, wa[1].y, wa[1].z, wa[1].w},
+                                {wa[2].x, wa[2].y, wa[2].z, wa[2].w},
+                                {wa[3].x, wa[3].y, wa[3].z, wa[3].w}};
+        const float wvq[4] = {wv.x, wv.y, wv.z, wv.w};
+        float gzp[4], gzv[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const float gh = fmaf(gm[3], wq[3][q], fmaf(gm[2], wq[2][q],
+                                  fmaf(gm[1], wq[1][q], gm[0] * wq[0][q])));
+            gzp[q] = gh * (1.0f - hp[q] * hp[q]);
+            gzv[q] = (gv * wvq[q]) * (1.0f - hv[q] * hv[q]);
+            sbp[q] += gzp[q];
+            sbv[q] += gzv[q];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) swa[j][q] = fmaf(gm[j], hp[q], swa[j][q]);
+            swv[q] = fmaf(gv, hv[q], swv[q]);
+        }
+        if (act) {
+            *reinterpret_cast<float4 *>(a.gz_pi + r * hd + c0) =
+                make_float4(gzp[0], gzp[1], gzp[2], gzp[3]);
+            *reinterpret_cast<float4 *>(a.gz_vf + r * hd + c0) =
+                make_float4(gzv[0], gzv[1], gzv[2], gzv[3]);
+        }
+    }
+    float *mine = sh_part + wid * a.P;
+    if (lane == 0) {
+#pragma unroll
+        for (int k = 0; k < kHeadFixed; ++k) mine[k] = u[k];
+    }
+    if (act) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            mine[kHeadFixed + c0 + q] = sbp[q];
+            mine[kHeadFixed + hd + c0 + q] = sbv[q];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) mine[kHeadFixed + 2 * hd + j * hd + c0 + q] = swa[j][q];
+            mine[kHeadFixed + 6 * hd + c0 + q] = swv[q];
+        }
+    }
+    __syncthreads();
+    const int P = a.P;
+    for (int p = threadIdx.x; p < P; p += kBlock)
+        a.part[(int64_t)blockIdx.x * P + p] =
+            ((sh_part[p] + sh_part[P + p]) + sh_part[2 * P + p]) + sh_part[3 * P + p];
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        a.part[(int64_t)gridDim.x * P + 0] = amean;
+        a.part[(int64_t)gridDim.x * P + 1] = astd;
+    }
+}
+
+// Column sums of the head partials in a fixed order, scattered into the
+// gradient outputs; block 0 also forms the loss statistics.
+struct HeadOut {
+    float *g_w_act, *g_b_act, *g_w_val, *g_b_val, *g_b_pi, *g_b_vf, *g_log_std, *stats;
+};
+
+__global__ __launch_bounds__(kBlock) void ppo_head_finish_kernel(
+    int nb, int P, int hd, int64_t m, const float *__restrict__ part,
+    const float *__restrict__ log_std, float ent_coef, float vf_coef, HeadOut o) {
+    __shared__ float loss[kLossK];
+    const int p = blockIdx.x * kBlock + threadIdx.x;
+    if (p < P) {
+        float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+        int b = 0;
+        for (; b + 3 < nb; b += 4) {
+            s0 += part[(int64_t)(b + 0) * P + p];
+            s1 += part[(int64_t)(b + 1) * P + p];
+            s2 += part[(int64_t)(b + 2) * P + p];
+            s3 += part[(int64_t)(b + 3) * P + p];
+        }
+        for (; b < nb; ++b) s0 += part[(int64_t)b * P + p];
+        const float s = ((s0 + s1) + s2) + s3;
+        if (p < kLossK) {
+            loss[p] = s;
+        } else if (p < 13) {
+            o.g_b_act[p - 9] = s;
+        } else if (p == 13) {
+            o.g_b_val[0] = s;
+        } else {
+            const int q = p - kHeadFixed;
+            if (q < hd) o.g_b_pi[q] = s;
+            else if (q < 2 * hd) o.g_b_vf[q - hd] = s;
+            else if (q < 6 * hd) o.g_w_act[q - 2 * hd] = s;
+            else o.g_w_val[q - 6 * hd] = s;
+        }
+    }
+    if (blockIdx.x != 0) return;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const float inv_m = 1.0f / (float)m;
+        const float pl = loss[0] * inv_m;
+        const float vl = loss[1] * inv_m;
+        float H = 0.f;
+        for (int j = 0; j < 4; ++j) H += 0.5f + kLogSqrt2Pi + log_std[j];
+        const float el = -H;
+        for (int j = 0; j < 4; ++j) o.g_log_std[j] = loss[4 + j] - ent_coef;
+        o.stats[0] = pl + ent_coef * el + vf_coef * vl;
+        o.stats[1] = pl;
+        o.stats[2] = vl;
+        o.stats[3] = el;
+        o.stats[4] = loss[2] * inv_m;
+        o.stats[5] = loss[3] * inv_m;
+        o.stats[6] = part[(int64_t)nb * P + 0];
+        o.stats[7] = part[(int64_t)nb * P + 1];
+    }
+}
+
+inline int head_blocks(int64_t m) {
+    const int64_t b = (m + 63) / 64;  // >= 16 rows per wave
+    return (int)(b < 512 ? b : 512);
 }
 
 // ---------------------------------------------------------------------------
@@ -663,6 +970,98 @@ int dr_clip_adam(int64_t n, float *params, float *grads, float *exp_avg, float *
                        (float)b2, (float)(1.0 - b2), step_size, bc2_sqrt, (float)eps,
                        grad_norm_out);
     return check_launch("dr_clip_adam");
+}
+
+
+int dr_linear_tanh(int64_t m, int64_t k, int64_t n, const float *x, const float *w,
+                   const float *b, float *h, void *stream) {
+    if (m < 1 || !x || !w || !b || !h || n < 4 || n > 256 || (n & 3))
+        return fail0(DR_ERR_INVALID, "dr_linear_tanh: bad arguments (need 4 <= n <= 256, n % 4 == 0)");
+    if ((((uintptr_t)h) & 15))
+        return fail0(DR_ERR_INVALID, "dr_linear_tanh: h must be 16-byte aligned");
+    const int nb = head_blocks(m);
+    hipStream_t st = as_stream(stream);
+    switch (k) {
+#define DR_LT_CASE(K)                                                                      \
+    case K:                                                                                \
+        hipLaunchKernelGGL(linear_tanh_kernel<K>, dim3(nb), dim3(kBlock), 0, st, m, (int)n, \
+                           x, w, b, h);                                                    \
+        break;
+        DR_LT_CASE(4) DR_LT_CASE(8) DR_LT_CASE(12) DR_LT_CASE(15) DR_LT_CASE(16)
+        DR_LT_CASE(18) DR_LT_CASE(24) DR_LT_CASE(32)
+#undef DR_LT_CASE
+        default:
+            return fail0(DR_ERR_UNSUPPORTED,
+                         "dr_linear_tanh: k must be one of 4, 8, 12, 15, 16, 18, 24, 32");
+    }
+    return check_launch("dr_linear_tanh");
+}
+
+int dr_policy_heads(int64_t m, int64_t hd, const float *h_pi, const float *h_vf,
+                    const float *w_act, const float *b_act, const float *w_val,
+                    const float *b_val, float *mean, float *value, void *stream) {
+    if (m < 1 || hd < 4 || hd > 256 || (hd & 3) || !h_pi || !h_vf || !w_act || !b_act ||
+        !w_val || !b_val || !mean || !value)
+        return fail0(DR_ERR_INVALID, "dr_policy_heads: bad arguments");
+    if ((((uintptr_t)h_pi) | ((uintptr_t)h_vf) | ((uintptr_t)w_act) | ((uintptr_t)w_val) |
+         ((uintptr_t)mean)) & 15)
+        return fail0(DR_ERR_INVALID, "dr_policy_heads: buffers must be 16-byte aligned");
+    hipLaunchKernelGGL(policy_heads_kernel, dim3(head_blocks(m)), dim3(kBlock), 0,
+                       as_stream(stream), m, (int)hd, h_pi, h_vf, w_act, b_act, w_val, b_val,
+                       reinterpret_cast<float4 *>(mean), value);
+    return check_launch("dr_policy_heads");
+}
+
+size_t dr_ppo_head_workspace_bytes(int64_t m, int64_t hd) {
+    const int64_t nb = (m + kBlock - 1) / kBlock;
+    const int64_t P = kHeadFixed + 7 * hd;
+    return align_up(sizeof(float) * 3 * nb) +
+           align_up(sizeof(float) * (size_t)(head_blocks(m > 0 ? m : 1) * P + 2));
+}
+
+int dr_ppo_head_loss_backward(int64_t m, int64_t hd, const float *h_pi, const float *h_vf,
+                              const float *w_act, const float *b_act, const float *w_val,
+                              const float *b_val, const float *log_std, const float *actions,
+                              const float *aux, float clip_range, float ent_coef,
+                              float vf_coef, int normalize_advantage, float *gz_pi,
+                              float *gz_vf, float *g_w_act, float *g_b_act, float *g_w_val,
+                              float *g_b_val, float *g_b_pi, float *g_b_vf, float *g_log_std,
+                              float *stats, void *workspace, size_t workspace_bytes,
+                              void *stream) {
+    if (m < 1 || hd < 4 || hd > 256 || (hd & 3) || !h_pi || !h_vf || !w_act || !b_act ||
+        !w_val || !b_val || !log_std || !actions || !aux || !gz_pi || !gz_vf || !g_w_act ||
+        !g_b_act || !g_w_val || !g_b_val || !g_b_pi || !g_b_vf || !g_log_std || !stats)
+        return fail0(DR_ERR_INVALID, "dr_ppo_head_loss_backward: bad arguments");
+    if ((((uintptr_t)h_pi) | ((uintptr_t)h_vf) | ((uintptr_t)w_act) | ((uintptr_t)w_val) |
+         ((uintptr_t)actions) | ((uintptr_t)gz_pi) | ((uintptr_t)gz_vf)) & 15)
+        return fail0(DR_ERR_INVALID,
+                     "dr_ppo_head_loss_backward: row buffers must be 16-byte aligned");
+    if (!workspace || workspace_bytes < dr_ppo_head_workspace_bytes(m, hd))
+        return fail0(DR_ERR_INVALID, "dr_ppo_head_loss_backward: workspace too small");
+    const int norm = normalize_advantage && m > 1;
+    const int anb = (int)grid_for(m);
+    float *adv_part = static_cast<float *>(workspace);
+    float *part = reinterpret_cast<float *>(static_cast<char *>(workspace) +
+                                            align_up(sizeof(float) * 3 * anb));
+    hipStream_t st = as_stream(stream);
+    if (norm) {
+        hipLaunchKernelGGL(adv_stats_kernel, dim3(anb), dim3(kBlock), 0, st, m, aux + 1,
+                           (int64_t)3, adv_part);
+        int rc = check_launch("dr_ppo_head_loss_backward stats");
+        if (rc) return rc;
+    }
+    const int nb = head_blocks(m);
+    const int P = kHeadFixed + 7 * (int)hd;
+    HeadArgs a{m, (int)hd, h_pi, h_vf, w_act, b_act, w_val, b_val, log_std,
+               reinterpret_cast<const float4 *>(actions), aux, clip_range, ent_coef,
+               vf_coef, norm, adv_part, anb, gz_pi, gz_vf, part, P};
+    hipLaunchKernelGGL(ppo_head_kernel, dim3(nb), dim3(kBlock), sizeof(float) * 4 * P, st, a);
+    int rc = check_launch("dr_ppo_head_loss_backward");
+    if (rc) return rc;
+    HeadOut o{g_w_act, g_b_act, g_w_val, g_b_val, g_b_pi, g_b_vf, g_log_std, stats};
+    hipLaunchKernelGGL(ppo_head_finish_kernel, dim3((P + kBlock - 1) / kBlock), dim3(kBlock),
+                       0, st, nb, P, (int)hd, m, part, log_std, ent_coef, vf_coef, o);
+    return check_launch("dr_ppo_head_loss_backward finish");
 }
 
 }  // extern "C"

@@ -201,6 +201,52 @@ class FusedTrainStep:
         a, b, shape = self.pol.offsets[name]
         return self.grad[a:b].view(shape)
 
+    # ------------------------------------------------- fused minibatch step
+    def fusable(self) -> bool:
+        return fusable(self.pol)
+
+    def _alloc_fused(self):
+        if getattr(self, "_acts", None) is not None:
+            return
+        pol, M = self.pol, self.m
+        f32 = dict(dtype=torch.float32, device=pol.device)
+        self._acts = {pre: [torch.empty(M, n, **f32) for n in pol.net_arch]
+                      for pre in ("pi", "vf")}
+        self._gzt = {pre: torch.empty(M, pol.net_arch[-1], **f32) for pre in ("pi", "vf")}
+
+    @torch.no_grad()
+    def step(self, obs, actions, aux, head):
+        """One PPO.train minibatch on the fused path: hidden forward
+        (dr_linear_tanh for the first layer, hipBLASLt addmm + tanh above),
+        dr_ppo_head_loss_backward (heads, loss, backward through the heads
+        and top tanh, head / top-bias / log_std gradients), then per MLP the
+        split-K weight gradients, grad_h = grad_z W and dr_tanh_backward down
+        the stack.  Returns (flat grad, stats (8))."""
+        self._alloc_fused()
+        pol, M = self.pol, obs.shape[0]
+        depth, top = len(pol.net_arch), len(pol.net_arch) - 1
+        hs = hidden_forward(pol, obs, self._acts)
+        stats = head(hs["pi"][top], hs["vf"][top], pol.p("action.w"), pol.p("action.b"),
+                     pol.p("value.w"), pol.p("value.b"), pol.log_std, actions, aux,
+                     self._gzt["pi"], self._gzt["vf"], self.gview("action.w"),
+                     self.gview("action.b"), self.gview("value.w"), self.gview("value.b"),
+                     self.gview(f"pi{top}.b"), self.gview(f"vf{top}.b"),
+                     self.gview("log_std"))
+        for pre in ("pi", "vf"):
+            gz = self._gzt[pre]
+            h = hs[pre]
+            for k in reversed(range(depth)):
+                x = h[k - 1] if k > 0 else obs
+                self._wgrad(gz, x, self.gview(f"{pre}{k}.w"))
+                if k > 0:
+                    n_in = x.shape[1]
+                    g = self._g[:M * n_in].view(M, n_in)
+                    torch.mm(gz, pol.p(f"{pre}{k}.w"), out=g)
+                    gz = self._gz[:M * n_in].view(M, n_in)
+                    self.K.tanh_backward(g, h[k - 1], gz, self.gview(f"{pre}{k - 1}.b"),
+                                         self.tanh_ws)
+        return self.grad, stats
+
     @torch.no_grad()
     def forward(self, obs):
         pol = self.pol
@@ -253,3 +299,56 @@ class FusedTrainStep:
                     torch.mm(gz, pol.p(f"{pre}{k}.w"), out=g)
         self.gview("log_std").copy_(g_log_std)
         return self.grad
+
+
+def fusable(pol: ActorCritic) -> bool:
+    """The fused MLP kernels cover widths % 4 == 0 up to 256, the obs
+    widths of dr_linear_tanh and the 4-d action head."""
+    from .ppo_kernels import LINEAR_TANH_K
+    return (all(n % 4 == 0 and n <= 256 for n in pol.net_arch) and
+            pol.obs_dim in LINEAR_TANH_K and pol.act_dim == 4)
+
+
+@torch.no_grad()
+def hidden_forward(pol: ActorCritic, obs, acts):
+    """Hidden activations of the pi and vf MLPs into preallocated buffers
+    acts[pre][k] (M, net_arch[k])."""
+    from . import ppo_kernels as K
+    out = {}
+    for pre in ("pi", "vf"):
+        x, hs = obs, []
+        for k in range(len(pol.net_arch)):
+            h = acts[pre][k]
+            if k == 0:
+                K.linear_tanh(x, pol.p(f"{pre}0.w"), pol.p(f"{pre}0.b"), h)
+            else:
+                torch.addmm(pol.p(f"{pre}{k}.b"), x, pol.p(f"{pre}{k}.w").t(), out=h)
+                torch.tanh_(h)
+            hs.append(h)
+            x = h
+        out[pre] = hs
+    return out
+
+
+class PolicyInference:
+    """Rollout forward for a fixed batch of n observations on the fused
+    kernels: returns (mean (n,4), value (n,)) in reused buffers.  Uses the
+    same kernels as FusedTrainStep.step, so the rollout's log-probs and the
+    first training epoch see identical network outputs."""
+
+    def __init__(self, pol: ActorCritic, n: int):
+        self.pol, self.n = pol, n
+        f32 = dict(dtype=torch.float32, device=pol.device)
+        self.acts = {pre: [torch.empty(n, w, **f32) for w in pol.net_arch]
+                     for pre in ("pi", "vf")}
+        self.mean = torch.empty(n, pol.act_dim, **f32)
+        self.value = torch.empty(n, **f32)
+
+    @torch.no_grad()
+    def __call__(self, obs):
+        from . import ppo_kernels as K
+        pol = self.pol
+        hs = hidden_forward(pol, obs, self.acts)
+        K.policy_heads(hs["pi"][-1], hs["vf"][-1], pol.p("action.w"), pol.p("action.b"),
+                       pol.p("value.w"), pol.p("value.b"), self.mean, self.value)
+        return self.mean, self.value

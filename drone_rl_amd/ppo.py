@@ -33,7 +33,7 @@ import torch
 from . import dist as D
 from . import ppo_kernels as K
 from .env import MOTOR_MAX, DroneBatch
-from .policy import ActorCritic, FusedTrainStep
+from .policy import ActorCritic, FusedTrainStep, PolicyInference, fusable
 
 
 @dataclasses.dataclass
@@ -108,6 +108,13 @@ class PPOTrainer:
         self.loss = K.PPOLoss(M, dev, cfg.clip_range, cfg.ent_coef, cfg.vf_coef,
                               cfg.normalize_advantage)
         self.fused = FusedTrainStep(self.policy, M)
+        # fused MLP path (first-layer linear+tanh, heads+loss+head backward)
+        # when the architecture fits the kernels; else forward/loss/backward
+        self.use_fused = fusable(self.policy)
+        if self.use_fused:
+            self.head = K.HeadLossBackward(M, cfg.net_arch[-1], dev, cfg.clip_range,
+                                           cfg.ent_coef, cfg.vf_coef, cfg.normalize_advantage)
+            self.infer = PolicyInference(self.policy, N)
         self.num_updates = 0
         self.num_timesteps = 0
         self._rolled = False
@@ -131,8 +138,9 @@ class PPOTrainer:
         self.dones[0].copy_(self.dones[T])          # episode_starts of step 0
         self._rolled = True
         ls = self.policy.log_std
+        fwd = self.infer if self.use_fused else self.policy
         for t in range(T):
-            mean, value = self.policy(self.obs[t])
+            mean, value = fwd(self.obs[t])
             self.values[t].copy_(value)
             K.policy_sample(mean, ls, seed=cfg.seed * 7919 + self.rank,
                             counter=self.num_updates * T + t, lo=0.0, hi=MOTOR_MAX,
@@ -143,7 +151,7 @@ class PPOTrainer:
             self.env.ep_len = self.ep_len[t]
             self.env.step(self.act_env, obs_out=self.obs[t + 1], rew_out=self.rewards[t],
                           done_out=self.dones[t + 1])
-        _, last_values = self.policy(self.obs[T])
+        _, last_values = fwd(self.obs[T])
         K.gae(self.rewards, self.values, self.dones[:T], last_values, self.dones[T],
               cfg.gamma, cfg.gae_lambda, advantages=self.adv, returns=self.ret)
         torch.stack([self.logp.reshape(-1), self.adv.reshape(-1), self.ret.reshape(-1)],
@@ -168,10 +176,14 @@ class PPOTrainer:
                 K.gather_rows(idx, obs_flat, out=self.mb_obs)
                 K.gather_rows(idx, act_flat, out=self.mb_act)
                 K.gather_rows(idx, self.aux, out=self.mb_aux)
-                mean, value, cache = self.fused.forward(self.mb_obs)
-                g_mean, g_ls, g_v, st = self.loss(mean, log_std, value, self.mb_act,
-                                                  aux=self.mb_aux)
-                grad = self.fused.backward(self.mb_obs, cache, g_mean, g_v, g_ls)
+                if self.use_fused:
+                    grad, st = self.fused.step(self.mb_obs, self.mb_act, self.mb_aux,
+                                               self.head)
+                else:
+                    mean, value, cache = self.fused.forward(self.mb_obs)
+                    g_mean, g_ls, g_v, st = self.loss(mean, log_std, value, self.mb_act,
+                                                      aux=self.mb_aux)
+                    grad = self.fused.backward(self.mb_obs, cache, g_mean, g_v, g_ls)
                 self._allreduce_grad(grad)
                 self.opt.step(grad)
                 stats[j].copy_(st)

@@ -157,3 +157,50 @@ class ClipAdam:
             float(self.eps), float(self.max_norm), self.t, ptr(self.grad_norm),
             ptr(self.ws), self.ws.numel(), _s(self.p)))
         return self.grad_norm
+
+
+LINEAR_TANH_K = (4, 8, 12, 15, 16, 18, 24, 32)
+
+
+def linear_tanh(x, w, b, out):
+    """out = tanh(x w^T + b) for a narrow input x (m,k), k in LINEAR_TANH_K."""
+    m, k = x.shape
+    n = w.shape[0]
+    check(_lib.lib().dr_linear_tanh(m, k, n, ptr(_f32(x)), ptr(_f32(w)), ptr(_f32(b)),
+                                    ptr(out), _s(x)))
+    return out
+
+
+def policy_heads(h_pi, h_vf, w_act, b_act, w_val, b_val, mean, value):
+    """mean (m,4) = h_pi w_act^T + b_act, value (m) = h_vf w_val^T + b_val."""
+    m, hd = h_pi.shape
+    check(_lib.lib().dr_policy_heads(m, hd, ptr(_f32(h_pi)), ptr(_f32(h_vf)), ptr(_f32(w_act)),
+                                     ptr(_f32(b_act)), ptr(_f32(w_val)), ptr(_f32(b_val)),
+                                     ptr(mean), ptr(value), _s(h_pi)))
+    return mean, value
+
+
+class HeadLossBackward:
+    """dr_ppo_head_loss_backward: heads + PPO loss + backward through the
+    heads and the top tanh of both MLPs, one minibatch of m rows."""
+
+    def __init__(self, m: int, hd: int, device, clip_range=0.2, ent_coef=0.0, vf_coef=0.5,
+                 normalize_advantage=True):
+        self.m, self.hd = m, hd
+        self.clip, self.ent, self.vf = clip_range, ent_coef, vf_coef
+        self.norm = int(bool(normalize_advantage))
+        self.ws = torch.empty(_lib.lib().dr_ppo_head_workspace_bytes(m, hd), dtype=torch.uint8,
+                              device=device)
+        self.stats = torch.empty(8, dtype=torch.float32, device=device)
+
+    def __call__(self, h_pi, h_vf, w_act, b_act, w_val, b_val, log_std, actions, aux,
+                 gz_pi, gz_vf, g_w_act, g_b_act, g_w_val, g_b_val, g_b_pi, g_b_vf, g_log_std):
+        assert h_pi.shape == (self.m, self.hd) and aux.shape == (self.m, 3)
+        check(_lib.lib().dr_ppo_head_loss_backward(
+            self.m, self.hd, ptr(_f32(h_pi)), ptr(_f32(h_vf)), ptr(_f32(w_act)),
+            ptr(_f32(b_act)), ptr(_f32(w_val)), ptr(_f32(b_val)), ptr(_f32(log_std)),
+            ptr(_f32(actions)), ptr(_f32(aux)), float(self.clip), float(self.ent),
+            float(self.vf), self.norm, ptr(gz_pi), ptr(gz_vf), ptr(g_w_act), ptr(g_b_act),
+            ptr(g_w_val), ptr(g_b_val), ptr(g_b_pi), ptr(g_b_vf), ptr(g_log_std),
+            ptr(self.stats), ptr(self.ws), self.ws.numel(), _s(h_pi)))
+        return self.stats

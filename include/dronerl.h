@@ -231,6 +231,47 @@ int dr_tanh_backward(int64_t m, int64_t n, const float *grad_h, const float *h,
                      float *grad_z, float *bias_grad, void *workspace,
                      size_t workspace_bytes, void *stream);
 
+/* First MLP layer forward fused with its activation: h = tanh(x W^T + b)
+   for x (m,k), W (n,k), b (n), h (m,n) (SB3 MlpExtractor's Linear + Tanh,
+   the narrow-input layer).  k in {4,8,12,15,16,18,24,32}; n % 4 == 0,
+   n <= 256; h 16-byte aligned.  Replaces an addmm plus a separate tanh pass
+   over the (m,n) activation. */
+int dr_linear_tanh(int64_t m, int64_t k, int64_t n, const float *x,
+                   const float *w, const float *b, float *h, void *stream);
+
+/* Policy heads for rollouts (ActorCriticPolicy.forward's action_net /
+   value_net): mean (m,4) = h_pi W_act^T + b_act, value (m) = h_vf W_val^T +
+   b_val, for the top hidden activations h_pi, h_vf (m,hd), hd % 4 == 0,
+   hd <= 256.  Row buffers 16-byte aligned. */
+int dr_policy_heads(int64_t m, int64_t hd, const float *h_pi, const float *h_vf,
+                    const float *w_act, const float *b_act, const float *w_val,
+                    const float *b_val, float *mean, float *value, void *stream);
+
+/* One PPO.train minibatch step from the top hidden layer down, fused:
+   heads (as dr_policy_heads), the loss of dr_ppo_loss (aux = interleaved
+   (m,3) rows of old_logp, advantage, return), and the backward through the
+   heads and the top tanh:
+     gz_pi = (dL/dmean W_act) * (1 - h_pi^2),  gz_vf = (dL/dvalue W_val) *
+     (1 - h_vf^2)   (m,hd) each, for the hidden-layer backward,
+   plus the gradients of W_act (4,hd), b_act (4), W_val (1,hd), b_val (1),
+   the top hidden biases b_pi, b_vf (hd) and log_std (4), and stats (8) as
+   dr_ppo_loss.  Gradient outputs are written (not accumulated); they may be
+   views into one flat gradient buffer.  Deterministic (fixed-order partial
+   sums).  `workspace` >= dr_ppo_head_workspace_bytes(m, hd). */
+size_t dr_ppo_head_workspace_bytes(int64_t m, int64_t hd);
+int dr_ppo_head_loss_backward(int64_t m, int64_t hd, const float *h_pi,
+                              const float *h_vf, const float *w_act,
+                              const float *b_act, const float *w_val,
+                              const float *b_val, const float *log_std,
+                              const float *actions, const float *aux,
+                              float clip_range, float ent_coef, float vf_coef,
+                              int normalize_advantage, float *gz_pi,
+                              float *gz_vf, float *g_w_act, float *g_b_act,
+                              float *g_w_val, float *g_b_val, float *g_b_pi,
+                              float *g_b_vf, float *g_log_std, float *stats,
+                              void *workspace, size_t workspace_bytes,
+                              void *stream);
+
 /* Fused PPO loss + gradient of the loss w.r.t. the policy head outputs
    (PPO.train: normalised advantage, ratio/clip surrogate, value MSE,
    entropy).  Inputs for a minibatch of m rows:

@@ -182,3 +182,67 @@ def test_fused_train_step_matches_autograd():
         lo, hi, _ = pol.offsets[name]
         scale = ref[lo:hi].abs().max().item() + 1e-12
         assert (grad[lo:hi] - ref[lo:hi]).abs().max().item() <= 1e-4 * scale, name
+
+
+@pytest.mark.parametrize("k,n", [(15, 256), (12, 64), (18, 128)])
+def test_linear_tanh_matches_torch(k, n):
+    from drone_rl_amd import ppo_kernels as K
+    m = 5001
+    x = torch.randn(m, k, device="cuda")
+    w = torch.randn(n, k, device="cuda") * 0.4
+    b = torch.randn(n, device="cuda") * 0.1
+    h = torch.empty(m, n, device="cuda")
+    K.linear_tanh(x, w, b, h)
+    ref = torch.tanh(torch.addmm(b, x, w.t()))
+    assert (h - ref).abs().max().item() <= 2e-6
+
+
+def test_policy_heads_match_torch():
+    from drone_rl_amd import ppo_kernels as K
+    m, hd = 3001, 256
+    hp = torch.tanh(torch.randn(m, hd, device="cuda"))
+    hv = torch.tanh(torch.randn(m, hd, device="cuda"))
+    wa, ba = torch.randn(4, hd, device="cuda") * 0.1, torch.randn(4, device="cuda")
+    wv, bv = torch.randn(1, hd, device="cuda") * 0.1, torch.randn(1, device="cuda")
+    mean = torch.empty(m, 4, device="cuda")
+    value = torch.empty(m, device="cuda")
+    K.policy_heads(hp, hv, wa, ba, wv, bv, mean, value)
+    assert (mean - torch.addmm(ba, hp, wa.t())).abs().max().item() <= 1e-5
+    assert (value - torch.addmm(bv, hv, wv.t()).squeeze(1)).abs().max().item() <= 1e-5
+
+
+@pytest.mark.parametrize("arch,m", [((256, 256), 65536), ((64, 64), 64), ((64, 128), 1000)])
+def test_fused_step_matches_unfused_path(arch, m):
+    """FusedTrainStep.step (first-layer linear+tanh kernel, heads + loss +
+    head backward kernel) == forward -> dr_ppo_loss -> hand backward, to f32
+    summation-order noise; two runs are bitwise identical."""
+    from drone_rl_amd import ppo_kernels as K
+    from drone_rl_amd.policy import ActorCritic, FusedTrainStep
+    torch.manual_seed(1)
+    pol = ActorCritic(15, 4, arch, device="cuda", seed=4)
+    with torch.no_grad():
+        pol.flat.mul_(3.0)              # non-trivial heads / log_std
+    obs = torch.randn(m, 15, device="cuda")
+    fs = FusedTrainStep(pol, m)
+    with torch.no_grad():
+        mean, value, cache = fs.forward(obs)
+        d = torch.distributions.Normal(mean, pol.log_std.exp())
+        act = d.sample()
+        aux = torch.stack([d.log_prob(act).sum(1) + 0.1 * torch.randn(m, device="cuda"),
+                           torch.randn(m, device="cuda"), torch.randn(m, device="cuda")], 1)
+    L = K.PPOLoss(m, "cuda", 0.2, 0.01, 0.5, True)
+    g_mean, g_ls, g_v, st = L(mean, pol.log_std.detach(), value, act, aux=aux)
+    ref = fs.backward(obs, cache, g_mean, g_v, g_ls).clone()
+    st_ref = st.clone()
+    head = K.HeadLossBackward(m, arch[-1], "cuda", 0.2, 0.01, 0.5, True)
+    grad, st2 = fs.step(obs, act, aux, head)
+    grad = grad.clone()
+    for name, _, _ in pol.layout:
+        lo, hi, _ = pol.offsets[name]
+        scale = ref[lo:hi].abs().max().item() + 1e-12
+        # + an absolute floor for sums that cancel (e.g. the value bias: 65k
+        # terms of ~3e-5 summing to ~2e-5 in a different order)
+        assert (grad[lo:hi] - ref[lo:hi]).abs().max().item() <= 2e-4 * scale + 1e-7, name
+    assert torch.allclose(st2, st_ref, rtol=1e-4, atol=1e-6)
+    grad2, _ = fs.step(obs, act, aux, head)
+    assert torch.equal(grad, grad2)
