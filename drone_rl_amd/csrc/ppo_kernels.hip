@@ -476,6 +476,26 @@ __device__ inline float wave_allsum(float x) {
            __int_as_float(__builtin_amdgcn_readlane(__float_as_int(x), 32));
 }
 
+// Branch-free f32 tanh (<= 2 ulp): odd Taylor polynomial through x^15 for
+// |x| < 0.55 (truncation < 0.5 ulp there), 1 - 2 / (e^{2|x|} + 1) above
+// (hardware exp2 / rcp, the cancellation costs <= 2 ulp at the switch),
+// sign restored; NaN propagates, +-inf -> +-1.  The device library's tanhf
+// branches per element, which costs ~3x the instructions in a wave.
+__device__ inline float tanh_fast(float x) {
+    const float ax = fabsf(x);
+    const float z = ax * ax;
+    float p = fmaf(z, -929569.0f / 638512875.0f, 21844.0f / 6081075.0f);
+    p = fmaf(z, p, -1382.0f / 155925.0f);
+    p = fmaf(z, p, 62.0f / 2835.0f);
+    p = fmaf(z, p, -17.0f / 315.0f);
+    p = fmaf(z, p, 2.0f / 15.0f);
+    p = fmaf(z, p, -1.0f / 3.0f);
+    const float small = fmaf(ax * z, p, ax);
+    const float e = __builtin_amdgcn_exp2f(ax * 2.8853900817779268f);  // e^{2|x|}
+    const float large = fmaf(-2.0f, __builtin_amdgcn_rcpf(e + 1.0f), 1.0f);
+    return copysignf(ax < 0.55f ? small : large, x);
+}
+
 __device__ inline float4 ld4(const float *p) { return *reinterpret_cast<const float4 *>(p); }
 __device__ inline float dot4(float4 a, float4 b) {
     return fmaf(a.w, b.w, fmaf(a.z, b.z, fmaf(a.y, b.y, a.x * b.x)));
@@ -493,15 +513,37 @@ __global__ __launch_bounds__(kBlock) void linear_tanh_kernel(int64_t m, int n,
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     const int c0 = 4 * lane;
     const bool act = c0 < n;
+    // this lane's 4 weight rows are 4K contiguous floats: K float4 loads
+    // (the flat parameter layout keeps every weight 16-byte aligned; the
+    // ABI checks it)
     float wr[4][K], bb[4];
+    {
+        const float4 *w4 = reinterpret_cast<const float4 *>(w + (act ? c0 : 0) * K);
+        float flat[4 * K];
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-        bb[q] = act ? b[c0 + q] : 0.f;
+        for (int t = 0; t < K; ++t) {
+            const float4 v4 = w4[t];
+            flat[4 * t + 0] = v4.x;
+            flat[4 * t + 1] = v4.y;
+            flat[4 * t + 2] = v4.z;
+            flat[4 * t + 3] = v4.w;
+        }
 #pragma unroll
-        for (int k = 0; k < K; ++k) wr[q][k] = act ? w[(c0 + q) * K + k] : 0.f;
+        for (int q = 0; q < 4; ++q) {
+            bb[q] = act ? b[c0 + q] : 0.f;
+#pragma unroll
+            for (int k = 0; k < K; ++k) wr[q][k] = flat[q * K + k];
+        }
     }
-    for (int64_t r = (int64_t)blockIdx.x * 4 + wid; r < m; r += (int64_t)gridDim.x * 4) {
-        const float xv = lane < K ? x[r * K + lane] : 0.f;
+    // rows are wave-strided; the next row's input is loaded before this
+    // row's arithmetic (software pipelining hides the load latency)
+    const int64_t stride = (int64_t)gridDim.x * 4;
+    int64_t r = (int64_t)blockIdx.x * 4 + wid;
+    float xnext = (r < m && lane < K) ? x[r * K + lane] : 0.f;
+    for (; r < m; r += stride) {
+        const float xv = xnext;
+        const int64_t rn = r + stride;
+        xnext = (rn < m && lane < K) ? x[rn * K + lane] : 0.f;
         float acc[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int k = 0; k < K; ++k) {
@@ -511,8 +553,8 @@ __global__ __launch_bounds__(kBlock) void linear_tanh_kernel(int64_t m, int n,
         }
         if (act)
             *reinterpret_cast<float4 *>(h + r * n + c0) =
-                make_float4(tanhf(acc[0] + bb[0]), tanhf(acc[1] + bb[1]),
-                            tanhf(acc[2] + bb[2]), tanhf(acc[3] + bb[3]));
+                make_float4(tanh_fast(acc[0] + bb[0]), tanh_fast(acc[1] + bb[1]),
+                            tanh_fast(acc[2] + bb[2]), tanh_fast(acc[3] + bb[3]));
     }
 }
 
@@ -573,6 +615,13 @@ struct HeadArgs {
     int P;
 };
 
+// Rows are processed in tiles of kHeadTile per wave: the tile's activations
+// stay in registers, the 5 head dot products per row are wave reductions,
+// the row results are parked one row per lane, the PPO row loss runs once
+// for the whole tile lane-parallel, and the per-row gradients come back by
+// v_readlane for the backward through the heads and the top tanh.
+constexpr int kHeadTile = 8;
+
 __global__ __launch_bounds__(kBlock) void ppo_head_kernel(HeadArgs a) {
     extern __shared__ float sh_part[];  // 4 * P
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
@@ -593,52 +642,91 @@ __global__ __launch_bounds__(kBlock) void ppo_head_kernel(HeadArgs a) {
     const float4 wv = act ? ld4(a.w_val + c0) : z4;
     const float ba[4] = {a.b_act[0], a.b_act[1], a.b_act[2], a.b_act[3]};
     const float bv = a.b_val[0];
+    // lane-partial sums of the loss terms and of d b_act / d b_val
     float u[kHeadFixed];
 #pragma unroll
     for (int k = 0; k < kHeadFixed; ++k) u[k] = 0.f;
     float sbp[4] = {0.f, 0.f, 0.f, 0.f}, sbv[4] = {0.f, 0.f, 0.f, 0.f};
     float swa[4][4] = {}, swv[4] = {0.f, 0.f, 0.f, 0.f};
-    for (int64_t r = (int64_t)blockIdx.x * 4 + wid; r < a.m; r += (int64_t)gridDim.x * 4) {
-        const float4 hp4 = act ? ld4(a.h_pi + r * hd + c0) : z4;
-        const float4 hv4 = act ? ld4(a.h_vf + r * hd + c0) : z4;
-        float mu[4];
+    const float wq[4][4] = {{wa[0].x, wa[0].y, wa[0].z, wa[0].w},
+                            {wa[1].x, wa[1].y, wa[1].z, wa[1].w},
+                            {wa[2].x, wa[2].y, wa[2].z, wa[2].w},
+                            {wa[3].x, wa[3].y, wa[3].z, wa[3].w}};
+    const float wvq[4] = {wv.x, wv.y, wv.z, wv.w};
+    const int64_t nwaves = (int64_t)gridDim.x * 4;
+    for (int64_t tile = (int64_t)blockIdx.x * 4 + wid; tile * kHeadTile < a.m; tile += nwaves) {
+        const int64_t r0 = tile * kHeadTile;
+        const int nr = (int)min((int64_t)kHeadTile, a.m - r0);
+        float4 hp[kHeadTile], hv[kHeadTile];
 #pragma unroll
-        for (int j = 0; j < 4; ++j) mu[j] = wave_allsum(dot4(hp4, wa[j])) + ba[j];
-        const float v = wave_allsum(dot4(hv4, wv)) + bv;
-        const float4 ac4 = a.actions[r];
-        const float ac[4] = {ac4.x, ac4.y, ac4.z, ac4.w};
-        float gm[4], gv;
-        ppo_row(c, mu, ac, a.aux[3 * r], a.aux[3 * r + 1], a.aux[3 * r + 2], v, gm, gv, u);
-#pragma unroll
-        for (int j = 0; j < 4; ++j) u[9 + j] += gm[j];
-        u[13] += gv;
-        const float hp[4] = {hp4.x, hp4.y, hp4.z, hp4.w};
-        const float hv[4] = {hv4.x, hv4.y, hv4.z, hv4.w};
-        const float wq[4][4] = {{wa[0].x, wa[0].y, wa[0].z, wa[0].w},
-                                {wa[1].x, wa[1].y, wa[1].z, wa[1].w},
-                                {wa[2].x, wa[2].y, wa[2].z, wa[2].w},
-                                {wa[3].x, wa[3].y, wa[3].z, wa[3].w}};
-        const float wvq[4] = {wv.x, wv.y, wv.z, wv.w};
-        float gzp[4], gzv[4];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const float gh = fmaf(gm[3], wq[3][q], fmaf(gm[2], wq[2][q],
-                                  fmaf(gm[1], wq[1][q], gm[0] * wq[0][q])));
-            gzp[q] = gh * (1.0f - hp[q] * hp[q]);
-            gzv[q] = (gv * wvq[q]) * (1.0f - hv[q] * hv[q]);
-            sbp[q] += gzp[q];
-            sbv[q] += gzv[q];
-#pragma unroll
-            for (int j = 0; j < 4; ++j) swa[j][q] = fmaf(gm[j], hp[q], swa[j][q]);
-            swv[q] = fmaf(gv, hv[q], swv[q]);
+        for (int i = 0; i < kHeadTile; ++i) {
+            const bool ok = act && i < nr;
+            hp[i] = ok ? ld4(a.h_pi + (r0 + i) * hd + c0) : z4;
+            hv[i] = ok ? ld4(a.h_vf + (r0 + i) * hd + c0) : z4;
         }
-        if (act) {
-            *reinterpret_cast<float4 *>(a.gz_pi + r * hd + c0) =
-                make_float4(gzp[0], gzp[1], gzp[2], gzp[3]);
-            *reinterpret_cast<float4 *>(a.gz_vf + r * hd + c0) =
-                make_float4(gzv[0], gzv[1], gzv[2], gzv[3]);
+        // this lane's row (lane < nr): its loss inputs, loaded while the dots run
+        const bool own = lane < nr;
+        const int64_t ro = r0 + (own ? lane : 0);
+        const float4 ac4 = a.actions[ro];
+        const float lp_old = a.aux[3 * ro], A = a.aux[3 * ro + 1], R = a.aux[3 * ro + 2];
+        float mu[4] = {0.f, 0.f, 0.f, 0.f}, v = 0.f;
+#pragma unroll
+        for (int i = 0; i < kHeadTile; ++i) {
+            const float m0 = wave_allsum(dot4(hp[i], wa[0])) + ba[0];
+            const float m1 = wave_allsum(dot4(hp[i], wa[1])) + ba[1];
+            const float m2 = wave_allsum(dot4(hp[i], wa[2])) + ba[2];
+            const float m3 = wave_allsum(dot4(hp[i], wa[3])) + ba[3];
+            const float vv = wave_allsum(dot4(hv[i], wv)) + bv;
+            const bool me = lane == i;
+            mu[0] = me ? m0 : mu[0];
+            mu[1] = me ? m1 : mu[1];
+            mu[2] = me ? m2 : mu[2];
+            mu[3] = me ? m3 : mu[3];
+            v = me ? vv : v;
+        }
+        float gm[4] = {0.f, 0.f, 0.f, 0.f}, gv = 0.f;
+        if (own) {
+            const float ac[4] = {ac4.x, ac4.y, ac4.z, ac4.w};
+            ppo_row(c, mu, ac, lp_old, A, R, v, gm, gv, u);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) u[9 + j] += gm[j];
+            u[13] += gv;
+        }
+#pragma unroll
+        for (int i = 0; i < kHeadTile; ++i) {
+            // rows past the end (last tile only) carry zero activations and
+            // zero gradients (gm, gv = 0 on lanes >= nr): no effect on sums
+            float g[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+                g[j] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(gm[j]), i));
+            const float gvi = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(gv), i));
+            const float hpq[4] = {hp[i].x, hp[i].y, hp[i].z, hp[i].w};
+            const float hvq[4] = {hv[i].x, hv[i].y, hv[i].z, hv[i].w};
+            float gzp[4], gzv[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const float gh = fmaf(g[3], wq[3][q], fmaf(g[2], wq[2][q],
+                                      fmaf(g[1], wq[1][q], g[0] * wq[0][q])));
+                gzp[q] = gh * (1.0f - hpq[q] * hpq[q]);
+                gzv[q] = (gvi * wvq[q]) * (1.0f - hvq[q] * hvq[q]);
+                sbp[q] += gzp[q];
+                sbv[q] += gzv[q];
+#pragma unroll
+                for (int j = 0; j < 4; ++j) swa[j][q] = fmaf(g[j], hpq[q], swa[j][q]);
+                swv[q] = fmaf(gvi, hvq[q], swv[q]);
+            }
+            if (act && i < nr) {
+                *reinterpret_cast<float4 *>(a.gz_pi + (r0 + i) * hd + c0) =
+                    make_float4(gzp[0], gzp[1], gzp[2], gzp[3]);
+                *reinterpret_cast<float4 *>(a.gz_vf + (r0 + i) * hd + c0) =
+                    make_float4(gzv[0], gzv[1], gzv[2], gzv[3]);
+            }
         }
     }
+    // the lane-partial scalars to wave totals (fixed butterfly order)
+#pragma unroll
+    for (int k = 0; k < kHeadFixed; ++k) u[k] = wave_allsum(u[k]);
     float *mine = sh_part + wid * a.P;
     if (lane == 0) {
 #pragma unroll
@@ -665,15 +753,34 @@ __global__ __launch_bounds__(kBlock) void ppo_head_kernel(HeadArgs a) {
     }
 }
 
-// Column sums of the head partials in a fixed order, scattered into the
-// gradient outputs; block 0 also forms the loss statistics.
+// Gradient outputs of the head step (finish kernel).
 struct HeadOut {
     float *g_w_act, *g_b_act, *g_w_val, *g_b_val, *g_b_pi, *g_b_vf, *g_log_std, *stats;
 };
 
+// Fixed-order column sums of row groups: out[g][p] = sum of in[b][p] over
+// b in [g*gsize, (g+1)*gsize); 8 independent accumulators per thread.
+__global__ __launch_bounds__(kBlock) void colsum_groups_kernel(int nb, int P, int gsize,
+                                                               const float *__restrict__ in,
+                                                               float *__restrict__ out) {
+    const int p = blockIdx.x * kBlock + threadIdx.x;
+    if (p >= P) return;
+    const int b0 = blockIdx.y * gsize;
+    const int b1 = min(nb, b0 + gsize);
+    float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    int b = b0;
+    for (; b + 7 < b1; b += 8) {
+#pragma unroll
+        for (int u = 0; u < 8; ++u) s[u] += in[(int64_t)(b + u) * P + p];
+    }
+    for (; b < b1; ++b) s[0] += in[(int64_t)b * P + p];
+    out[(int64_t)blockIdx.y * P + p] = ((s[0] + s[1]) + (s[2] + s[3])) + ((s[4] + s[5]) + (s[6] + s[7]));
+}
+
 __global__ __launch_bounds__(kBlock) void ppo_head_finish_kernel(
     int nb, int P, int hd, int64_t m, const float *__restrict__ part,
-    const float *__restrict__ log_std, float ent_coef, float vf_coef, HeadOut o) {
+    const float *__restrict__ adv_ms, const float *__restrict__ log_std, float ent_coef,
+    float vf_coef, HeadOut o) {
     __shared__ float loss[kLossK];
     const int p = blockIdx.x * kBlock + threadIdx.x;
     if (p < P) {
@@ -717,13 +824,15 @@ __global__ __launch_bounds__(kBlock) void ppo_head_finish_kernel(
         o.stats[3] = el;
         o.stats[4] = loss[2] * inv_m;
         o.stats[5] = loss[3] * inv_m;
-        o.stats[6] = part[(int64_t)nb * P + 0];
-        o.stats[7] = part[(int64_t)nb * P + 1];
+        o.stats[6] = adv_ms[0];
+        o.stats[7] = adv_ms[1];
     }
 }
 
+constexpr int kHeadGroups = 16;  // first-level row groups of the partial sums
+
 inline int head_blocks(int64_t m) {
-    const int64_t b = (m + 63) / 64;  // >= 16 rows per wave
+    const int64_t b = (m + 4 * kHeadTile - 1) / (4 * kHeadTile);  // >= 1 tile per wave
     return (int)(b < 512 ? b : 512);
 }
 
@@ -977,9 +1086,10 @@ int dr_linear_tanh(int64_t m, int64_t k, int64_t n, const float *x, const float 
                    const float *b, float *h, void *stream) {
     if (m < 1 || !x || !w || !b || !h || n < 4 || n > 256 || (n & 3))
         return fail0(DR_ERR_INVALID, "dr_linear_tanh: bad arguments (need 4 <= n <= 256, n % 4 == 0)");
-    if ((((uintptr_t)h) & 15))
-        return fail0(DR_ERR_INVALID, "dr_linear_tanh: h must be 16-byte aligned");
-    const int nb = head_blocks(m);
+    if ((((uintptr_t)h) | ((uintptr_t)w)) & 15)
+        return fail0(DR_ERR_INVALID, "dr_linear_tanh: h and w must be 16-byte aligned");
+    const int64_t nbl = (m + 63) / 64;    // >= 16 rows per wave
+    const int nb = (int)(nbl < 1024 ? nbl : 1024);
     hipStream_t st = as_stream(stream);
     switch (k) {
 #define DR_LT_CASE(K)                                                                      \
@@ -1016,7 +1126,8 @@ size_t dr_ppo_head_workspace_bytes(int64_t m, int64_t hd) {
     const int64_t nb = (m + kBlock - 1) / kBlock;
     const int64_t P = kHeadFixed + 7 * hd;
     return align_up(sizeof(float) * 3 * nb) +
-           align_up(sizeof(float) * (size_t)(head_blocks(m > 0 ? m : 1) * P + 2));
+           align_up(sizeof(float) * (size_t)(head_blocks(m > 0 ? m : 1) * P + 2)) +
+           align_up(sizeof(float) * (size_t)(kHeadGroups * P));
 }
 
 int dr_ppo_head_loss_backward(int64_t m, int64_t hd, const float *h_pi, const float *h_vf,
@@ -1058,9 +1169,19 @@ int dr_ppo_head_loss_backward(int64_t m, int64_t hd, const float *h_pi, const fl
     hipLaunchKernelGGL(ppo_head_kernel, dim3(nb), dim3(kBlock), sizeof(float) * 4 * P, st, a);
     int rc = check_launch("dr_ppo_head_loss_backward");
     if (rc) return rc;
+    // two-level fixed-order reduction of the nb x P partials
+    float *part2 = reinterpret_cast<float *>(
+        reinterpret_cast<char *>(part) + align_up(sizeof(float) * (size_t)(nb * P + 2)));
+    const int gsize = (nb + kHeadGroups - 1) / kHeadGroups;
+    const int ng = (nb + gsize - 1) / gsize;
+    hipLaunchKernelGGL(colsum_groups_kernel, dim3((P + kBlock - 1) / kBlock, ng), dim3(kBlock),
+                       0, st, nb, P, gsize, part, part2);
+    rc = check_launch("dr_ppo_head_loss_backward groups");
+    if (rc) return rc;
     HeadOut o{g_w_act, g_b_act, g_w_val, g_b_val, g_b_pi, g_b_vf, g_log_std, stats};
     hipLaunchKernelGGL(ppo_head_finish_kernel, dim3((P + kBlock - 1) / kBlock), dim3(kBlock),
-                       0, st, nb, P, (int)hd, m, part, log_std, ent_coef, vf_coef, o);
+                       0, st, ng, P, (int)hd, m, part2, part + (int64_t)nb * P, log_std,
+                       ent_coef, vf_coef, o);
     return check_launch("dr_ppo_head_loss_backward finish");
 }
 
