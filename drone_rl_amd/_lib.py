@@ -82,6 +82,9 @@ SIGNATURES = {
     "dr_tanh_backward_workspace_bytes": (c_size_t, [c_int64, c_int64]),
     "dr_tanh_backward": (c_int, [c_int64, c_int64, _P, _P, _P, _P, _P, c_size_t, _P]),
     "dr_linear_tanh": (c_int, [c_int64, c_int64, c_int64, _P, _P, _P, _P, _P]),
+    "dr_first_layer_backward_workspace_bytes": (c_size_t, [c_int64, c_int64, c_int64]),
+    "dr_first_layer_backward": (c_int, [c_int64, c_int64, c_int64, _P, _P, _P, _P, _P, _P,
+                                        c_size_t, _P]),
     "dr_policy_heads": (c_int, [c_int64, c_int64, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
     "dr_ppo_head_workspace_bytes": (c_size_t, [c_int64, c_int64]),
     "dr_ppo_head_loss_backward": (c_int, [c_int64, c_int64] + [_P] * 9 +

@@ -753,6 +753,100 @@ __global__ __launch_bounds__(kBlock) void ppo_head_kernel(HeadArgs a) {
     }
 }
 
+// Backward of the first (narrow-input) layer, fused: grad_z = grad_h *
+// (1 - h^2) is formed in registers and never stored; per-block partials of
+// d b = sum_r grad_z[r,:] and d W = grad_z^T x (n x K) are written instead.
+// Replaces tanh_backward (write of grad_z) + the split-K weight-gradient
+// GEMM (re-read of grad_z).  Tiles of kFirstTile rows per wave, loads first.
+// Partial layout per block (P = (K+1) n): [k*n + c] = dW[c][k], [K*n + c] = db[c].
+constexpr int kFirstTile = 8;
+
+template <int K>
+__global__ __launch_bounds__(kBlock) void first_layer_bwd_kernel(int64_t m, int n,
+                                                                 const float *__restrict__ gh,
+                                                                 const float *__restrict__ h,
+                                                                 const float *__restrict__ x,
+                                                                 float *__restrict__ part) {
+    extern __shared__ float sh_fl[];  // 4 * P
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const int c0 = 4 * lane;
+    const bool act = c0 < n;
+    const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
+    float aw[K][4], ab[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int k = 0; k < K; ++k)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) aw[k][q] = 0.f;
+    const int64_t nwaves = (int64_t)gridDim.x * 4;
+    for (int64_t tile = (int64_t)blockIdx.x * 4 + wid; tile * kFirstTile < m; tile += nwaves) {
+        const int64_t r0 = tile * kFirstTile;
+        const int nr = (int)min((int64_t)kFirstTile, m - r0);
+        float4 g[kFirstTile], y[kFirstTile];
+        float xv[kFirstTile];
+#pragma unroll
+        for (int i = 0; i < kFirstTile; ++i) {
+            const bool ok = act && i < nr;
+            g[i] = ok ? ld4(gh + (r0 + i) * n + c0) : z4;
+            y[i] = ok ? ld4(h + (r0 + i) * n + c0) : z4;
+            xv[i] = (i < nr && lane < K) ? x[(r0 + i) * K + lane] : 0.f;
+        }
+#pragma unroll
+        for (int i = 0; i < kFirstTile; ++i) {
+            const float gq[4] = {g[i].x, g[i].y, g[i].z, g[i].w};
+            const float yq[4] = {y[i].x, y[i].y, y[i].z, y[i].w};
+            float gz[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                gz[q] = gq[q] * (1.0f - yq[q] * yq[q]);
+                ab[q] += gz[q];
+            }
+#pragma unroll
+            for (int k = 0; k < K; ++k) {
+                const float xk =
+                    __int_as_float(__builtin_amdgcn_readlane(__float_as_int(xv[i]), k));
+#pragma unroll
+                for (int q = 0; q < 4; ++q) aw[k][q] = fmaf(gz[q], xk, aw[k][q]);
+            }
+        }
+    }
+    const int P = (K + 1) * n;
+    float *mine = sh_fl + wid * P;
+    if (act) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+#pragma unroll
+            for (int k = 0; k < K; ++k) mine[k * n + c0 + q] = aw[k][q];
+            mine[K * n + c0 + q] = ab[q];
+        }
+    }
+    __syncthreads();
+    for (int p = threadIdx.x; p < P; p += kBlock)
+        part[(int64_t)blockIdx.x * P + p] =
+            ((sh_fl[p] + sh_fl[P + p]) + sh_fl[2 * P + p]) + sh_fl[3 * P + p];
+}
+
+// Sum of the grouped partials (ng rows) scattered to d W (n,K) row-major and
+// d b (n).
+__global__ __launch_bounds__(kBlock) void first_layer_finish_kernel(int ng, int n, int K,
+                                                                    const float *__restrict__ part,
+                                                                    float *__restrict__ gw,
+                                                                    float *__restrict__ gb) {
+    const int P = (K + 1) * n;
+    const int p = blockIdx.x * kBlock + threadIdx.x;
+    if (p >= P) return;
+    float s0 = 0.f, s1 = 0.f;
+    int g = 0;
+    for (; g + 1 < ng; g += 2) {
+        s0 += part[(int64_t)g * P + p];
+        s1 += part[(int64_t)(g + 1) * P + p];
+    }
+    if (g < ng) s0 += part[(int64_t)g * P + p];
+    const float s = s0 + s1;
+    const int k = p / n, c = p - k * n;
+    if (k < K) gw[c * K + k] = s;
+    else gb[c] = s;
+}
+
 // Gradient outputs of the head step (finish kernel).
 struct HeadOut {
     float *g_w_act, *g_b_act, *g_w_val, *g_b_val, *g_b_pi, *g_b_vf, *g_log_std, *stats;
@@ -1183,6 +1277,63 @@ int dr_ppo_head_loss_backward(int64_t m, int64_t hd, const float *h_pi, const fl
                        0, st, ng, P, (int)hd, m, part2, part + (int64_t)nb * P, log_std,
                        ent_coef, vf_coef, o);
     return check_launch("dr_ppo_head_loss_backward finish");
+}
+
+
+static int first_blocks(int64_t m) {
+    const int64_t b = (m + 4 * kFirstTile - 1) / (4 * kFirstTile);
+    return (int)(b < 512 ? b : 512);
+}
+
+size_t dr_first_layer_backward_workspace_bytes(int64_t m, int64_t k, int64_t n) {
+    const int64_t P = (k + 1) * n;
+    return align_up(sizeof(float) * (size_t)(first_blocks(m > 0 ? m : 1) * P)) +
+           align_up(sizeof(float) * (size_t)(kHeadGroups * P));
+}
+
+int dr_first_layer_backward(int64_t m, int64_t k, int64_t n, const float *grad_h,
+                            const float *h, const float *x, float *grad_w, float *grad_b,
+                            void *workspace, size_t workspace_bytes, void *stream) {
+    if (m < 1 || !grad_h || !h || !x || !grad_w || !grad_b || n < 4 || n > 256 || (n & 3))
+        return fail0(DR_ERR_INVALID, "dr_first_layer_backward: bad arguments");
+    if ((((uintptr_t)grad_h) | ((uintptr_t)h)) & 15)
+        return fail0(DR_ERR_INVALID, "dr_first_layer_backward: grad_h / h must be 16-byte aligned");
+    if (!workspace || workspace_bytes < dr_first_layer_backward_workspace_bytes(m, k, n))
+        return fail0(DR_ERR_INVALID, "dr_first_layer_backward: workspace too small");
+    const int nb = first_blocks(m);
+    const int P = (int)((k + 1) * n);
+    float *part = static_cast<float *>(workspace);
+    float *part2 = reinterpret_cast<float *>(static_cast<char *>(workspace) +
+                                             align_up(sizeof(float) * (size_t)(nb * P)));
+    hipStream_t st = as_stream(stream);
+    const size_t lds = sizeof(float) * 4 * P;
+    switch (k) {
+#define DR_FL_CASE(K)                                                                      \
+    case K:                                                                                \
+        if (lds > 65536)                                                                   \
+            (void)hipFuncSetAttribute(reinterpret_cast<const void *>(first_layer_bwd_kernel<K>), \
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds); \
+        hipLaunchKernelGGL(first_layer_bwd_kernel<K>, dim3(nb), dim3(kBlock), lds, st, m,   \
+                           (int)n, grad_h, h, x, part);                                    \
+        break;
+        DR_FL_CASE(4) DR_FL_CASE(8) DR_FL_CASE(12) DR_FL_CASE(15) DR_FL_CASE(16)
+        DR_FL_CASE(18) DR_FL_CASE(24) DR_FL_CASE(32)
+#undef DR_FL_CASE
+        default:
+            return fail0(DR_ERR_UNSUPPORTED,
+                         "dr_first_layer_backward: k must be one of 4, 8, 12, 15, 16, 18, 24, 32");
+    }
+    int rc = check_launch("dr_first_layer_backward");
+    if (rc) return rc;
+    const int gsize = (nb + kHeadGroups - 1) / kHeadGroups;
+    const int ng = (nb + gsize - 1) / gsize;
+    hipLaunchKernelGGL(colsum_groups_kernel, dim3((P + kBlock - 1) / kBlock, ng), dim3(kBlock),
+                       0, st, nb, P, gsize, part, part2);
+    rc = check_launch("dr_first_layer_backward groups");
+    if (rc) return rc;
+    hipLaunchKernelGGL(first_layer_finish_kernel, dim3((P + kBlock - 1) / kBlock), dim3(kBlock),
+                       0, st, ng, (int)n, (int)k, part2, grad_w, grad_b);
+    return check_launch("dr_first_layer_backward finish");
 }
 
 }  // extern "C"

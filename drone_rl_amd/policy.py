@@ -213,6 +213,7 @@ class FusedTrainStep:
         self._acts = {pre: [torch.empty(M, n, **f32) for n in pol.net_arch]
                       for pre in ("pi", "vf")}
         self._gzt = {pre: torch.empty(M, pol.net_arch[-1], **f32) for pre in ("pi", "vf")}
+        self._first = self.K.FirstLayerBackward(M, pol.obs_dim, pol.net_arch[0], pol.device)
 
     @torch.no_grad()
     def step(self, obs, actions, aux, head):
@@ -221,7 +222,8 @@ class FusedTrainStep:
         dr_ppo_head_loss_backward (heads, loss, backward through the heads
         and top tanh, head / top-bias / log_std gradients), then per MLP the
         split-K weight gradients, grad_h = grad_z W and dr_tanh_backward down
-        the stack.  Returns (flat grad, stats (8))."""
+        the stack, the first layer by dr_first_layer_backward (its grad_z is
+        never stored).  Returns (flat grad, stats (8))."""
         self._alloc_fused()
         pol, M = self.pol, obs.shape[0]
         depth, top = len(pol.net_arch), len(pol.net_arch) - 1
@@ -235,13 +237,19 @@ class FusedTrainStep:
         for pre in ("pi", "vf"):
             gz = self._gzt[pre]
             h = hs[pre]
-            for k in reversed(range(depth)):
-                x = h[k - 1] if k > 0 else obs
+            if depth == 1:                    # the head kernel gave grad_z of layer 0
+                self._wgrad(gz, obs, self.gview(f"{pre}0.w"))
+                continue
+            for k in reversed(range(1, depth)):
+                x = h[k - 1]
                 self._wgrad(gz, x, self.gview(f"{pre}{k}.w"))
-                if k > 0:
-                    n_in = x.shape[1]
-                    g = self._g[:M * n_in].view(M, n_in)
-                    torch.mm(gz, pol.p(f"{pre}{k}.w"), out=g)
+                n_in = x.shape[1]
+                g = self._g[:M * n_in].view(M, n_in)
+                torch.mm(gz, pol.p(f"{pre}{k}.w"), out=g)
+                if k == 1:
+                    # first layer: tanh backward + weight/bias gradients fused
+                    self._first(g, h[0], obs, self.gview(f"{pre}0.w"), self.gview(f"{pre}0.b"))
+                else:
                     gz = self._gz[:M * n_in].view(M, n_in)
                     self.K.tanh_backward(g, h[k - 1], gz, self.gview(f"{pre}{k - 1}.b"),
                                          self.tanh_ws)

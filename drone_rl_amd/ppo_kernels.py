@@ -204,3 +204,19 @@ class HeadLossBackward:
             ptr(g_w_val), ptr(g_b_val), ptr(g_b_pi), ptr(g_b_vf), ptr(g_log_std),
             ptr(self.stats), ptr(self.ws), self.ws.numel(), _s(h_pi)))
         return self.stats
+
+
+class FirstLayerBackward:
+    """dr_first_layer_backward: grad_w (n,k), grad_b (n) of h = tanh(x W^T + b)
+    from grad_h, without materialising grad_z."""
+
+    def __init__(self, m: int, k: int, n: int, device):
+        self.m, self.k, self.n = m, k, n
+        self.ws = torch.empty(_lib.lib().dr_first_layer_backward_workspace_bytes(m, k, n),
+                              dtype=torch.uint8, device=device)
+
+    def __call__(self, grad_h, h, x, grad_w, grad_b):
+        assert grad_h.shape == (self.m, self.n) and x.shape == (self.m, self.k)
+        check(_lib.lib().dr_first_layer_backward(
+            self.m, self.k, self.n, ptr(_f32(grad_h)), ptr(_f32(h)), ptr(_f32(x)), ptr(grad_w),
+            ptr(grad_b), ptr(self.ws), self.ws.numel(), _s(h)))

@@ -239,6 +239,19 @@ int dr_tanh_backward(int64_t m, int64_t n, const float *grad_h, const float *h,
 int dr_linear_tanh(int64_t m, int64_t k, int64_t n, const float *x,
                    const float *w, const float *b, float *h, void *stream);
 
+/* Backward of the first layer h = tanh(x W^T + b), fused: for grad_h (m,n)
+   = dLoss/dh, forms grad_z = grad_h * (1 - h^2) in registers (never stored)
+   and writes grad_w (n,k) = grad_z^T x and grad_b (n) = sum_r grad_z
+   (dr_tanh_backward + the weight-gradient GEMM in one pass; the input
+   gradient of the first layer is not needed).  k as dr_linear_tanh; n % 4
+   == 0, n <= 256; grad_h and h 16-byte aligned.  Deterministic.
+   `workspace` >= dr_first_layer_backward_workspace_bytes(m, k, n). */
+size_t dr_first_layer_backward_workspace_bytes(int64_t m, int64_t k, int64_t n);
+int dr_first_layer_backward(int64_t m, int64_t k, int64_t n, const float *grad_h,
+                            const float *h, const float *x, float *grad_w,
+                            float *grad_b, void *workspace,
+                            size_t workspace_bytes, void *stream);
+
 /* Policy heads for rollouts (ActorCriticPolicy.forward's action_net /
    value_net): mean (m,4) = h_pi W_act^T + b_act, value (m) = h_vf W_val^T +
    b_val, for the top hidden activations h_pi, h_vf (m,hd), hd % 4 == 0,

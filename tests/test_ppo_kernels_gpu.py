@@ -246,3 +246,20 @@ def test_fused_step_matches_unfused_path(arch, m):
     assert torch.allclose(st2, st_ref, rtol=1e-4, atol=1e-6)
     grad2, _ = fs.step(obs, act, aux, head)
     assert torch.equal(grad, grad2)
+
+
+@pytest.mark.parametrize("k,n,m", [(15, 256, 65536), (12, 64, 1001), (18, 128, 77)])
+def test_first_layer_backward_matches_torch(k, n, m):
+    from drone_rl_amd import ppo_kernels as K
+    x = torch.randn(m, k, device="cuda")
+    h = torch.tanh(torch.randn(m, n, device="cuda"))
+    g = torch.randn(m, n, device="cuda")
+    gw = torch.empty(n, k, device="cuda")
+    gb = torch.empty(n, device="cuda")
+    K.FirstLayerBackward(m, k, n, "cuda")(g, h, x, gw, gb)
+    gz = (g.double() * (1 - h.double() ** 2))
+    ref_w = gz.t() @ x.double()
+    ref_b = gz.sum(0)
+    tol = 1e-5 * (gz.abs().t() @ x.double().abs()).max().item()
+    assert (gw.double() - ref_w).abs().max().item() <= tol
+    assert (gb.double() - ref_b).abs().max().item() <= 1e-5 * gz.abs().sum(0).max().item()
