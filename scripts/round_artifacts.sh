@@ -1,0 +1,31 @@
+#!/bin/bash
+# Everything the round's judged artefacts come from, in one GPU session:
+# GPU tests, smoke, the default bench line, the --extra bench, a rocprofv3
+# kernel trace of the default bench and the PMC passes for the env kernel.
+# Each GPU step has its own time limit; a crash/abort/timeout ends the script.
+cd "$(dirname "$0")/.."
+OUT=gpurun_out
+mkdir -p $OUT
+step() {  # name, seconds, command...
+  local name=$1 secs=$2; shift 2
+  echo "== $name ($(date +%T))"
+  timeout -k 10 "$secs" "$@" > "$OUT/$name.log" 2>&1
+  local rc=$?
+  echo "== $name rc=$rc"; tail -3 "$OUT/$name.log"
+  if [ $rc -ge 124 ] || [ $rc -eq 134 ] || [ $rc -eq 139 ]; then
+    echo "fatal rc=$rc in $name: stopping"; exit $rc
+  fi
+  return 0
+}
+step pytest_gpu 900 python -m pytest tests -m gpu -q
+step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
+step bench 600 python bench.py
+grep '^{' $OUT/bench.log > $OUT/bench.json || true
+step bench_extra 900 python bench.py --no-cpu-baseline --extra
+grep '^{' $OUT/bench_extra.log > $OUT/bench_extra.json || true
+export TMPDIR=/tmp
+step rocprof 600 rocprofv3 --kernel-trace --stats --output-format csv \
+    -d "$PWD/$OUT/prof" -o run -- python3 "$PWD/bench.py" --no-cpu-baseline
+step pmc_n65536 900 bash scripts/pmc.sh n65536 --steps 50 --ppo-updates 0
+step pmc_n4m 900 bash scripts/pmc.sh n4m --envs 4194304 --steps 20 --warmup 5 --ppo-updates 0
+echo "== done"
