@@ -179,10 +179,19 @@ def main():
 
     import torch
     import torch.distributed as dist
+    # one rank per GPU over RCCL.  DRONERL_DIST_BACKEND=gloo (with ranks
+    # wrapping onto the available devices) only rehearses the multi-rank
+    # path on a box with fewer GPUs than ranks (RCCL refuses 2 ranks/GPU).
+    backend = os.environ.get("DRONERL_DIST_BACKEND", "nccl")
+    if backend != "nccl":
+        local = local % max(torch.cuda.device_count(), 1)
     torch.cuda.set_device(local)
     device = torch.device("cuda", local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=device)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=device)
+        else:
+            dist.init_process_group(backend)
 
     elapsed, gpu_ms, ep = time_env(args, args.state_dtype, args.envs, rank, world, device,
                                    args.steps, args.warmup)
