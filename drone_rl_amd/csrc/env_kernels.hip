@@ -414,25 +414,27 @@ __device__ inline S physics_step(S st[F_N], float4 act, S dt, bool &crash) {
 // Per-wave variant: each wave stages its own 64 rows (3,840 B) and writes
 // them out with no workgroup barrier, so a wave delayed by a reset or a late
 // load does not hold back the other three waves of its block.
-template <int OD>
+template <int OD, int RPW = 64>
 __device__ inline void store_obs_wave(float *sh_block, const float ob[OD],
                                       float *dst_all, int64_t n) {
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    float *sh = sh_block + w * 64 * OD;
+    float *sh = sh_block + w * RPW * OD;
+    if (lane < RPW) {
 #pragma unroll
-    for (int k = 0; k < OD; ++k) sh[lane * OD + k] = ob[k];
+        for (int k = 0; k < OD; ++k) sh[lane * OD + k] = ob[k];
+    }
     // DS ops of one wave execute in order; the barrier only pins the
     // compiler's schedule (no workgroup s_barrier is emitted)
     __builtin_amdgcn_wave_barrier();
-    const int64_t wbase = (int64_t)blockIdx.x * kBlock + w * 64;
-    const int64_t nvalid = (n - wbase) < 64 ? (n - wbase) : 64;
+    const int64_t wbase = (int64_t)blockIdx.x * (4 * RPW) + w * RPW;
+    const int64_t nvalid = (n - wbase) < RPW ? (n - wbase) : RPW;
     if (nvalid <= 0) return;
     float *dst = dst_all + wbase * OD;
-    if (nvalid == 64 && (((uintptr_t)dst) & 15) == 0) {
+    if (nvalid == RPW && (((uintptr_t)dst) & 15) == 0) {
         const float4 *s4 = reinterpret_cast<const float4 *>(sh);
         float4 *d4 = reinterpret_cast<float4 *>(dst);
 #pragma unroll
-        for (int q = lane; q < 64 * OD / 4; q += 64) d4[q] = s4[q];
+        for (int q = lane; q < RPW * OD / 4; q += 64) d4[q] = s4[q];
     } else {
         for (int q = lane; q < (int)nvalid * OD; q += 64) dst[q] = sh[q];
     }
@@ -459,14 +461,16 @@ __device__ inline void store_obs_block(float *sh, const float ob[OD],
     }
 }
 
-template <typename S, int VAR, bool MON>
+template <typename S, int VAR, bool MON, int RPW>
 __global__ __launch_bounds__(kBlock) void env_step_kernel(EnvView<S> v,
                                                           StepIO io) {
     constexpr int OD = VAR == DR_VARIANT_GYM ? 15 : (VAR == DR_VARIANT_MOVING ? 18 : 12);
     constexpr bool GYMLIKE = VAR != DR_VARIANT_VECTORIZED;
     __shared__ float4 sh4[kBlock * OD / 4];
-    const int64_t base = (int64_t)blockIdx.x * kBlock;
-    const int64_t i = base + threadIdx.x;
+    const int64_t base = (int64_t)blockIdx.x * (4 * RPW);
+    const int lane_ = threadIdx.x & 63;
+    // env of this lane; lanes >= RPW of a half-populated wave own none
+    const int64_t i = lane_ < RPW ? base + (threadIdx.x >> 6) * RPW + lane_ : v.n;
     DR_STAMP(0);
     float ob[OD];
     if (i < v.n) {
@@ -579,7 +583,7 @@ __global__ __launch_bounds__(kBlock) void env_step_kernel(EnvView<S> v,
     }
     (void)sh4;
 #elif DR_WAVE_STAGE
-    store_obs_wave<OD>(reinterpret_cast<float *>(sh4), ob, io.obs, v.n);
+    store_obs_wave<OD, RPW>(reinterpret_cast<float *>(sh4), ob, io.obs, v.n);
 #else
     store_obs_block<OD>(reinterpret_cast<float *>(sh4), ob, io.obs, base, v.n);
 #endif
@@ -949,6 +953,10 @@ struct dr_handle {
     int64_t stride = 0;
     int obs_dim = 15;
     bool quad = false;  // true: 4 lanes per env (env_step_quad_kernel)
+    // envs per wave of env_step_kernel: 64, or 32 (half-populated waves:
+    // twice the waves in flight; measured faster from 2M envs up, slower
+    // below 1M: scripts/micro/ab_cross.sh)
+    int rpw = 64;
     void *mem = nullptr;
     const double *host_u = nullptr;
     std::string err;
@@ -1043,9 +1051,17 @@ int launch_step(dr_handle *h, const StepIO &io, hipStream_t st) {
             launched = true;
         }
     }
-    if (!launched)
-        hipLaunchKernelGGL((env_step_kernel<S, VAR, MON>), dim3(grid_for(h->n)),
-                           dim3(kBlock), 0, st, v, io);
+    if (!launched) {
+        switch (h->rpw) {
+            case 32:
+                hipLaunchKernelGGL((env_step_kernel<S, VAR, MON, 32>), dim3(grid_for(h->n, 128)),
+                                   dim3(kBlock), 0, st, v, io);
+                break;
+            default:
+                hipLaunchKernelGGL((env_step_kernel<S, VAR, MON, 64>), dim3(grid_for(h->n, 256)),
+                                   dim3(kBlock), 0, st, v, io);
+        }
+    }
     hipError_t e = hipGetLastError();
     if (e != hipSuccess)
         return fail(h, DR_ERR_HIP, std::string("env_step_kernel: ") + hipGetErrorString(e));
@@ -1118,6 +1134,11 @@ int dr_create(const dr_config *cfg_in, dr_handle **out) {
     // slower on MI355X at every measured size, kept for A/B measurement).
     if (const char *kk = std::getenv("DRONERL_STEP_KERNEL"))
         h->quad = std::strcmp(kk, "quad") == 0;
+    h->rpw = cfg.num_envs >= ((int64_t)3 << 19) ? 32 : 64;   // >= 1.5M envs
+    if (const char *r = std::getenv("DRONERL_ROWS_PER_WAVE")) {
+        const int v = std::atoi(r);
+        if (v == 32 || v == 64) h->rpw = v;
+    }
 
     DeviceGuard g(cfg.device);
     const size_t bytes = state_bytes(h->stride, cfg.state_dtype, cfg.variant);

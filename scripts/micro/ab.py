@@ -2,7 +2,8 @@
 variance is larger than the effects being measured).  Each variant is a
 separately built .so; its env_step is captured into a hipGraph of K steps
 and the graphs are replayed alternately R times; medians are reported.
-Usage: python scripts/micro/ab.py lib1.so lib2.so ... [--n N] [--dtype f64]"""
+Usage: python scripts/micro/ab.py lib1.so lib2.so:ENV=VAL ... [--n N] [--dtype f64]
+(ENV=VAL pairs are set while that library's handle is created)."""
 import argparse
 import ctypes
 import json
@@ -39,7 +40,12 @@ def main():
     rew = torch.zeros(n, device=dev)
     done = torch.zeros(n, dtype=torch.uint8, device=dev)
     runs = []
-    for path in a.libs:
+    for spec in a.libs:
+        # "lib.so" or "lib.so:VAR=VAL,VAR=VAL" (env read by dr_create)
+        path, _, envs = spec.partition(":")
+        for kv in filter(None, envs.split(",")):
+            k, _, val = kv.partition("=")
+            os.environ[k] = val
         L = load(path)
         cfg = _lib.dr_config(num_envs=n, variant=0, state_dtype=0 if a.dtype == "f64" else 1,
                              rng_mode=0, auto_reset=1, device=0, max_steps=0, seed=1,
@@ -60,7 +66,9 @@ def main():
                     L.dr_step(h, acts[t].data_ptr(), obs.data_ptr(), rew.data_ptr(),
                               done.data_ptr(), None, cs)
         torch.cuda.current_stream().wait_stream(s)
-        runs.append((os.path.basename(path), L, h, g))
+        runs.append((os.path.basename(path) + (":" + envs if envs else ""), L, h, g))
+        for kv in filter(None, envs.split(",")):
+            os.environ.pop(kv.partition("=")[0], None)
     torch.cuda.synchronize()
     times = {r[0]: [] for r in runs}
     for _ in range(a.reps):

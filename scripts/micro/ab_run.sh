@@ -1,9 +1,12 @@
-set -o pipefail
+#!/bin/bash
+# In-process A/B of libdronerl.so builds (scripts/micro/ab.py) at three sizes.
+# Usage: bash scripts/micro/ab_run.sh lib1.so lib2.so ...
+cd "$(dirname "$0")/../.."
 mkdir -p gpurun_out
-timeout -k 10 600 python -m pytest tests -m gpu -x -q > gpurun_out/t.log 2>&1; rc=$?; tail -4 gpurun_out/t.log
-[ $rc -le 1 ] || exit $rc
-B=scripts/micro/build
-timeout -k 10 300 python scripts/micro/ab.py $B/libold.so $B/liblibtrig.so $B/libnew.so --n 65536 --reps 25 > gpurun_out/ab1.log 2>&1 || exit $?
-cat gpurun_out/ab1.log | grep '^{'
-timeout -k 10 300 python scripts/micro/ab.py $B/libold.so $B/liblibtrig.so $B/libnew.so --n 4194304 --k 50 --reps 9 > gpurun_out/ab2.log 2>&1 || exit $?
-cat gpurun_out/ab2.log | grep '^{'
+i=0
+for spec in "65536 200 25" "131072 200 25" "4194304 50 9"; do
+  read n k reps <<< "$spec"
+  i=$((i+1))
+  timeout -k 10 300 python scripts/micro/ab.py "$@" --n $n --k $k --reps $reps > gpurun_out/ab$i.log 2>&1 || exit $?
+  echo "n=$n $(grep '^{' gpurun_out/ab$i.log)"
+done

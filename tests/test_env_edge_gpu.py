@@ -25,9 +25,13 @@ def _close(a, b, tol=1e-5):
     assert err.max() <= tol, err.max()
 
 
-@pytest.mark.parametrize("n", [1, 63, 64, 65, 255, 257, 1000])
+@pytest.mark.parametrize("rpw", ["64", "32"])
+@pytest.mark.parametrize("n", [1, 31, 33, 63, 64, 65, 255, 257, 1000])
 @pytest.mark.parametrize("dtype", [torch.float64, torch.float32])
-def test_ragged_sizes_match_oracle(golden, n, dtype):
+def test_ragged_sizes_match_oracle(golden, n, dtype, rpw, monkeypatch):
+    """Also with half-populated waves (32 envs per wave, the layout chosen
+    from 1.5M envs up), forced here by DRONERL_ROWS_PER_WAVE."""
+    monkeypatch.setenv("DRONERL_ROWS_PER_WAVE", rpw)
     from drone_rl_amd import DroneBatch
     g = golden("gym_step.npz")
     idx = np.arange(n) * 7 % len(g["action"])
@@ -108,6 +112,24 @@ def test_abi_argument_errors():
     assert L.dr_destroy(h) == 0
     with pytest.raises(ValueError):
         b.step(torch.zeros(63, 4, device="cuda"))
+
+
+def test_half_populated_waves_equal_full_waves(monkeypatch):
+    """The 32-envs-per-wave launch computes exactly what the 64 one does,
+    over 60 steps with auto-resets, terminal obs and monitor outputs."""
+    from drone_rl_amd import DroneBatch, random_actions
+    n = 4099
+    out = []
+    for rpw in ("64", "32"):
+        monkeypatch.setenv("DRONERL_ROWS_PER_WAVE", rpw)
+        b = DroneBatch(n, "gym", seed=21, keep_terminal_obs=True, monitor=True)
+        b.reset()
+        acc = []
+        for t in range(60):
+            o, r, d = b.step(random_actions(n, seed=4, step=t))
+            acc += [o.clone(), r.clone(), d.clone(), b.term_obs.clone(), b.ep_ret.clone()]
+        out.append(acc + [b.get("pos"), b.get("ep_num")])
+    assert all(torch.equal(x, y) for x, y in zip(*out))
 
 
 def test_sharded_equals_unsharded():
