@@ -61,7 +61,9 @@ class ActorCritic:
         self.obs_dim, self.act_dim = obs_dim, act_dim
         self.net_arch = tuple(net_arch)
         self.device = torch.device(device) if device is not None else torch.device("cpu")
-        self.layout = []            # (name, shape, init gain or None)
+        # Parameters in SB3 registration order (also the init order, so a
+        # seed gives SB3's draw sequence): (name, shape, init gain or None)
+        self.layout = []
         dims = (obs_dim,) + self.net_arch
         for pre in ("pi", "vf"):
             for k in range(len(self.net_arch)):
@@ -74,9 +76,20 @@ class ActorCritic:
                 self.layout.append(("value.w", (1, dims[-1]), 1.0))
                 self.layout.append(("value.b", (1,), None))
         self.layout.append(("log_std", (act_dim,), "log_std"))
+        # Storage order in the flat buffer: the pi and vf tensors of each
+        # hidden layer adjacent (pi{k}.w, vf{k}.w, pi{k}.b, vf{k}.b), so a
+        # layer of both MLPs is one (2, out, in) view for batched GEMMs;
+        # every tensor size is a multiple of 4 floats up to value.b, so each
+        # weight stays 16-byte aligned.
+        by_name = {name: (shape, gain) for name, shape, gain in self.layout}
+        store = []
+        for k in range(len(self.net_arch)):
+            store += [f"pi{k}.w", f"vf{k}.w", f"pi{k}.b", f"vf{k}.b"]
+        store += ["action.w", "action.b", "value.w", "value.b", "log_std"]
         self.offsets = {}
         off = 0
-        for name, shape, _ in self.layout:
+        for name in store:
+            shape = by_name[name][0]
             n = int(np.prod(shape))
             self.offsets[name] = (off, off + n, shape)
             off += n
@@ -102,6 +115,14 @@ class ActorCritic:
     def p(self, name):
         a, b, shape = self.offsets[name]
         return self.flat[a:b].view(shape)
+
+    def p2(self, k: int, kind: str, buf=None):
+        """Layer k of both MLPs as one (2, ...) view of `buf` (default the
+        parameters): kind "w" -> (2, out, in), "b" -> (2, out)."""
+        buf = self.flat if buf is None else buf
+        a, _, shape = self.offsets[f"pi{k}.{kind}"]
+        _, b, _ = self.offsets[f"vf{k}.{kind}"]
+        return buf[a:b].view((2,) + tuple(shape))
 
     @property
     def log_std(self):
@@ -206,52 +227,75 @@ class FusedTrainStep:
         return fusable(self.pol)
 
     def _alloc_fused(self):
-        if getattr(self, "_acts", None) is not None:
+        if getattr(self, "_acts2", None) is not None:
             return
         pol, M = self.pol, self.m
         f32 = dict(dtype=torch.float32, device=pol.device)
-        self._acts = {pre: [torch.empty(M, n, **f32) for n in pol.net_arch]
-                      for pre in ("pi", "vf")}
-        self._gzt = {pre: torch.empty(M, pol.net_arch[-1], **f32) for pre in ("pi", "vf")}
+        # both MLPs' activations of a layer in one (2, M, n) buffer, so the
+        # layers above the first run as one batched GEMM for pi and vf
+        self._acts2 = [torch.empty(2, M, n, **f32) for n in pol.net_arch]
+        self._acts = {pre: [a[j] for a in self._acts2] for j, pre in enumerate(("pi", "vf"))}
+        self._gz2 = [torch.empty(2, M, n, **f32) for n in pol.net_arch]
+        self._g2 = torch.empty(2, M, max(pol.net_arch), **f32)
+        self._ws2 = torch.empty(2 * self.C * max(pol.net_arch) ** 2, **f32) if self.C > 1 else None
         self._first = self.K.FirstLayerBackward(M, pol.obs_dim, pol.net_arch[0], pol.device)
+
+    def _wgrad2(self, gz, x, out):
+        """out (2, N, K) = gz[j]^T x[j] for both MLPs in one batched split-K
+        GEMM over 2C row chunks, then one fixed-order sum over the chunks."""
+        _, M, N = gz.shape
+        Kd = x.shape[2]
+        C = self.C
+        if C == 1:
+            torch.bmm(gz.transpose(1, 2), x, out=out)
+            return
+        ws = self._ws2[:2 * C * N * Kd].view(2 * C, N, Kd)
+        torch.bmm(gz.reshape(2 * C, M // C, N).transpose(1, 2), x.reshape(2 * C, M // C, Kd),
+                  out=ws)
+        torch.sum(ws.view(2, C, N, Kd), dim=1, out=out)
 
     @torch.no_grad()
     def step(self, obs, actions, aux, head):
         """One PPO.train minibatch on the fused path: hidden forward
         (dr_linear_tanh for the first layer, hipBLASLt addmm + tanh above),
         dr_ppo_head_loss_backward (heads, loss, backward through the heads
-        and top tanh, head / top-bias / log_std gradients), then per MLP the
-        split-K weight gradients, grad_h = grad_z W and dr_tanh_backward down
-        the stack, the first layer by dr_first_layer_backward (its grad_z is
-        never stored).  Returns (flat grad, stats (8))."""
+        and top tanh, head / top-bias / log_std gradients), then for the
+        layers above the first ONE batched split-K weight-gradient GEMM and
+        ONE batched grad_h = grad_z W for pi and vf together (the flat
+        layout keeps the two MLPs' tensors of a layer adjacent), tanh
+        backward down the stack, and the first layer by
+        dr_first_layer_backward (its grad_z is never stored).
+        Returns (flat grad, stats (8))."""
         self._alloc_fused()
         pol, M = self.pol, obs.shape[0]
         depth, top = len(pol.net_arch), len(pol.net_arch) - 1
-        hs = hidden_forward(pol, obs, self._acts)
+        hs = hidden_forward(pol, obs, self._acts, self._acts2)
+        gz = self._gz2[top]
         stats = head(hs["pi"][top], hs["vf"][top], pol.p("action.w"), pol.p("action.b"),
                      pol.p("value.w"), pol.p("value.b"), pol.log_std, actions, aux,
-                     self._gzt["pi"], self._gzt["vf"], self.gview("action.w"),
+                     gz[0], gz[1], self.gview("action.w"),
                      self.gview("action.b"), self.gview("value.w"), self.gview("value.b"),
                      self.gview(f"pi{top}.b"), self.gview(f"vf{top}.b"),
                      self.gview("log_std"))
-        for pre in ("pi", "vf"):
-            gz = self._gzt[pre]
-            h = hs[pre]
-            if depth == 1:                    # the head kernel gave grad_z of layer 0
-                self._wgrad(gz, obs, self.gview(f"{pre}0.w"))
-                continue
-            for k in reversed(range(1, depth)):
-                x = h[k - 1]
-                self._wgrad(gz, x, self.gview(f"{pre}{k}.w"))
-                n_in = x.shape[1]
-                g = self._g[:M * n_in].view(M, n_in)
-                torch.mm(gz, pol.p(f"{pre}{k}.w"), out=g)
-                if k == 1:
-                    # first layer: tanh backward + weight/bias gradients fused
-                    self._first(g, h[0], obs, self.gview(f"{pre}0.w"), self.gview(f"{pre}0.b"))
-                else:
-                    gz = self._gz[:M * n_in].view(M, n_in)
-                    self.K.tanh_backward(g, h[k - 1], gz, self.gview(f"{pre}{k - 1}.b"),
+        if depth == 1:                        # the head kernel gave grad_z of layer 0
+            for j, pre in enumerate(("pi", "vf")):
+                self._wgrad(gz[j], obs, self.gview(f"{pre}0.w"))
+            return self.grad, stats
+        for k in reversed(range(1, depth)):
+            x = self._acts2[k - 1]
+            n_in = x.shape[2]
+            self._wgrad2(gz, x, pol.p2(k, "w", self.grad))
+            g = self._g2.view(-1)[:2 * M * n_in].view(2, M, n_in)
+            torch.bmm(gz, pol.p2(k, "w"), out=g)
+            if k == 1:
+                # first layer: tanh backward + weight/bias gradients fused
+                for j, pre in enumerate(("pi", "vf")):
+                    self._first(g[j], x[j], obs, self.gview(f"{pre}0.w"),
+                                self.gview(f"{pre}0.b"))
+            else:
+                gz = self._gz2[k - 1]
+                for j, pre in enumerate(("pi", "vf")):
+                    self.K.tanh_backward(g[j], x[j], gz[j], self.gview(f"{pre}{k - 1}.b"),
                                          self.tanh_ws)
         return self.grad, stats
 
@@ -318,24 +362,23 @@ def fusable(pol: ActorCritic) -> bool:
 
 
 @torch.no_grad()
-def hidden_forward(pol: ActorCritic, obs, acts):
+def hidden_forward(pol: ActorCritic, obs, acts, acts2=None):
     """Hidden activations of the pi and vf MLPs into preallocated buffers
-    acts[pre][k] (M, net_arch[k])."""
+    acts[pre][k] (M, net_arch[k]); with acts2 (the (2, M, n) buffers that
+    acts views) each layer's tanh runs once over both MLPs."""
     from . import ppo_kernels as K
-    out = {}
-    for pre in ("pi", "vf"):
-        x, hs = obs, []
-        for k in range(len(pol.net_arch)):
-            h = acts[pre][k]
-            if k == 0:
-                K.linear_tanh(x, pol.p(f"{pre}0.w"), pol.p(f"{pre}0.b"), h)
-            else:
-                torch.addmm(pol.p(f"{pre}{k}.b"), x, pol.p(f"{pre}{k}.w").t(), out=h)
-                torch.tanh_(h)
-            hs.append(h)
-            x = h
-        out[pre] = hs
-    return out
+    for j, pre in enumerate(("pi", "vf")):
+        K.linear_tanh(obs, pol.p(f"{pre}0.w"), pol.p(f"{pre}0.b"), acts[pre][0])
+    for k in range(1, len(pol.net_arch)):
+        for pre in ("pi", "vf"):
+            torch.addmm(pol.p(f"{pre}{k}.b"), acts[pre][k - 1], pol.p(f"{pre}{k}.w").t(),
+                        out=acts[pre][k])
+        if acts2 is not None:
+            torch.tanh_(acts2[k])
+        else:
+            for pre in ("pi", "vf"):
+                torch.tanh_(acts[pre][k])
+    return acts
 
 
 class PolicyInference:
@@ -347,8 +390,8 @@ class PolicyInference:
     def __init__(self, pol: ActorCritic, n: int):
         self.pol, self.n = pol, n
         f32 = dict(dtype=torch.float32, device=pol.device)
-        self.acts = {pre: [torch.empty(n, w, **f32) for w in pol.net_arch]
-                     for pre in ("pi", "vf")}
+        self.acts2 = [torch.empty(2, n, w, **f32) for w in pol.net_arch]
+        self.acts = {pre: [a[j] for a in self.acts2] for j, pre in enumerate(("pi", "vf"))}
         self.mean = torch.empty(n, pol.act_dim, **f32)
         self.value = torch.empty(n, **f32)
 
@@ -356,7 +399,7 @@ class PolicyInference:
     def __call__(self, obs):
         from . import ppo_kernels as K
         pol = self.pol
-        hs = hidden_forward(pol, obs, self.acts)
+        hs = hidden_forward(pol, obs, self.acts, self.acts2)
         K.policy_heads(hs["pi"][-1], hs["vf"][-1], pol.p("action.w"), pol.p("action.b"),
                        pol.p("value.w"), pol.p("value.b"), self.mean, self.value)
         return self.mean, self.value
