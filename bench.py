@@ -58,15 +58,20 @@ def parse():
 
 
 def cpu_baseline(seconds):
-    from oracle.cpu_baseline import cpu_model, run_pool
+    from oracle.cpu_baseline import c1_ppo, cpu_model, numpy_batched, run_pool, single_env
     procs = max(1, min(16, len(os.sched_getaffinity(0))))
     r = run_pool(procs, 64, seconds)
+    # BASELINE.md CPU plan (i), (iii), (iv) beside the headline (ii)
+    plan = {"single_env": single_env(seconds),
+            "numpy_batched_65536": numpy_batched(65536, seconds),
+            "c1_ppo_sb3_defaults": c1_ppo(2, procs)}
     return {"value": round(r["value"], 1), "unit": "env-steps/s", "cores": procs,
             "kind": "port",
             "sample": (f"{procs} worker processes x 64 numpy-port envs (oracle/drone_np, "
                        f"bit-exact vs reference), random U[0,7.3575)^4 actions, DummyVecEnv "
                        f"auto-reset, {r['elapsed']:.2f} s wall each ({r['steps']} env-steps); "
-                       f"SubprocVecEnv-equivalent without pipe IPC; CPU: {cpu_model()}")}
+                       f"SubprocVecEnv-equivalent without pipe IPC; CPU: {cpu_model()}"),
+            "plan": plan}
 
 
 def time_env(args, dtype_name, n_envs, rank, world, device, steps, warmup, variant="gym"):
@@ -230,6 +235,8 @@ def main():
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1),
                      "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                     "traffic_GBs": (round(traffic / per_launch_s / 1e9, 1)
+                                     if traffic else None),
                      "kernel": "env_step_kernel", "bytes_per_env_step": bpe,
                      "avg_launch_us": round(per_launch_s * 1e6, 3)},
         "mean_ep_num": round(ep, 2),

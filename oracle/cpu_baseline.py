@@ -68,6 +68,47 @@ def run_pool(procs: int, envs_per_proc: int, seconds: float) -> dict:
             "procs": procs, "envs_per_proc": envs_per_proc}
 
 
+def single_env(seconds: float) -> dict:
+    """BASELINE.md CPU plan (i): one DroneGymEnv-equivalent, one process."""
+    r = worker(1, seconds, 7)
+    return {"value": round(r["steps"] / r["elapsed"], 1), "unit": "env-steps/s", "cores": 1,
+            "sample": f"1 numpy-port env, DummyVecEnv auto-reset, {r['elapsed']:.2f} s"}
+
+
+def numpy_batched(n: int, seconds: float) -> dict:
+    """Plan (iii): VectorizedDroneEnv-style numpy-batched step of n envs in
+    one process (oracle/drone_np.gym_step_batched; no resets)."""
+    from oracle.drone_np import A_MAX, gym_step_batched
+    rng = np.random.default_rng(3)
+    s = {k: np.zeros((n, 3)) for k in ("pos", "vel", "euler", "omega", "target")}
+    s["pos"][:, 2] = 1.0
+    s["target"][:, 2] = 1.0
+    s["step"] = np.zeros(n, np.int32)
+    acts = rng.uniform(0, A_MAX, (8, n, 4)).astype(np.float32)
+    steps, k = 0, 0
+    t0 = time.perf_counter()
+    while time.perf_counter() - t0 < seconds:
+        gym_step_batched(s, acts[k % 8])
+        steps += n
+        k += 1
+    el = time.perf_counter() - t0
+    return {"value": round(steps / el, 1), "unit": "env-steps/s", "cores": 1,
+            "sample": f"{k} batched steps of {n} envs, {el:.2f} s"}
+
+
+def c1_ppo(updates: int, threads: int) -> dict:
+    """Plan (iv): configs[0] PPO (SB3 defaults, 1 env, 64x64) restated in
+    torch-CPU (oracle/sb3_c1.py), `updates` iterations of 2048 steps."""
+    import torch
+    from oracle.sb3_c1 import run
+    torch.set_num_threads(threads)
+    r = run(steps=2048 * updates, seed=0, log_every=10 ** 9, log=lambda *_: None)
+    return {"updates_per_s": round(updates / r["elapsed_s"], 4),
+            "env_steps_per_s": round(2048 * updates / r["elapsed_s"], 1), "cores": threads,
+            "sample": f"{updates} PPO iterations (2048 steps + 10 epochs x 32 minibatches of 64), "
+                      f"{r['elapsed_s']:.1f} s, torch.set_num_threads({threads})"}
+
+
 def cpu_model() -> str:
     try:
         for line in open("/proc/cpuinfo"):
