@@ -66,6 +66,7 @@ SIGNATURES = {
     "dr_step": (c_int, [_P, _P, _P, _P, _P, _P, _P]),
     "dr_step_monitored": (c_int, [_P, _P, _P, _P, _P, _P, _P, _P, _P]),
     "dr_get_state": (c_int, [_P, c_int, _P, _P]),
+    "dr_gather_state": (c_int, [_P, c_int, _P, c_int64, _P, _P]),
     "dr_set_state": (c_int, [_P, c_int, _P, _P]),
     "dr_set_reset_uniforms": (c_int, [_P, _P]),
     "dr_set_seed": (c_int, [_P, c_uint64]),

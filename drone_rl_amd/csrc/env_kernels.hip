@@ -902,6 +902,33 @@ __global__ void get_field_kernel(EnvView<S> v, int field, void *out) {
 }
 
 template <typename S>
+__global__ void gather_field_kernel(EnvView<S> v, int field, const int32_t *ids, int64_t k,
+                                    void *out) {
+    const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= k) return;
+    const int64_t i = ids[j];
+    if (i < 0 || i >= v.n) return;
+    if (field <= DR_FIELD_TARGET) {
+        double *o = static_cast<double *>(out);
+#pragma unroll
+        for (int c = 0; c < 3; ++c) o[j * 3 + c] = (double)v.field(field * 3 + c)[i];
+    } else if (field == DR_FIELD_STEP) {
+        static_cast<int32_t *>(out)[j] = v.step[i];
+    } else if (field == DR_FIELD_EP_NUM) {
+        static_cast<int32_t *>(out)[j] = v.ep_num[i];
+    } else if (field == DR_FIELD_EPS) {
+        static_cast<double *>(out)[j] = v.eps[i];
+    } else if (field == DR_FIELD_EP_RETURN) {
+        static_cast<float *>(out)[j] = v.ep_ret[i];
+    } else if (field == DR_FIELD_EP_LENGTH) {
+        static_cast<int32_t *>(out)[j] = v.ep_len[i];
+    } else if (field == DR_FIELD_MOTION) {
+#pragma unroll
+        for (int c = 0; c < 9; ++c) static_cast<float *>(out)[j * 9 + c] = v.mot[c * v.stride + i];
+    }
+}
+
+template <typename S>
 __global__ void set_field_kernel(EnvView<S> v, int field, const void *in) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= v.n) return;
@@ -1250,6 +1277,27 @@ int dr_get_state(dr_handle *h, int field, void *out, void *stream) {
                            as_stream(stream), view_of<float>(h), field, out);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return fail(h, DR_ERR_HIP, std::string("get_field: ") + hipGetErrorString(e));
+    return DR_OK;
+}
+
+int dr_gather_state(dr_handle *h, int field, const int32_t *env_ids, int64_t k, void *out,
+                    void *stream) {
+    if (!h) return fail(nullptr, DR_ERR_INVALID, "dr_gather_state: null handle");
+    if (!env_ids || !out || k < 0) return fail(h, DR_ERR_INVALID, "dr_gather_state: bad arguments");
+    if (field < DR_FIELD_POS || field > DR_FIELD_MOTION)
+        return fail(h, DR_ERR_INVALID, "dr_gather_state: unknown field");
+    if (field == DR_FIELD_MOTION && h->cfg.variant != DR_VARIANT_MOVING)
+        return fail(h, DR_ERR_INVALID, "dr_gather_state: motion exists only for DR_VARIANT_MOVING");
+    if (k == 0) return DR_OK;
+    DeviceGuard g(h->cfg.device);
+    if (h->cfg.state_dtype == DR_STATE_F64)
+        hipLaunchKernelGGL(gather_field_kernel<double>, dim3(grid_for(k)), dim3(kBlock), 0,
+                           as_stream(stream), view_of<double>(h), field, env_ids, k, out);
+    else
+        hipLaunchKernelGGL(gather_field_kernel<float>, dim3(grid_for(k)), dim3(kBlock), 0,
+                           as_stream(stream), view_of<float>(h), field, env_ids, k, out);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return fail(h, DR_ERR_HIP, std::string("gather_field: ") + hipGetErrorString(e));
     return DR_OK;
 }
 

@@ -168,6 +168,27 @@ class DroneBatch:
         check(self.L.dr_get_state(self.handle, fid, ptr(out), _stream(self.device)), self.handle)
         return out
 
+    def gather(self, field: str, env_ids: torch.Tensor, out: torch.Tensor | None = None):
+        """`get(field)` for the envs in env_ids (int32 device tensor), into
+        `out` if given (k,3) f64 / (k,) / (k,9) f32 for "motion"."""
+        fid = _lib.FIELDS[field]
+        k = env_ids.numel()
+        if out is None:
+            if field in _VEC_FIELDS:
+                out = torch.empty(k, 3, dtype=torch.float64, device=self.device)
+            elif field == "eps":
+                out = torch.empty(k, dtype=torch.float64, device=self.device)
+            elif field == "ep_return":
+                out = torch.empty(k, dtype=torch.float32, device=self.device)
+            elif field == "motion":
+                out = torch.empty(k, 9, dtype=torch.float32, device=self.device)
+            else:
+                out = torch.empty(k, dtype=torch.int32, device=self.device)
+        ids = env_ids.to(device=self.device, dtype=torch.int32).contiguous()
+        check(self.L.dr_gather_state(self.handle, fid, ptr(ids), k, ptr(out),
+                                     _stream(self.device)), self.handle)
+        return out
+
     def set(self, field: str, value) -> None:
         fid = _lib.FIELDS[field]
         if field in _VEC_FIELDS:

@@ -118,6 +118,8 @@ class PPOTrainer:
         self.num_updates = 0
         self.num_timesteps = 0
         self._rolled = False
+        # optional TrajectoryTensorboardCallback equivalent (trajectory.py)
+        self.trajectory = None
         self.env.reset(self.obs[0])
         if self.world > 1:
             self.sync_params()
@@ -151,6 +153,10 @@ class PPOTrainer:
             self.env.ep_len = self.ep_len[t]
             self.env.step(self.act_env, obs_out=self.obs[t + 1], rew_out=self.rewards[t],
                           done_out=self.dones[t + 1])
+            if self.trajectory is not None:
+                self.trajectory.on_step(self.dones[t + 1])
+        if self.trajectory is not None:
+            self.trajectory.flush()
         _, last_values = fwd(self.obs[T])
         K.gae(self.rewards, self.values, self.dones[:T], last_values, self.dones[T],
               cfg.gamma, cfg.gae_lambda, advantages=self.adv, returns=self.ret)

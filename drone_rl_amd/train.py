@@ -39,6 +39,9 @@ def main(argv=None):
                     help="SB3 PPO defaults of the reference (n_steps 2048, batch 64, 64x64)")
     ap.add_argument("--checkpoint", default="./dd_gpu.pt")
     ap.add_argument("--log-every", type=int, default=1)
+    ap.add_argument("--traj-dir", default=None,
+                    help="record env 0's trajectories like traj_tb.py (every 25th episode, "
+                         "blocks of 500) into this directory (npz, PNG if matplotlib)")
     a = ap.parse_args(argv)
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -54,6 +57,9 @@ def main(argv=None):
                         n_epochs=a.epochs, learning_rate=a.lr, net_arch=tuple(a.net),
                         seed=a.seed, state_dtype=a.state_dtype, variant=a.variant)
     tr = PPOTrainer(cfg, rank=rank, world_size=world)
+    if a.traj_dir and rank == 0:
+        from .trajectory import TrajectoryRecorder
+        tr.trajectory = TrajectoryRecorder(tr.env, out_dir=a.traj_dir)
     ck = a.checkpoint if world == 1 else f"{a.checkpoint}.rank{rank}"
     # *.zip = stable-baselines3 PPO checkpoint (the reference's dd.zip,
     # train.py:10-31 / 70); anything else = this trainer's bit-exact resume file

@@ -162,6 +162,12 @@ int dr_step_monitored(dr_handle *h, const float *actions, float *obs_out,
 
 /* Device-side state access (parity injection, checkpointing, get_attr). */
 int dr_get_state(dr_handle *h, int field, void *out, void *stream);
+/* dr_get_state for k selected envs: out row j = field of env env_ids[j]
+   ((k,3) f64 for vector fields, (k,) for scalars, (k,9) f32 for MOTION).
+   The per-step `get_attr('pos')` of TrajectoryTensorboardCallback
+   (traj_tb.py:34) without copying the whole batch. */
+int dr_gather_state(dr_handle *h, int field, const int32_t *env_ids, int64_t k,
+                    void *out, void *stream);
 int dr_set_state(dr_handle *h, int field, const void *in, void *stream);
 
 /* DR_RNG_HOST_UNIFORMS: device pointer to (N,5) f64 ((N,14) for the moving
