@@ -232,11 +232,12 @@ __device__ inline void block_sum(float (&x)[K], float *sh /* K*4 */) {
 // Pass 1 of the advantage normalisation: per-block (count, mean, M2)
 // (Chan et al. parallel variance) -> partials[3*b].
 __global__ __launch_bounds__(kBlock) void adv_stats_kernel(
-    int64_t m, const float *__restrict__ adv, int64_t stride, float *__restrict__ part) {
+    int64_t m, const float *__restrict__ adv, int64_t stride, const int32_t *__restrict__ rows,
+    float *__restrict__ part) {
     __shared__ float sh[8];
     const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     const int64_t cnt = min((int64_t)kBlock, m - (int64_t)blockIdx.x * kBlock);
-    const float ai = i < m ? adv[i * stride] : 0.f;
+    const float ai = i < m ? adv[(rows ? (int64_t)rows[i] : i) * stride] : 0.f;
     float x[1] = {ai};
     block_sum<1>(x, sh);
     const float mean = x[0] / (float)cnt;
@@ -507,6 +508,7 @@ __device__ inline float dot4(float4 a, float4 b) {
 template <int K>
 __global__ __launch_bounds__(kBlock) void linear_tanh_kernel(int64_t m, int n,
                                                              const float *__restrict__ x,
+                                                             const int32_t *__restrict__ rows,
                                                              const float *__restrict__ w,
                                                              const float *__restrict__ b,
                                                              float *__restrict__ h) {
@@ -539,11 +541,14 @@ __global__ __launch_bounds__(kBlock) void linear_tanh_kernel(int64_t m, int n,
     // row's arithmetic (software pipelining hides the load latency)
     const int64_t stride = (int64_t)gridDim.x * 4;
     int64_t r = (int64_t)blockIdx.x * 4 + wid;
-    float xnext = (r < m && lane < K) ? x[r * K + lane] : 0.f;
+    // row r of the input is x[rows[r]] when a row index is given (a
+    // minibatch read in place from the rollout buffer), else x[r]
+    auto xrow = [&](int64_t q) -> int64_t { return rows ? (int64_t)rows[q] : q; };
+    float xnext = (r < m && lane < K) ? x[xrow(r) * K + lane] : 0.f;
     for (; r < m; r += stride) {
         const float xv = xnext;
         const int64_t rn = r + stride;
-        xnext = (rn < m && lane < K) ? x[rn * K + lane] : 0.f;
+        xnext = (rn < m && lane < K) ? x[xrow(rn) * K + lane] : 0.f;
         float acc[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int k = 0; k < K; ++k) {
@@ -606,6 +611,7 @@ struct HeadArgs {
     const float *w_act, *b_act, *w_val, *b_val, *log_std;
     const float4 *actions;
     const float *aux;  // (m,3): old_logp, advantage, return
+    const int32_t *rows;  // nullable: minibatch row r reads actions / aux row rows[r]
     float clip, ent_coef, vf_coef;
     int normalize;
     const float *adv_part;
@@ -666,7 +672,8 @@ __global__ __launch_bounds__(kBlock) void ppo_head_kernel(HeadArgs a) {
         }
         // this lane's row (lane < nr): its loss inputs, loaded while the dots run
         const bool own = lane < nr;
-        const int64_t ro = r0 + (own ? lane : 0);
+        const int64_t rr = r0 + (own ? lane : 0);
+        const int64_t ro = a.rows ? (int64_t)a.rows[rr] : rr;
         const float4 ac4 = a.actions[ro];
         const float lp_old = a.aux[3 * ro], A = a.aux[3 * ro + 1], R = a.aux[3 * ro + 2];
         float mu[4] = {0.f, 0.f, 0.f, 0.f}, v = 0.f;
@@ -766,6 +773,7 @@ __global__ __launch_bounds__(kBlock) void first_layer_bwd_kernel(int64_t m, int 
                                                                  const float *__restrict__ gh,
                                                                  const float *__restrict__ h,
                                                                  const float *__restrict__ x,
+                                                                 const int32_t *__restrict__ rows,
                                                                  float *__restrict__ part) {
     extern __shared__ float sh_fl[];  // 4 * P
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
@@ -788,7 +796,8 @@ __global__ __launch_bounds__(kBlock) void first_layer_bwd_kernel(int64_t m, int 
             const bool ok = act && i < nr;
             g[i] = ok ? ld4(gh + (r0 + i) * n + c0) : z4;
             y[i] = ok ? ld4(h + (r0 + i) * n + c0) : z4;
-            xv[i] = (i < nr && lane < K) ? x[(r0 + i) * K + lane] : 0.f;
+            const int64_t xr = rows ? (int64_t)rows[min(r0 + i, m - 1)] : r0 + i;
+            xv[i] = (i < nr && lane < K) ? x[xr * K + lane] : 0.f;
         }
 #pragma unroll
         for (int i = 0; i < kFirstTile; ++i) {
@@ -1128,7 +1137,7 @@ int dr_ppo_loss(int64_t m, const float *mean, const float *log_std, const float 
     hipStream_t st = as_stream(stream);
     if (norm) {
         hipLaunchKernelGGL(adv_stats_kernel, dim3(nb), dim3(kBlock), 0, st, m, advantages,
-                           aux_stride, adv_part);
+                           aux_stride, (const int32_t *)nullptr, adv_part);
         int rc = check_launch("dr_ppo_loss stats");
         if (rc) return rc;
     }
@@ -1176,8 +1185,8 @@ int dr_clip_adam(int64_t n, float *params, float *grads, float *exp_avg, float *
 }
 
 
-int dr_linear_tanh(int64_t m, int64_t k, int64_t n, const float *x, const float *w,
-                   const float *b, float *h, void *stream) {
+int dr_linear_tanh(int64_t m, int64_t k, int64_t n, const float *x, const int32_t *rows,
+                   const float *w, const float *b, float *h, void *stream) {
     if (m < 1 || !x || !w || !b || !h || n < 4 || n > 256 || (n & 3))
         return fail0(DR_ERR_INVALID, "dr_linear_tanh: bad arguments (need 4 <= n <= 256, n % 4 == 0)");
     if ((((uintptr_t)h) | ((uintptr_t)w)) & 15)
@@ -1189,7 +1198,7 @@ int dr_linear_tanh(int64_t m, int64_t k, int64_t n, const float *x, const float 
 #define DR_LT_CASE(K)                                                                      \
     case K:                                                                                \
         hipLaunchKernelGGL(linear_tanh_kernel<K>, dim3(nb), dim3(kBlock), 0, st, m, (int)n, \
-                           x, w, b, h);                                                    \
+                           x, rows, w, b, h);                                              \
         break;
         DR_LT_CASE(4) DR_LT_CASE(8) DR_LT_CASE(12) DR_LT_CASE(15) DR_LT_CASE(16)
         DR_LT_CASE(18) DR_LT_CASE(24) DR_LT_CASE(32)
@@ -1227,7 +1236,8 @@ size_t dr_ppo_head_workspace_bytes(int64_t m, int64_t hd) {
 int dr_ppo_head_loss_backward(int64_t m, int64_t hd, const float *h_pi, const float *h_vf,
                               const float *w_act, const float *b_act, const float *w_val,
                               const float *b_val, const float *log_std, const float *actions,
-                              const float *aux, float clip_range, float ent_coef,
+                              const float *aux, const int32_t *rows, float clip_range,
+                              float ent_coef,
                               float vf_coef, int normalize_advantage, float *gz_pi,
                               float *gz_vf, float *g_w_act, float *g_b_act, float *g_w_val,
                               float *g_b_val, float *g_b_pi, float *g_b_vf, float *g_log_std,
@@ -1251,14 +1261,14 @@ int dr_ppo_head_loss_backward(int64_t m, int64_t hd, const float *h_pi, const fl
     hipStream_t st = as_stream(stream);
     if (norm) {
         hipLaunchKernelGGL(adv_stats_kernel, dim3(anb), dim3(kBlock), 0, st, m, aux + 1,
-                           (int64_t)3, adv_part);
+                           (int64_t)3, rows, adv_part);
         int rc = check_launch("dr_ppo_head_loss_backward stats");
         if (rc) return rc;
     }
     const int nb = head_blocks(m);
     const int P = kHeadFixed + 7 * (int)hd;
     HeadArgs a{m, (int)hd, h_pi, h_vf, w_act, b_act, w_val, b_val, log_std,
-               reinterpret_cast<const float4 *>(actions), aux, clip_range, ent_coef,
+               reinterpret_cast<const float4 *>(actions), aux, rows, clip_range, ent_coef,
                vf_coef, norm, adv_part, anb, gz_pi, gz_vf, part, P};
     hipLaunchKernelGGL(ppo_head_kernel, dim3(nb), dim3(kBlock), sizeof(float) * 4 * P, st, a);
     int rc = check_launch("dr_ppo_head_loss_backward");
@@ -1292,8 +1302,9 @@ size_t dr_first_layer_backward_workspace_bytes(int64_t m, int64_t k, int64_t n) 
 }
 
 int dr_first_layer_backward(int64_t m, int64_t k, int64_t n, const float *grad_h,
-                            const float *h, const float *x, float *grad_w, float *grad_b,
-                            void *workspace, size_t workspace_bytes, void *stream) {
+                            const float *h, const float *x, const int32_t *rows, float *grad_w,
+                            float *grad_b, void *workspace, size_t workspace_bytes,
+                            void *stream) {
     if (m < 1 || !grad_h || !h || !x || !grad_w || !grad_b || n < 4 || n > 256 || (n & 3))
         return fail0(DR_ERR_INVALID, "dr_first_layer_backward: bad arguments");
     if ((((uintptr_t)grad_h) | ((uintptr_t)h)) & 15)
@@ -1314,7 +1325,7 @@ int dr_first_layer_backward(int64_t m, int64_t k, int64_t n, const float *grad_h
             (void)hipFuncSetAttribute(reinterpret_cast<const void *>(first_layer_bwd_kernel<K>), \
                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds); \
         hipLaunchKernelGGL(first_layer_bwd_kernel<K>, dim3(nb), dim3(kBlock), lds, st, m,   \
-                           (int)n, grad_h, h, x, part);                                    \
+                           (int)n, grad_h, h, x, rows, part);                              \
         break;
         DR_FL_CASE(4) DR_FL_CASE(8) DR_FL_CASE(12) DR_FL_CASE(15) DR_FL_CASE(16)
         DR_FL_CASE(18) DR_FL_CASE(24) DR_FL_CASE(32)

@@ -255,7 +255,7 @@ class FusedTrainStep:
         torch.sum(ws.view(2, C, N, Kd), dim=1, out=out)
 
     @torch.no_grad()
-    def step(self, obs, actions, aux, head):
+    def step(self, obs, actions, aux, head, rows=None):
         """One PPO.train minibatch on the fused path: hidden forward
         (dr_linear_tanh for the first layer, hipBLASLt addmm + tanh above),
         dr_ppo_head_loss_backward (heads, loss, backward through the heads
@@ -265,19 +265,23 @@ class FusedTrainStep:
         layout keeps the two MLPs' tensors of a layer adjacent), tanh
         backward down the stack, and the first layer by
         dr_first_layer_backward (its grad_z is never stored).
+        With `rows` (int32, m), obs / actions / aux are the whole rollout
+        buffers and minibatch row r is their row rows[r] (no gather copies).
         Returns (flat grad, stats (8))."""
         self._alloc_fused()
-        pol, M = self.pol, obs.shape[0]
+        pol, M = self.pol, (obs.shape[0] if rows is None else rows.numel())
         depth, top = len(pol.net_arch), len(pol.net_arch) - 1
-        hs = hidden_forward(pol, obs, self._acts, self._acts2)
+        hs = hidden_forward(pol, obs, self._acts, self._acts2, rows)
         gz = self._gz2[top]
         stats = head(hs["pi"][top], hs["vf"][top], pol.p("action.w"), pol.p("action.b"),
                      pol.p("value.w"), pol.p("value.b"), pol.log_std, actions, aux,
                      gz[0], gz[1], self.gview("action.w"),
                      self.gview("action.b"), self.gview("value.w"), self.gview("value.b"),
                      self.gview(f"pi{top}.b"), self.gview(f"vf{top}.b"),
-                     self.gview("log_std"))
+                     self.gview("log_std"), rows)
         if depth == 1:                        # the head kernel gave grad_z of layer 0
+            if rows is not None:
+                obs = obs.index_select(0, rows.long())
             for j, pre in enumerate(("pi", "vf")):
                 self._wgrad(gz[j], obs, self.gview(f"{pre}0.w"))
             return self.grad, stats
@@ -291,7 +295,7 @@ class FusedTrainStep:
                 # first layer: tanh backward + weight/bias gradients fused
                 for j, pre in enumerate(("pi", "vf")):
                     self._first(g[j], x[j], obs, self.gview(f"{pre}0.w"),
-                                self.gview(f"{pre}0.b"))
+                                self.gview(f"{pre}0.b"), rows)
             else:
                 gz = self._gz2[k - 1]
                 for j, pre in enumerate(("pi", "vf")):
@@ -362,13 +366,14 @@ def fusable(pol: ActorCritic) -> bool:
 
 
 @torch.no_grad()
-def hidden_forward(pol: ActorCritic, obs, acts, acts2=None):
+def hidden_forward(pol: ActorCritic, obs, acts, acts2=None, rows=None):
     """Hidden activations of the pi and vf MLPs into preallocated buffers
     acts[pre][k] (M, net_arch[k]); with acts2 (the (2, M, n) buffers that
-    acts views) each layer's tanh runs once over both MLPs."""
+    acts views) each layer's tanh runs once over both MLPs; with rows the
+    input rows are obs[rows]."""
     from . import ppo_kernels as K
     for j, pre in enumerate(("pi", "vf")):
-        K.linear_tanh(obs, pol.p(f"{pre}0.w"), pol.p(f"{pre}0.b"), acts[pre][0])
+        K.linear_tanh(obs, pol.p(f"{pre}0.w"), pol.p(f"{pre}0.b"), acts[pre][0], rows)
     for k in range(1, len(pol.net_arch)):
         for pre in ("pi", "vf"):
             torch.addmm(pol.p(f"{pre}{k}.b"), acts[pre][k - 1], pol.p(f"{pre}{k}.w").t(),

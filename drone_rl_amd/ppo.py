@@ -179,6 +179,9 @@ class PPOTrainer:
                              counter=self.num_updates * cfg.n_epochs + epoch)
             for k in range(nmb):
                 idx = perm[k * M:(k + 1) * M]
+                # gathered copies: the consumers then stream rows in order
+                # (reading through `rows=idx` in the kernels measured 3 %
+                # slower: 60-B random rows waste most of each cache line)
                 K.gather_rows(idx, obs_flat, out=self.mb_obs)
                 K.gather_rows(idx, act_flat, out=self.mb_act)
                 K.gather_rows(idx, self.aux, out=self.mb_aux)

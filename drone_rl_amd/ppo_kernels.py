@@ -162,12 +162,21 @@ class ClipAdam:
 LINEAR_TANH_K = (4, 8, 12, 15, 16, 18, 24, 32)
 
 
-def linear_tanh(x, w, b, out):
-    """out = tanh(x w^T + b) for a narrow input x (m,k), k in LINEAR_TANH_K."""
-    m, k = x.shape
+def _rows(rows):
+    if rows is None:
+        return None
+    assert rows.dtype == torch.int32 and rows.is_contiguous()
+    return ptr(rows)
+
+
+def linear_tanh(x, w, b, out, rows=None):
+    """out = tanh(x w^T + b) for a narrow input x (., k), k in LINEAR_TANH_K;
+    row r of the input is x[rows[r]] when rows (int32) is given."""
+    k = x.shape[1]
+    m = out.shape[0]
     n = w.shape[0]
-    check(_lib.lib().dr_linear_tanh(m, k, n, ptr(_f32(x)), ptr(_f32(w)), ptr(_f32(b)),
-                                    ptr(out), _s(x)))
+    check(_lib.lib().dr_linear_tanh(m, k, n, ptr(_f32(x)), _rows(rows), ptr(_f32(w)),
+                                    ptr(_f32(b)), ptr(out), _s(x)))
     return out
 
 
@@ -194,12 +203,16 @@ class HeadLossBackward:
         self.stats = torch.empty(8, dtype=torch.float32, device=device)
 
     def __call__(self, h_pi, h_vf, w_act, b_act, w_val, b_val, log_std, actions, aux,
-                 gz_pi, gz_vf, g_w_act, g_b_act, g_w_val, g_b_val, g_b_pi, g_b_vf, g_log_std):
-        assert h_pi.shape == (self.m, self.hd) and aux.shape == (self.m, 3)
+                 gz_pi, gz_vf, g_w_act, g_b_act, g_w_val, g_b_val, g_b_pi, g_b_vf, g_log_std,
+                 rows=None):
+        """actions (.,4) / aux (.,3) rows are read as [rows[r]] when rows
+        (int32, m) is given, else the first m rows."""
+        assert h_pi.shape == (self.m, self.hd) and aux.shape[1] == 3
+        assert rows is not None or aux.shape[0] == self.m
         check(_lib.lib().dr_ppo_head_loss_backward(
             self.m, self.hd, ptr(_f32(h_pi)), ptr(_f32(h_vf)), ptr(_f32(w_act)),
             ptr(_f32(b_act)), ptr(_f32(w_val)), ptr(_f32(b_val)), ptr(_f32(log_std)),
-            ptr(_f32(actions)), ptr(_f32(aux)), float(self.clip), float(self.ent),
+            ptr(_f32(actions)), ptr(_f32(aux)), _rows(rows), float(self.clip), float(self.ent),
             float(self.vf), self.norm, ptr(gz_pi), ptr(gz_vf), ptr(g_w_act), ptr(g_b_act),
             ptr(g_w_val), ptr(g_b_val), ptr(g_b_pi), ptr(g_b_vf), ptr(g_log_std),
             ptr(self.stats), ptr(self.ws), self.ws.numel(), _s(h_pi)))
@@ -215,8 +228,9 @@ class FirstLayerBackward:
         self.ws = torch.empty(_lib.lib().dr_first_layer_backward_workspace_bytes(m, k, n),
                               dtype=torch.uint8, device=device)
 
-    def __call__(self, grad_h, h, x, grad_w, grad_b):
-        assert grad_h.shape == (self.m, self.n) and x.shape == (self.m, self.k)
+    def __call__(self, grad_h, h, x, grad_w, grad_b, rows=None):
+        assert grad_h.shape == (self.m, self.n) and x.shape[1] == self.k
+        assert rows is not None or x.shape[0] == self.m
         check(_lib.lib().dr_first_layer_backward(
-            self.m, self.k, self.n, ptr(_f32(grad_h)), ptr(_f32(h)), ptr(_f32(x)), ptr(grad_w),
-            ptr(grad_b), ptr(self.ws), self.ws.numel(), _s(h)))
+            self.m, self.k, self.n, ptr(_f32(grad_h)), ptr(_f32(h)), ptr(_f32(x)), _rows(rows),
+            ptr(grad_w), ptr(grad_b), ptr(self.ws), self.ws.numel(), _s(h)))

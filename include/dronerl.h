@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define DR_ABI_VERSION 2
+#define DR_ABI_VERSION 3
 
 enum dr_status {
     DR_OK = 0,
@@ -241,21 +241,25 @@ int dr_tanh_backward(int64_t m, int64_t n, const float *grad_h, const float *h,
    for x (m,k), W (n,k), b (n), h (m,n) (SB3 MlpExtractor's Linear + Tanh,
    the narrow-input layer).  k in {4,8,12,15,16,18,24,32}; n % 4 == 0,
    n <= 256; h 16-byte aligned.  Replaces an addmm plus a separate tanh pass
-   over the (m,n) activation. */
+   over the (m,n) activation.  `rows` (nullable, m int32): input row r is
+   x[rows[r]] -- a minibatch read in place from the rollout buffer through
+   its permutation (RolloutBuffer.get without the gather copy). */
 int dr_linear_tanh(int64_t m, int64_t k, int64_t n, const float *x,
-                   const float *w, const float *b, float *h, void *stream);
+                   const int32_t *rows, const float *w, const float *b, float *h,
+                   void *stream);
 
 /* Backward of the first layer h = tanh(x W^T + b), fused: for grad_h (m,n)
    = dLoss/dh, forms grad_z = grad_h * (1 - h^2) in registers (never stored)
    and writes grad_w (n,k) = grad_z^T x and grad_b (n) = sum_r grad_z
    (dr_tanh_backward + the weight-gradient GEMM in one pass; the input
    gradient of the first layer is not needed).  k as dr_linear_tanh; n % 4
-   == 0, n <= 256; grad_h and h 16-byte aligned.  Deterministic.
+   == 0, n <= 256; grad_h and h 16-byte aligned.  `rows` as dr_linear_tanh
+   (x row r = x[rows[r]]).  Deterministic.
    `workspace` >= dr_first_layer_backward_workspace_bytes(m, k, n). */
 size_t dr_first_layer_backward_workspace_bytes(int64_t m, int64_t k, int64_t n);
 int dr_first_layer_backward(int64_t m, int64_t k, int64_t n, const float *grad_h,
-                            const float *h, const float *x, float *grad_w,
-                            float *grad_b, void *workspace,
+                            const float *h, const float *x, const int32_t *rows,
+                            float *grad_w, float *grad_b, void *workspace,
                             size_t workspace_bytes, void *stream);
 
 /* Policy heads for rollouts (ActorCriticPolicy.forward's action_net /
@@ -268,7 +272,8 @@ int dr_policy_heads(int64_t m, int64_t hd, const float *h_pi, const float *h_vf,
 
 /* One PPO.train minibatch step from the top hidden layer down, fused:
    heads (as dr_policy_heads), the loss of dr_ppo_loss (aux = interleaved
-   (m,3) rows of old_logp, advantage, return), and the backward through the
+   (m,3) rows of old_logp, advantage, return; with `rows` non-null, minibatch
+   row r reads actions / aux row rows[r]), and the backward through the
    heads and the top tanh:
      gz_pi = (dL/dmean W_act) * (1 - h_pi^2),  gz_vf = (dL/dvalue W_val) *
      (1 - h_vf^2)   (m,hd) each, for the hidden-layer backward,
@@ -283,7 +288,8 @@ int dr_ppo_head_loss_backward(int64_t m, int64_t hd, const float *h_pi,
                               const float *b_act, const float *w_val,
                               const float *b_val, const float *log_std,
                               const float *actions, const float *aux,
-                              float clip_range, float ent_coef, float vf_coef,
+                              const int32_t *rows, float clip_range,
+                              float ent_coef, float vf_coef,
                               int normalize_advantage, float *gz_pi,
                               float *gz_vf, float *g_w_act, float *g_b_act,
                               float *g_w_val, float *g_b_val, float *g_b_pi,

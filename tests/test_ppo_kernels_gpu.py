@@ -263,3 +263,24 @@ def test_first_layer_backward_matches_torch(k, n, m):
     tol = 1e-5 * (gz.abs().t() @ x.double().abs()).max().item()
     assert (gw.double() - ref_w).abs().max().item() <= tol
     assert (gb.double() - ref_b).abs().max().item() <= 1e-5 * gz.abs().sum(0).max().item()
+
+
+def test_fused_step_rows_in_place_equals_gathered():
+    """Reading the minibatch through the permutation (rows=) inside the
+    kernels is bitwise the same as gathering it first."""
+    from drone_rl_amd import ppo_kernels as K
+    from drone_rl_amd.policy import ActorCritic, FusedTrainStep
+    torch.manual_seed(2)
+    pol = ActorCritic(15, 4, (256, 256), device="cuda", seed=5)
+    total, m = 3 * 4096, 4096
+    obs = torch.randn(total, 15, device="cuda")
+    act = torch.rand(total, 4, device="cuda") * 7.3575
+    aux = torch.randn(total, 3, device="cuda")
+    rows = torch.randperm(total, device="cuda")[:m].to(torch.int32)
+    fs = FusedTrainStep(pol, m)
+    head = K.HeadLossBackward(m, 256, "cuda")
+    g1, s1 = fs.step(obs, act, aux, head, rows=rows)
+    g1, s1 = g1.clone(), s1.clone()
+    r = rows.long()
+    g2, s2 = fs.step(obs[r].contiguous(), act[r].contiguous(), aux[r].contiguous(), head)
+    assert torch.equal(g1, g2) and torch.equal(s1, s2)
