@@ -169,7 +169,11 @@ def time_ppo(args, rank, world, device):
                        "optimizer_steps_per_update": cfg.n_epochs * cfg.n_steps *
                        cfg.num_envs // cfg.batch_size,
                        "net_arch": list(cfg.net_arch), "mlp_dtype": "fp32",
-                       "grad_allreduce": "rccl" if world > 1 else "none"},
+                       "grad_allreduce": ({"nccl": "rccl"}.get(dist.get_backend(),
+                                                               dist.get_backend())
+                                          + " (2 buckets, overlapped with the "
+                                            "first-layer backward)") if world > 1
+                       else "none"},
             "last_update_stats": stats, "episodes": es}
 
 

@@ -4,9 +4,12 @@ The env batch shards with no exchange at all: rank r owns global env ids
 [r*N, (r+1)*N) (its Philox streams are keyed by those ids).  PPO adds the
 only collectives on the hot path:
   * one broadcast of the flat parameter buffer at start (rank 0 -> all),
-  * one all-reduce (sum, then 1/world) of the flat fp32 gradient per
-    optimizer step -- 141,065 floats = 564 KB for the 2x256 net, a single
-    bucket: on xGMI this is latency-bound, so it is never split,
+  * the all-reduce (sum, then 1/world) of the flat fp32 gradient per
+    optimizer step -- 141,065 floats = 564 KB for the 2x256 net -- as two
+    buckets: everything but the first layer (started asynchronously as soon
+    as the fused backward has finished it, so it overlaps the first-layer
+    backward) and the first layer (8k floats) at the end.  Buckets are not
+    split further: at this size xGMI is latency-bound,
   * one all-reduce of 3 episode-statistics scalars per logged update.
 Backend "nccl" is RCCL on ROCm; every function also runs under gloo (CPU
 tests, tests/test_dist_cpu.py).
@@ -45,3 +48,40 @@ def allreduce_max_(t: torch.Tensor, world: int, group=None) -> torch.Tensor:
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
     return t
+
+
+class BucketedAllReduce:
+    """Mean all-reduce of one flat buffer in buckets started as they become
+    ready (async collectives on the backend's stream; each waits for the
+    work already queued on the current stream), then finished together."""
+
+    def __init__(self, flat: torch.Tensor, world: int, group=None):
+        self.flat, self.world, self.group = flat, world, group
+        self.works = []
+        self.done_ranges = []
+
+    def start(self, lo: int, hi: int):
+        if self.world > 1 and hi > lo:
+            self.works.append(dist.all_reduce(self.flat[lo:hi], op=dist.ReduceOp.SUM,
+                                              group=self.group, async_op=True))
+            self.done_ranges.append((lo, hi))
+
+    def finish(self):
+        """Start whatever was not covered, wait for all, scale by 1/world."""
+        if self.world <= 1:
+            return self.flat
+        gaps, pos = [], 0
+        for lo, hi in sorted(self.done_ranges):
+            if lo > pos:
+                gaps.append((pos, lo))
+            pos = max(pos, hi)
+        if pos < self.flat.numel():
+            gaps.append((pos, self.flat.numel()))
+        for lo, hi in gaps:
+            self.start(lo, hi)
+        for w in self.works:
+            w.wait()
+        self.works.clear()
+        self.done_ranges.clear()
+        self.flat.mul_(1.0 / self.world)
+        return self.flat

@@ -240,6 +240,12 @@ class FusedTrainStep:
         self._ws2 = torch.empty(2 * self.C * max(pol.net_arch) ** 2, **f32) if self.C > 1 else None
         self._first = self.K.FirstLayerBackward(M, pol.obs_dim, pol.net_arch[0], pol.device)
 
+    def first_layer_end(self) -> int:
+        """Flat offset where the first layer's parameters end (they come
+        first in the interleaved layout)."""
+        return self.pol.offsets["pi1.w"][0] if len(self.pol.net_arch) > 1 else \
+            self.grad.numel()
+
     def _wgrad2(self, gz, x, out):
         """out (2, N, K) = gz[j]^T x[j] for both MLPs in one batched split-K
         GEMM over 2C row chunks, then one fixed-order sum over the chunks."""
@@ -255,7 +261,7 @@ class FusedTrainStep:
         torch.sum(ws.view(2, C, N, Kd), dim=1, out=out)
 
     @torch.no_grad()
-    def step(self, obs, actions, aux, head, rows=None):
+    def step(self, obs, actions, aux, head, rows=None, on_ready=None):
         """One PPO.train minibatch on the fused path: hidden forward
         (dr_linear_tanh for the first layer, hipBLASLt addmm + tanh above),
         dr_ppo_head_loss_backward (heads, loss, backward through the heads
@@ -267,6 +273,10 @@ class FusedTrainStep:
         dr_first_layer_backward (its grad_z is never stored).
         With `rows` (int32, m), obs / actions / aux are the whole rollout
         buffers and minibatch row r is their row rows[r] (no gather copies).
+        `on_ready(lo, hi)` is called (depth >= 2) as soon as grad[lo:hi] --
+        every parameter except the first layer's -- is final on the current
+        stream, so a data-parallel caller can start that bucket's
+        all-reduce while the first-layer backward still runs.
         Returns (flat grad, stats (8))."""
         self._alloc_fused()
         pol, M = self.pol, (obs.shape[0] if rows is None else rows.numel())
@@ -292,6 +302,8 @@ class FusedTrainStep:
             g = self._g2.view(-1)[:2 * M * n_in].view(2, M, n_in)
             torch.bmm(gz, pol.p2(k, "w"), out=g)
             if k == 1:
+                if on_ready is not None:
+                    on_ready(self.first_layer_end(), self.grad.numel())
                 # first layer: tanh backward + weight/bias gradients fused
                 for j, pre in enumerate(("pi", "vf")):
                     self._first(g[j], x[j], obs, self.gview(f"{pre}0.w"),

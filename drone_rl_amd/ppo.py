@@ -186,14 +186,22 @@ class PPOTrainer:
                 K.gather_rows(idx, act_flat, out=self.mb_act)
                 K.gather_rows(idx, self.aux, out=self.mb_aux)
                 if self.use_fused:
-                    grad, st = self.fused.step(self.mb_obs, self.mb_act, self.mb_aux,
-                                               self.head)
+                    if self.world > 1:
+                        # DP: the gradient all-reduce starts while the
+                        # first-layer backward is still running
+                        bar = D.BucketedAllReduce(self.fused.grad, self.world, self.pg)
+                        grad, st = self.fused.step(self.mb_obs, self.mb_act, self.mb_aux,
+                                                   self.head, on_ready=bar.start)
+                        bar.finish()
+                    else:
+                        grad, st = self.fused.step(self.mb_obs, self.mb_act, self.mb_aux,
+                                                   self.head)
                 else:
                     mean, value, cache = self.fused.forward(self.mb_obs)
                     g_mean, g_ls, g_v, st = self.loss(mean, log_std, value, self.mb_act,
                                                       aux=self.mb_aux)
                     grad = self.fused.backward(self.mb_obs, cache, g_mean, g_v, g_ls)
-                self._allreduce_grad(grad)
+                    self._allreduce_grad(grad)
                 self.opt.step(grad)
                 stats[j].copy_(st)
                 j += 1

@@ -70,6 +70,12 @@ def _worker(rank, world, port):
     # all ranks hold the identical reduced gradient
     g_max = D.allreduce_max_(g.clone(), world)
     assert torch.equal(g_max, g)
+    # 2b. the bucketed form (a middle bucket started early, the gaps at the
+    # end) gives exactly the single all-reduce's result
+    bar = D.BucketedAllReduce(g_local.clone(), world)
+    bar.start(1000, g_local.numel() - 500)
+    gb = bar.finish()
+    assert torch.equal(gb, g)
     # 3. env shards are disjoint and cover [0, world*N)
     lo, hi = D.env_shard(rank, 65536)
     r = torch.tensor([lo, hi], dtype=torch.int64)
