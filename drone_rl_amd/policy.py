@@ -299,11 +299,12 @@ class FusedTrainStep:
             x = self._acts2[k - 1]
             n_in = x.shape[2]
             self._wgrad2(gz, x, pol.p2(k, "w", self.grad))
+            if k == 1 and on_ready is not None:
+                # all but the first layer's gradient is final from here on
+                on_ready(self.first_layer_end(), self.grad.numel())
             g = self._g2.view(-1)[:2 * M * n_in].view(2, M, n_in)
             torch.bmm(gz, pol.p2(k, "w"), out=g)
             if k == 1:
-                if on_ready is not None:
-                    on_ready(self.first_layer_end(), self.grad.numel())
                 # first layer: tanh backward + weight/bias gradients fused
                 for j, pre in enumerate(("pi", "vf")):
                     self._first(g[j], x[j], obs, self.gview(f"{pre}0.w"),
