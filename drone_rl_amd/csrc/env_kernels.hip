@@ -225,14 +225,37 @@ template <typename S>
 __device__ inline void gym_reset_regs(const EnvView<S> &v, int64_t i, int mode,
                                       S st[F_N], int32_t ep_old, double eps) {
     const int32_t ep_new = ep_old + 1;        // ep_num += 1          (61)
-    double u[5];
-    reset_uniforms<5>(v, i, ep_new, mode, u);
-    DR_STAMP(6);
     if (!DR_PREFETCH_EPS) eps = v.eps[i];
     if (ep_new % 2000 == 0) {                 // curriculum bump      (68-70)
         eps += 0.1;
         v.eps[i] = eps;
     }
+    double u[5];
+    if (mode == 0 && DR_ABLATE != 5) {
+        // Philox block 0 = (pos x, pos y, target x, target y); block 1 word
+        // 0 = target z.  The target draws are multiplied by eps, and 0 * u
+        // is exactly +0 for the uniforms in [0,1): while the curriculum is
+        // at eps == 0 (the first 2000 episodes of every env) block 1 cannot
+        // change any result bit, so it is skipped.
+        const uint64_t gid = (uint64_t)(v.env_id_offset + i);
+        const u32x4 r0 = philox4x32_10(
+            u32x4{(uint32_t)ep_new, (uint32_t)gid, (uint32_t)(gid >> 32), TAG_RESET},
+            v.seed_lo, v.seed_hi);
+        u[0] = u01_w32(r0.x);
+        u[1] = u01_w32(r0.y);
+        u[2] = u01_w32(r0.z);
+        u[3] = u01_w32(r0.w);
+        u[4] = 0.0;
+        if (eps != 0.0) {
+            const u32x4 r1 = philox4x32_10(
+                u32x4{(uint32_t)ep_new, (uint32_t)gid, (uint32_t)(gid >> 32), TAG_RESET | 1u},
+                v.seed_lo, v.seed_hi);
+            u[4] = u01_w32(r1.x);
+        }
+    } else {
+        reset_uniforms<5>(v, i, ep_new, mode, u);
+    }
+    DR_STAMP(6);
     v.ep_num[i] = ep_new;
     st[F_POS + 0] = (S)(u[0] - 0.5);          // (57)
     st[F_POS + 1] = (S)(u[1] - 0.5);
