@@ -498,6 +498,9 @@ __device__ inline float tanh_fast(float x) {
 }
 
 __device__ inline float4 ld4(const float *p) { return *reinterpret_cast<const float4 *>(p); }
+__device__ inline float4 tanh4(float4 v) {
+    return make_float4(tanh_fast(v.x), tanh_fast(v.y), tanh_fast(v.z), tanh_fast(v.w));
+}
 __device__ inline float dot4(float4 a, float4 b) {
     return fmaf(a.w, b.w, fmaf(a.z, b.z, fmaf(a.y, b.y, a.x * b.x)));
 }
@@ -566,7 +569,7 @@ __global__ __launch_bounds__(kBlock) void linear_tanh_kernel(int64_t m, int n,
 // Policy heads for inference (rollouts): mean = h_pi Wa^T + ba (m,4),
 // value = h_vf Wv^T + bv (m).
 __global__ __launch_bounds__(kBlock) void policy_heads_kernel(
-    int64_t m, int hd, const float *__restrict__ h_pi, const float *__restrict__ h_vf,
+    int64_t m, int hd, int preact, const float *__restrict__ h_pi, const float *__restrict__ h_vf,
     const float *__restrict__ w_act, const float *__restrict__ b_act,
     const float *__restrict__ w_val, const float *__restrict__ b_val,
     float4 *__restrict__ mean, float *__restrict__ value) {
@@ -579,8 +582,12 @@ __global__ __launch_bounds__(kBlock) void policy_heads_kernel(
     for (int j = 0; j < 4; ++j) wa[j] = act ? ld4(w_act + j * hd + c0) : z4;
     const float4 wv = act ? ld4(w_val + c0) : z4;
     for (int64_t r = (int64_t)blockIdx.x * 4 + wid; r < m; r += (int64_t)gridDim.x * 4) {
-        const float4 hp = act ? ld4(h_pi + r * hd + c0) : z4;
-        const float4 hv = act ? ld4(h_vf + r * hd + c0) : z4;
+        float4 hp = act ? ld4(h_pi + r * hd + c0) : z4;
+        float4 hv = act ? ld4(h_vf + r * hd + c0) : z4;
+        if (preact) {         // inputs are pre-activations: the layer's tanh here
+            hp = tanh4(hp);
+            hv = tanh4(hv);
+        }
         float d[5];
 #pragma unroll
         for (int j = 0; j < 4; ++j) d[j] = wave_allsum(dot4(hp, wa[j]));
@@ -607,6 +614,7 @@ constexpr int kHeadFixed = 14;
 struct HeadArgs {
     int64_t m;
     int hd;
+    int preact;  // h_pi / h_vf are pre-activations z; the top tanh is applied here
     const float *h_pi, *h_vf;
     const float *w_act, *b_act, *w_val, *b_val, *log_std;
     const float4 *actions;
@@ -669,6 +677,13 @@ __global__ __launch_bounds__(kBlock) void ppo_head_kernel(HeadArgs a) {
             const bool ok = act && i < nr;
             hp[i] = ok ? ld4(a.h_pi + (r0 + i) * hd + c0) : z4;
             hv[i] = ok ? ld4(a.h_vf + (r0 + i) * hd + c0) : z4;
+        }
+        if (a.preact) {
+#pragma unroll
+            for (int i = 0; i < kHeadTile; ++i) {
+                hp[i] = tanh4(hp[i]);
+                hv[i] = tanh4(hv[i]);
+            }
         }
         // this lane's row (lane < nr): its loss inputs, loaded while the dots run
         const bool own = lane < nr;
@@ -1210,7 +1225,7 @@ int dr_linear_tanh(int64_t m, int64_t k, int64_t n, const float *x, const int32_
     return check_launch("dr_linear_tanh");
 }
 
-int dr_policy_heads(int64_t m, int64_t hd, const float *h_pi, const float *h_vf,
+int dr_policy_heads(int64_t m, int64_t hd, int preact, const float *h_pi, const float *h_vf,
                     const float *w_act, const float *b_act, const float *w_val,
                     const float *b_val, float *mean, float *value, void *stream) {
     if (m < 1 || hd < 4 || hd > 256 || (hd & 3) || !h_pi || !h_vf || !w_act || !b_act ||
@@ -1220,7 +1235,7 @@ int dr_policy_heads(int64_t m, int64_t hd, const float *h_pi, const float *h_vf,
          ((uintptr_t)mean)) & 15)
         return fail0(DR_ERR_INVALID, "dr_policy_heads: buffers must be 16-byte aligned");
     hipLaunchKernelGGL(policy_heads_kernel, dim3(head_blocks(m)), dim3(kBlock), 0,
-                       as_stream(stream), m, (int)hd, h_pi, h_vf, w_act, b_act, w_val, b_val,
+                       as_stream(stream), m, (int)hd, preact, h_pi, h_vf, w_act, b_act, w_val, b_val,
                        reinterpret_cast<float4 *>(mean), value);
     return check_launch("dr_policy_heads");
 }
@@ -1233,7 +1248,8 @@ size_t dr_ppo_head_workspace_bytes(int64_t m, int64_t hd) {
            align_up(sizeof(float) * (size_t)(kHeadGroups * P));
 }
 
-int dr_ppo_head_loss_backward(int64_t m, int64_t hd, const float *h_pi, const float *h_vf,
+int dr_ppo_head_loss_backward(int64_t m, int64_t hd, int preact, const float *h_pi,
+                              const float *h_vf,
                               const float *w_act, const float *b_act, const float *w_val,
                               const float *b_val, const float *log_std, const float *actions,
                               const float *aux, const int32_t *rows, float clip_range,
@@ -1267,7 +1283,7 @@ int dr_ppo_head_loss_backward(int64_t m, int64_t hd, const float *h_pi, const fl
     }
     const int nb = head_blocks(m);
     const int P = kHeadFixed + 7 * (int)hd;
-    HeadArgs a{m, (int)hd, h_pi, h_vf, w_act, b_act, w_val, b_val, log_std,
+    HeadArgs a{m, (int)hd, preact, h_pi, h_vf, w_act, b_act, w_val, b_val, log_std,
                reinterpret_cast<const float4 *>(actions), aux, rows, clip_range, ent_coef,
                vf_coef, norm, adv_part, anb, gz_pi, gz_vf, part, P};
     hipLaunchKernelGGL(ppo_head_kernel, dim3(nb), dim3(kBlock), sizeof(float) * 4 * P, st, a);

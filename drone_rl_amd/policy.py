@@ -281,14 +281,15 @@ class FusedTrainStep:
         self._alloc_fused()
         pol, M = self.pol, (obs.shape[0] if rows is None else rows.numel())
         depth, top = len(pol.net_arch), len(pol.net_arch) - 1
-        hs = hidden_forward(pol, obs, self._acts, self._acts2, rows)
+        preact = depth >= 2                   # top tanh applied inside the head kernel
+        hs = hidden_forward(pol, obs, self._acts, self._acts2, rows, top_preact=preact)
         gz = self._gz2[top]
         stats = head(hs["pi"][top], hs["vf"][top], pol.p("action.w"), pol.p("action.b"),
                      pol.p("value.w"), pol.p("value.b"), pol.log_std, actions, aux,
                      gz[0], gz[1], self.gview("action.w"),
                      self.gview("action.b"), self.gview("value.w"), self.gview("value.b"),
                      self.gview(f"pi{top}.b"), self.gview(f"vf{top}.b"),
-                     self.gview("log_std"), rows)
+                     self.gview("log_std"), rows, preact=preact)
         if depth == 1:                        # the head kernel gave grad_z of layer 0
             if rows is not None:
                 obs = obs.index_select(0, rows.long())
@@ -379,11 +380,13 @@ def fusable(pol: ActorCritic) -> bool:
 
 
 @torch.no_grad()
-def hidden_forward(pol: ActorCritic, obs, acts, acts2=None, rows=None):
+def hidden_forward(pol: ActorCritic, obs, acts, acts2=None, rows=None, top_preact=False):
     """Hidden activations of the pi and vf MLPs into preallocated buffers
     acts[pre][k] (M, net_arch[k]); with acts2 (the (2, M, n) buffers that
     acts views) each layer's tanh runs once over both MLPs; with rows the
-    input rows are obs[rows]."""
+    input rows are obs[rows].  With top_preact (and depth >= 2) the top
+    layer is left as pre-activations z: its only consumer, the head kernel,
+    applies tanh on load, so the (M, n) tanh pass is skipped."""
     from . import ppo_kernels as K
     for j, pre in enumerate(("pi", "vf")):
         K.linear_tanh(obs, pol.p(f"{pre}0.w"), pol.p(f"{pre}0.b"), acts[pre][0], rows)
@@ -391,6 +394,8 @@ def hidden_forward(pol: ActorCritic, obs, acts, acts2=None, rows=None):
         for pre in ("pi", "vf"):
             torch.addmm(pol.p(f"{pre}{k}.b"), acts[pre][k - 1], pol.p(f"{pre}{k}.w").t(),
                         out=acts[pre][k])
+        if top_preact and k == len(pol.net_arch) - 1:
+            continue
         if acts2 is not None:
             torch.tanh_(acts2[k])
         else:
@@ -417,7 +422,9 @@ class PolicyInference:
     def __call__(self, obs):
         from . import ppo_kernels as K
         pol = self.pol
-        hs = hidden_forward(pol, obs, self.acts, self.acts2)
+        preact = len(pol.net_arch) >= 2
+        hs = hidden_forward(pol, obs, self.acts, self.acts2, top_preact=preact)
         K.policy_heads(hs["pi"][-1], hs["vf"][-1], pol.p("action.w"), pol.p("action.b"),
-                       pol.p("value.w"), pol.p("value.b"), self.mean, self.value)
+                       pol.p("value.w"), pol.p("value.b"), self.mean, self.value,
+                       preact=preact)
         return self.mean, self.value

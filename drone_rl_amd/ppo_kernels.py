@@ -180,10 +180,12 @@ def linear_tanh(x, w, b, out, rows=None):
     return out
 
 
-def policy_heads(h_pi, h_vf, w_act, b_act, w_val, b_val, mean, value):
-    """mean (m,4) = h_pi w_act^T + b_act, value (m) = h_vf w_val^T + b_val."""
+def policy_heads(h_pi, h_vf, w_act, b_act, w_val, b_val, mean, value, preact=False):
+    """mean (m,4) = h_pi w_act^T + b_act, value (m) = h_vf w_val^T + b_val;
+    with preact the inputs are pre-activations and tanh is applied on load."""
     m, hd = h_pi.shape
-    check(_lib.lib().dr_policy_heads(m, hd, ptr(_f32(h_pi)), ptr(_f32(h_vf)), ptr(_f32(w_act)),
+    check(_lib.lib().dr_policy_heads(m, hd, int(bool(preact)), ptr(_f32(h_pi)), ptr(_f32(h_vf)),
+                                     ptr(_f32(w_act)),
                                      ptr(_f32(b_act)), ptr(_f32(w_val)), ptr(_f32(b_val)),
                                      ptr(mean), ptr(value), _s(h_pi)))
     return mean, value
@@ -204,13 +206,14 @@ class HeadLossBackward:
 
     def __call__(self, h_pi, h_vf, w_act, b_act, w_val, b_val, log_std, actions, aux,
                  gz_pi, gz_vf, g_w_act, g_b_act, g_w_val, g_b_val, g_b_pi, g_b_vf, g_log_std,
-                 rows=None):
+                 rows=None, preact=False):
         """actions (.,4) / aux (.,3) rows are read as [rows[r]] when rows
-        (int32, m) is given, else the first m rows."""
+        (int32, m) is given, else the first m rows; with preact h_pi / h_vf
+        are the top layer's pre-activations (tanh applied on load)."""
         assert h_pi.shape == (self.m, self.hd) and aux.shape[1] == 3
         assert rows is not None or aux.shape[0] == self.m
         check(_lib.lib().dr_ppo_head_loss_backward(
-            self.m, self.hd, ptr(_f32(h_pi)), ptr(_f32(h_vf)), ptr(_f32(w_act)),
+            self.m, self.hd, int(bool(preact)), ptr(_f32(h_pi)), ptr(_f32(h_vf)), ptr(_f32(w_act)),
             ptr(_f32(b_act)), ptr(_f32(w_val)), ptr(_f32(b_val)), ptr(_f32(log_std)),
             ptr(_f32(actions)), ptr(_f32(aux)), _rows(rows), float(self.clip), float(self.ent),
             float(self.vf), self.norm, ptr(gz_pi), ptr(gz_vf), ptr(g_w_act), ptr(g_b_act),

@@ -209,6 +209,12 @@ def test_policy_heads_match_torch():
     K.policy_heads(hp, hv, wa, ba, wv, bv, mean, value)
     assert (mean - torch.addmm(ba, hp, wa.t())).abs().max().item() <= 1e-5
     assert (value - torch.addmm(bv, hv, wv.t()).squeeze(1)).abs().max().item() <= 1e-5
+    # pre-activation inputs: the layer's tanh is applied on load
+    z = torch.randn(m, hd, device="cuda") * 2
+    K.policy_heads(z, z, wa, ba, wv, bv, mean, value, preact=True)
+    t = torch.tanh(z)
+    assert (mean - torch.addmm(ba, t, wa.t())).abs().max().item() <= 1e-5
+    assert (value - torch.addmm(bv, t, wv.t()).squeeze(1)).abs().max().item() <= 1e-5
 
 
 @pytest.mark.parametrize("arch,m", [((256, 256), 65536), ((64, 64), 64), ((64, 128), 1000)])
