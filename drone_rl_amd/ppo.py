@@ -55,6 +55,14 @@ class PPOConfig:
     seed: int = 0
     state_dtype: str = "f64"       # env state precision ("f64" = reference)
     variant: str = "gym"
+    # curriculum level every env starts at (drone.py:33 starts at 0.0 and
+    # adds 0.1 per 2000 episodes of an env; with 65k envs per GPU that takes
+    # ~4e9 steps, so large-batch runs of the moving target start higher)
+    initial_eps: float = 0.0
+    # staged curriculum for large batches: ((update, eps), ...) -- at the
+    # start of that PPO iteration every env's eps is set to the value (the
+    # per-env 2000-episode bump of drone.py:68-70 keeps running on top)
+    eps_schedule: tuple = ()
 
     @classmethod
     def sb3_defaults(cls, **kw):
@@ -81,6 +89,8 @@ class PPOTrainer:
         self.env = DroneBatch(N, cfg.variant, device=dev, seed=cfg.seed,
                               env_id_offset=D.env_shard(rank, N)[0], monitor=True,
                               dtype=torch.float64 if cfg.state_dtype == "f64" else torch.float32)
+        if cfg.initial_eps:
+            self.env.set("eps", torch.full((N,), float(cfg.initial_eps), dtype=torch.float64))
         od = self.env.obs_dim
         # every rank starts from the same parameters (the seed is shared);
         # with world > 1 rank 0's copy is also broadcast (sync_params)
@@ -210,6 +220,10 @@ class PPOTrainer:
 
     def learn_step(self):
         """One PPO iteration: rollout + GAE + n_epochs of minibatch updates."""
+        for upd, eps in self.cfg.eps_schedule:
+            if int(upd) == self.num_updates:
+                self.env.set("eps", torch.full((self.cfg.num_envs,), float(eps),
+                                               dtype=torch.float64))
         self.collect_rollouts()
         return self.train()
 

@@ -39,6 +39,10 @@ def main(argv=None):
                     help="SB3 PPO defaults of the reference (n_steps 2048, batch 64, 64x64)")
     ap.add_argument("--checkpoint", default="./dd_gpu.pt")
     ap.add_argument("--log-every", type=int, default=1)
+    ap.add_argument("--initial-eps", type=float, default=0.0,
+                    help="curriculum level every env starts at (reference: 0.0)")
+    ap.add_argument("--eps-schedule", default="",
+                    help="staged curriculum 'update:eps,update:eps,...' (all envs)")
     ap.add_argument("--traj-dir", default=None,
                     help="record env 0's trajectories like traj_tb.py (every 25th episode, "
                          "blocks of 500) into this directory (npz, PNG if matplotlib)")
@@ -55,7 +59,11 @@ def main(argv=None):
     else:
         cfg = PPOConfig(num_envs=a.envs, n_steps=a.n_steps, batch_size=a.batch_size,
                         n_epochs=a.epochs, learning_rate=a.lr, net_arch=tuple(a.net),
-                        seed=a.seed, state_dtype=a.state_dtype, variant=a.variant)
+                        seed=a.seed, state_dtype=a.state_dtype, variant=a.variant,
+                        initial_eps=a.initial_eps,
+                        eps_schedule=tuple((int(u), float(e)) for u, e in
+                                           (kv.split(":") for kv in a.eps_schedule.split(",")
+                                            if kv)))
     tr = PPOTrainer(cfg, rank=rank, world_size=world)
     if a.traj_dir and rank == 0:
         from .trajectory import TrajectoryRecorder
