@@ -89,6 +89,35 @@ __device__ unsigned long long g_stamps[16384 * 8];
 #ifndef DR_HOIST_RESET
 #define DR_HOIST_RESET 0
 #endif
+// 1: per-step outputs and state are written with nontemporal stores.  They
+// stream to HBM while the kernel runs instead of sitting dirty in L2 until
+// the end-of-kernel writeback (4-9 % faster from 65,536 to 4M envs).
+#ifndef DR_NT_STORES
+#define DR_NT_STORES 1
+#endif
+// State loads: nontemporal (NTL) only in the large-batch launch form, where
+// they measured faster; at 131,072 envs they measured 28 % slower.
+template <bool NTL, typename T>
+__device__ inline T ld_in(const T *p) {
+    if constexpr (NTL) return __builtin_nontemporal_load(p);
+    else return *p;
+}
+template <typename T>
+__device__ inline void st_out(T *p, T x) {
+#if DR_NT_STORES
+    __builtin_nontemporal_store(x, p);
+#else
+    *p = x;
+#endif
+}
+__device__ inline void st_out(float4 *p, float4 x) {
+#if DR_NT_STORES
+    typedef float f4v __attribute__((ext_vector_type(4)));
+    __builtin_nontemporal_store(f4v{x.x, x.y, x.z, x.w}, reinterpret_cast<f4v *>(p));
+#else
+    *p = x;
+#endif
+}
 // 1 (A/B builds only): the device library's sincos(double) instead of trig.h
 #ifndef DR_LIB_TRIG
 #define DR_LIB_TRIG 0
@@ -466,7 +495,7 @@ __device__ inline void store_obs_wave(float *sh_block, const float ob[OD],
         const float4 *s4 = reinterpret_cast<const float4 *>(sh);
         float4 *d4 = reinterpret_cast<float4 *>(dst);
 #pragma unroll
-        for (int q = lane; q < RPW * OD / 4; q += 64) d4[q] = s4[q];
+        for (int q = lane; q < RPW * OD / 4; q += 64) st_out(&d4[q], s4[q]);
     } else {
         for (int q = lane; q < (int)nvalid * OD; q += 64) dst[q] = sh[q];
     }
@@ -497,7 +526,7 @@ __device__ inline void store_obs_block(float *sh, const float ob[OD],
 // parameter, not a runtime branch, so the Philox reset path holds no global
 // load: a load there would make the waitcnt pass drain every outstanding
 // store of the wave (vmcnt counts stores too) before the reset could finish.
-template <typename S, int VAR, bool MON, int RPW, bool HU>
+template <typename S, int VAR, bool MON, int RPW, bool HU, bool NTL>
 __global__ __launch_bounds__(kBlock) void env_step_kernel(EnvView<S> v,
                                                           StepIO io) {
     constexpr int OD = VAR == DR_VARIANT_GYM ? 15 : (VAR == DR_VARIANT_MOVING ? 18 : 12);
@@ -517,15 +546,15 @@ __global__ __launch_bounds__(kBlock) void env_step_kernel(EnvView<S> v,
         // sincos range reductions start while pos / vel / target are still
         // in flight (s_waitcnt vmcnt counts oldest-first).
 #pragma unroll
-        for (int k = F_EUL; k < F_EUL + 6; ++k) st[k] = v.field(k)[i];
+        for (int k = F_EUL; k < F_EUL + 6; ++k) st[k] = ld_in<NTL>(&v.field(k)[i]);
         const float4 act = reinterpret_cast<const float4 *>(io.actions)[i];
 #pragma unroll
-        for (int k = 0; k < F_EUL; ++k) st[k] = v.field(k)[i];
+        for (int k = 0; k < F_EUL; ++k) st[k] = ld_in<NTL>(&v.field(k)[i]);
         S cen[3];
         float mp[9], tvel[3];
         if constexpr (VAR == DR_VARIANT_GYM) {
 #pragma unroll
-            for (int k = F_TGT; k < F_N; ++k) st[k] = v.field(k)[i];
+            for (int k = F_TGT; k < F_N; ++k) st[k] = ld_in<NTL>(&v.field(k)[i]);
         } else if constexpr (VAR == DR_VARIANT_MOVING) {
 #pragma unroll
             for (int k = 0; k < 3; ++k) cen[k] = v.field(F_TGT + k)[i];
@@ -536,7 +565,7 @@ __global__ __launch_bounds__(kBlock) void env_step_kernel(EnvView<S> v,
             st[F_TGT + 1] = (S)0;
             st[F_TGT + 2] = (S)10.0;
         }
-        int32_t step = v.step[i];
+        int32_t step = ld_in<NTL>(&v.step[i]);
         // needed only if this env resets; loaded up front so a reset does
         // not stall the wave on a dependent global load (+12 B per step,
         // counted in the measured traffic, not in the 305 B algorithmic)
@@ -578,8 +607,8 @@ __global__ __launch_bounds__(kBlock) void env_step_kernel(EnvView<S> v,
         step += 1;                                         // (155)
         bool done = crash || (step >= v.max_steps);        // (156-157)
         const float rf = (float)r;                         // SB3 f32 buffer
-        io.rew[i] = rf;
-        io.done[i] = (uint8_t)done;
+        st_out(&io.rew[i], rf);
+        st_out(&io.done[i], (uint8_t)done);
         make_obs<S, OD>(st, ob, tvel);
 
         float ret = 0.f;
@@ -624,8 +653,8 @@ __global__ __launch_bounds__(kBlock) void env_step_kernel(EnvView<S> v,
         }
         DR_STAMP(3);
 #pragma unroll
-        for (int k = 0; k < 12; ++k) v.field(k)[i] = st[k];
-        v.step[i] = step;
+        for (int k = 0; k < 12; ++k) st_out(&v.field(k)[i], st[k]);
+        st_out(&v.step[i], step);
         DR_STAMP(4);
     } else {
 #pragma unroll
@@ -1036,9 +1065,9 @@ struct dr_handle {
     int obs_dim = 15;
     bool quad = false;  // true: 4 lanes per env (env_step_quad_kernel)
     // envs per wave of env_step_kernel: 64, or 32 (half-populated waves:
-    // twice the waves in flight; measured faster from 2M envs up, slower
-    // below 1M: scripts/micro/ab_cross.sh)
+    // twice the waves in flight); chosen by batch size in dr_create
     int rpw = 64;
+    bool nt_loads = false;  // nontemporal state loads (large batches)
     void *mem = nullptr;
     const double *host_u = nullptr;
     std::string err;
@@ -1133,20 +1162,33 @@ int launch_step(dr_handle *h, const StepIO &io, hipStream_t st) {
             launched = true;
         }
     }
-    if (!launched && VAR != DR_VARIANT_VECTORIZED && v.host_u) {
-        hipLaunchKernelGGL((env_step_kernel<S, VAR, MON, 64, true>), dim3(grid_for(h->n, 256)),
-                           dim3(kBlock), 0, st, v, io);
+    if (!launched && VAR != DR_VARIANT_VECTORIZED && v.host_u) {   // parity mode
+        if (h->rpw == 32)
+            hipLaunchKernelGGL((env_step_kernel<S, VAR, MON, 32, true, false>),
+                               dim3(grid_for(h->n, 128)), dim3(kBlock), 0, st, v, io);
+        else
+            hipLaunchKernelGGL((env_step_kernel<S, VAR, MON, 64, true, false>),
+                               dim3(grid_for(h->n, 256)), dim3(kBlock), 0, st, v, io);
         launched = true;
     }
     if (!launched) {
-        switch (h->rpw) {
-            case 32:
-                hipLaunchKernelGGL((env_step_kernel<S, VAR, MON, 32, false>),
-                                   dim3(grid_for(h->n, 128)), dim3(kBlock), 0, st, v, io);
+        const dim3 g64(grid_for(h->n, 256)), g32(grid_for(h->n, 128));
+        switch (h->rpw * 2 + (int)h->nt_loads) {
+            case 64:
+                hipLaunchKernelGGL((env_step_kernel<S, VAR, MON, 32, false, false>), g32,
+                                   dim3(kBlock), 0, st, v, io);
+                break;
+            case 65:
+                hipLaunchKernelGGL((env_step_kernel<S, VAR, MON, 32, false, true>), g32,
+                                   dim3(kBlock), 0, st, v, io);
+                break;
+            case 129:
+                hipLaunchKernelGGL((env_step_kernel<S, VAR, MON, 64, false, true>), g64,
+                                   dim3(kBlock), 0, st, v, io);
                 break;
             default:
-                hipLaunchKernelGGL((env_step_kernel<S, VAR, MON, 64, false>),
-                                   dim3(grid_for(h->n, 256)), dim3(kBlock), 0, st, v, io);
+                hipLaunchKernelGGL((env_step_kernel<S, VAR, MON, 64, false, false>), g64,
+                                   dim3(kBlock), 0, st, v, io);
         }
     }
     hipError_t e = hipGetLastError();
@@ -1221,11 +1263,20 @@ int dr_create(const dr_config *cfg_in, dr_handle **out) {
     // slower on MI355X at every measured size, kept for A/B measurement).
     if (const char *kk = std::getenv("DRONERL_STEP_KERNEL"))
         h->quad = std::strcmp(kk, "quad") == 0;
-    h->rpw = cfg.num_envs >= ((int64_t)3 << 19) ? 32 : 64;   // >= 1.5M envs
+    // Launch form by batch size, from the measured sweep
+    // (scripts/micro/ab_sweep.sh, profiles/r01_env_launch_sweep.txt):
+    // [0, 384k) 64 rows/wave; [384k, 1.5M) 32 + nontemporal state loads;
+    // [1.5M, 3M) 32; [3M, ...) 64 + nontemporal state loads.
+    {
+        const int64_t n = cfg.num_envs, k = (int64_t)1 << 10;
+        h->rpw = (n >= 384 * k && n < 3072 * k) ? 32 : 64;
+        h->nt_loads = (n >= 384 * k && n < 1536 * k) || n >= 3072 * k;
+    }
     if (const char *r = std::getenv("DRONERL_ROWS_PER_WAVE")) {
         const int v = std::atoi(r);
         if (v == 32 || v == 64) h->rpw = v;
     }
+    if (const char *r = std::getenv("DRONERL_NT_LOADS")) h->nt_loads = std::atoi(r) != 0;
 
     DeviceGuard g(cfg.device);
     const size_t bytes = state_bytes(h->stride, cfg.state_dtype, cfg.variant);

@@ -30,7 +30,7 @@ def _close(a, b, tol=1e-5):
 @pytest.mark.parametrize("dtype", [torch.float64, torch.float32])
 def test_ragged_sizes_match_oracle(golden, n, dtype, rpw, monkeypatch):
     """Also with half-populated waves (32 envs per wave, the layout chosen
-    from 1.5M envs up), forced here by DRONERL_ROWS_PER_WAVE."""
+    for 384k-3M envs), forced here by DRONERL_ROWS_PER_WAVE."""
     monkeypatch.setenv("DRONERL_ROWS_PER_WAVE", rpw)
     from drone_rl_amd import DroneBatch
     g = golden("gym_step.npz")
@@ -114,14 +114,18 @@ def test_abi_argument_errors():
         b.step(torch.zeros(63, 4, device="cuda"))
 
 
-def test_half_populated_waves_equal_full_waves(monkeypatch):
-    """The 32-envs-per-wave launch computes exactly what the 64 one does,
-    over 60 steps with auto-resets, terminal obs and monitor outputs."""
+@pytest.mark.parametrize("form", [("32", "0"), ("64", "1"), ("32", "1")])
+def test_launch_forms_equal_default_form(form, monkeypatch):
+    """Every launch form (32 envs per wave, nontemporal state loads; chosen
+    by batch size in dr_create) computes exactly what the 64-envs-per-wave
+    plain-load form does, over 60 steps with auto-resets, terminal obs and
+    monitor outputs."""
     from drone_rl_amd import DroneBatch, random_actions
     n = 4099
     out = []
-    for rpw in ("64", "32"):
+    for rpw, ntl in (("64", "0"), form):
         monkeypatch.setenv("DRONERL_ROWS_PER_WAVE", rpw)
+        monkeypatch.setenv("DRONERL_NT_LOADS", ntl)
         b = DroneBatch(n, "gym", seed=21, keep_terminal_obs=True, monitor=True)
         b.reset()
         acc = []
