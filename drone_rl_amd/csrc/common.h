@@ -11,6 +11,17 @@
 
 namespace dr {
 
+// Nontemporal (streaming) stores: written through to memory as the kernel
+// runs instead of staying dirty in L2 until the end-of-kernel writeback.
+template <typename T>
+__device__ inline void store_nt(T *p, T x) {
+    __builtin_nontemporal_store(x, p);
+}
+__device__ inline void store_nt(float4 *p, float4 x) {
+    typedef float f4v __attribute__((ext_vector_type(4)));
+    __builtin_nontemporal_store(f4v{x.x, x.y, x.z, x.w}, reinterpret_cast<f4v *>(p));
+}
+
 // ----------------------------------------------------------------------------
 // Errors: a per-thread message for handle-less calls, a per-handle one else.
 // ----------------------------------------------------------------------------

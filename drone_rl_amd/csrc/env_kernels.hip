@@ -104,19 +104,8 @@ __device__ inline T ld_in(const T *p) {
 }
 template <typename T>
 __device__ inline void st_out(T *p, T x) {
-#if DR_NT_STORES
-    __builtin_nontemporal_store(x, p);
-#else
-    *p = x;
-#endif
-}
-__device__ inline void st_out(float4 *p, float4 x) {
-#if DR_NT_STORES
-    typedef float f4v __attribute__((ext_vector_type(4)));
-    __builtin_nontemporal_store(f4v{x.x, x.y, x.z, x.w}, reinterpret_cast<f4v *>(p));
-#else
-    *p = x;
-#endif
+    if (DR_NT_STORES) store_nt(p, x);
+    else *p = x;
 }
 // 1 (A/B builds only): the device library's sincos(double) instead of trig.h
 #ifndef DR_LIB_TRIG
