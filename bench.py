@@ -169,6 +169,8 @@ def time_ppo(args, rank, world, device):
                        "optimizer_steps_per_update": cfg.n_epochs * cfg.n_steps *
                        cfg.num_envs // cfg.batch_size,
                        "net_arch": list(cfg.net_arch), "mlp_dtype": "fp32",
+                       "gemm": ("hipBLASLt/rocBLAS, MI355X-tuned solutions (TunableOp lookup)"
+                                if tr.tuned_gemms else "hipBLASLt heuristic"),
                        "grad_allreduce": ({"nccl": "rccl"}.get(dist.get_backend(),
                                                                dist.get_backend())
                                           + " (2 buckets, overlapped with the "

@@ -16,10 +16,37 @@ GEMMs run through torch (hipBLASLt -> MFMA, fp32).  The layer order inside
 from __future__ import annotations
 
 import math
+import os
 
 import numpy as np
 import torch
 import torch.nn.functional as F
+
+
+TUNED_GEMMS_CSV = os.path.join(os.path.dirname(os.path.abspath(__file__)), "tuned",
+                               "gemm_gfx950.csv")
+
+
+def use_tuned_gemms(path: str = TUNED_GEMMS_CSV) -> bool:
+    """Load the GEMM solutions measured for this trainer's shapes on MI355X.
+
+    The three fp32 GEMM shapes of a 65,536-row 2x256 minibatch (forward
+    addmm, batched grad-input, batched split-K weight gradient) were timed by
+    PyTorch's TunableOp over every hipBLASLt and rocBLAS solution on the box
+    (scripts/tune_gemm.sh); the winners are committed in `tuned/`.  This
+    turns TunableOp on in lookup-only mode (no tuning at run time; shapes
+    not in the file keep the library heuristic).  The grad-input GEMM goes
+    from 146 to 123 us, the weight gradient from 126 to 122 us.
+    `DRONERL_TUNED_GEMMS=0` opts out; a caller that already enabled TunableOp
+    (PYTORCH_TUNABLEOP_*) keeps its own settings.  Returns whether the file
+    was loaded (False off-GPU or when its validators do not match)."""
+    if os.environ.get("DRONERL_TUNED_GEMMS", "1") == "0" or not torch.cuda.is_available():
+        return False
+    import torch.cuda.tunable as tun
+    if not tun.is_enabled():
+        tun.enable(True)
+        tun.tuning_enable(False)
+    return bool(tun.read_file(path))
 
 
 class _SplitKLinear(torch.autograd.Function):

@@ -33,7 +33,7 @@ import torch
 from . import dist as D
 from . import ppo_kernels as K
 from .env import MOTOR_MAX, DroneBatch
-from .policy import ActorCritic, FusedTrainStep, PolicyInference, fusable
+from .policy import ActorCritic, FusedTrainStep, PolicyInference, fusable, use_tuned_gemms
 
 
 @dataclasses.dataclass
@@ -63,6 +63,8 @@ class PPOConfig:
     # start of that PPO iteration every env's eps is set to the value (the
     # per-env 2000-episode bump of drone.py:68-70 keeps running on top)
     eps_schedule: tuple = ()
+    # look up the MI355X-tuned GEMM solutions (policy.use_tuned_gemms)
+    tuned_gemms: bool = True
 
     @classmethod
     def sb3_defaults(cls, **kw):
@@ -86,6 +88,7 @@ class PPOTrainer:
         if (N * T) % cfg.batch_size:
             raise ValueError("num_envs * n_steps must be a multiple of batch_size")
         dev = self.device
+        self.tuned_gemms = use_tuned_gemms() if cfg.tuned_gemms else False
         self.env = DroneBatch(N, cfg.variant, device=dev, seed=cfg.seed,
                               env_id_offset=D.env_shard(rank, N)[0], monitor=True,
                               dtype=torch.float64 if cfg.state_dtype == "f64" else torch.float32)

@@ -17,7 +17,7 @@ step() {  # name, seconds, command...
   fi
   return 0
 }
-step pytest_gpu 900 python -m pytest tests -m gpu -q
+step pytest_gpu 900 python -u -m pytest tests -m gpu -q --timeout 300 --timeout-method thread
 step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
 step bench 600 python bench.py
 grep '^{' $OUT/bench.log > $OUT/bench.json || true

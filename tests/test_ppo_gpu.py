@@ -121,3 +121,42 @@ def test_sb3_zip_roundtrip_on_gpu(tmp_path):
     assert torch.isfinite(b.learn_step()).all()
     a.close()
     b.close()
+
+
+def test_tuned_gemms_load_and_are_deterministic():
+    """The committed TunableOp solutions (policy.use_tuned_gemms) load on the
+    box, give a bitwise-reproducible minibatch gradient at the bench shape
+    (65,536 rows, 2x256) and agree with the library-heuristic GEMMs to fp32
+    reassociation error."""
+    import torch.cuda.tunable as tun
+
+    from drone_rl_amd.ppo import PPOConfig, PPOTrainer
+
+    cfg = PPOConfig(num_envs=65536, n_steps=2, batch_size=65536, n_epochs=1, seed=3)
+    tr = PPOTrainer(cfg)
+    assert tr.tuned_gemms and tun.is_enabled(), "tuned GEMM table not loaded"
+    tr.collect_rollouts()
+    M = cfg.batch_size
+    obs = tr.obs[:1].reshape(M, -1)
+    act = tr.actions[:1].reshape(M, 4)
+    aux = tr.aux[:M]
+
+    def grad():
+        g, st = tr.fused.step(obs, act, aux, tr.head)
+        torch.cuda.synchronize()
+        return g.clone(), st.clone()
+
+    g1, s1 = grad()
+    keys = " ".join(str(r) for r in tun.get_results())
+    assert "nt_256_256_1024_B_128" in keys and "nn_256_65536_256_B_2" in keys
+    g2, s2 = grad()
+    assert torch.equal(g1, g2) and torch.equal(s1, s2)
+    tun.enable(False)
+    try:
+        g3, s3 = grad()
+    finally:
+        tun.enable(True)
+    scale = g3.abs().max().item()
+    assert (g1 - g3).abs().max().item() <= 1e-4 * scale
+    np.testing.assert_allclose(s1.cpu(), s3.cpu(), rtol=1e-4, atol=1e-6)
+    tr.close()
