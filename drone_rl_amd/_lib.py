@@ -23,7 +23,7 @@ DR_ERR_HIP = -2
 DR_ERR_NOMEM = -3
 DR_ERR_UNSUPPORTED = -4
 
-ABI_VERSION = 4                 # DR_ABI_VERSION in include/dronerl.h
+ABI_VERSION = 5                 # DR_ABI_VERSION in include/dronerl.h
 DR_VARIANT_GYM = 0
 DR_VARIANT_VECTORIZED = 1
 DR_VARIANT_MOVING = 2
@@ -80,6 +80,11 @@ SIGNATURES = {
     "dr_permutation_workspace_bytes": (c_size_t, [c_int64]),
     "dr_permutation": (c_int, [c_int64, c_uint64, c_uint64, _P, _P, c_size_t, _P]),
     "dr_gather_rows": (c_int, [c_int64, c_int64, _P, _P, _P, _P]),
+    "dr_gather_minibatch": (c_int, [c_int64, _P, c_int64] + [_P] * 8),
+    "dr_linear_tanh2": (c_int, [c_int64, c_int64, c_int64] + [_P] * 9),
+    "dr_first_layer_backward2_workspace_bytes": (c_size_t, [c_int64, c_int64, c_int64]),
+    "dr_first_layer_backward2": (c_int, [c_int64, c_int64, c_int64] + [_P] * 11 +
+                                 [c_size_t, _P]),
     "dr_tanh_backward_workspace_bytes": (c_size_t, [c_int64, c_int64]),
     "dr_tanh_backward": (c_int, [c_int64, c_int64, _P, _P, _P, _P, _P, c_size_t, _P]),
     "dr_linear_tanh": (c_int, [c_int64, c_int64, c_int64, _P, _P, _P, _P, _P, _P]),

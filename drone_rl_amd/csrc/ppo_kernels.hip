@@ -251,6 +251,61 @@ __global__ __launch_bounds__(kBlock) void adv_stats_kernel(
     }
 }
 
+// One PPO.train minibatch formed in one launch (RolloutBuffer.get's
+// indexing of obs, actions and the (old_logp, advantage, return) rows):
+//   blocks [0, nb_obs)            obs elements, one thread per element;
+//   blocks [nb_obs, +nb_rows)     action rows, one float4 per thread;
+//   blocks [.., +nb_rows)         aux rows, one row per thread, plus the
+//                                 advantage (count, mean, M2) partial of the
+//                                 block's 256 rows -- the same rows, values
+//                                 and reduction order as adv_stats_kernel, so
+//                                 the partials are bitwise the same.
+__global__ __launch_bounds__(kBlock) void gather_minibatch_kernel(
+    int64_t m, int obs_dim, int nb_obs, int nb_rows, const int32_t *__restrict__ idx,
+    const float *__restrict__ obs, const float4 *__restrict__ act,
+    const float *__restrict__ aux, float *__restrict__ obs_out, float4 *__restrict__ act_out,
+    float *__restrict__ aux_out, float *__restrict__ adv_part) {
+    __shared__ float sh[8];
+    int b = blockIdx.x;
+    if (b < nb_obs) {
+        const int64_t e = (int64_t)b * kBlock + threadIdx.x;
+        if (e >= m * obs_dim) return;
+        const int64_t k = e / obs_dim, j = e - k * obs_dim;
+        obs_out[e] = obs[(int64_t)idx[k] * obs_dim + j];
+        return;
+    }
+    b -= nb_obs;
+    if (b < nb_rows) {
+        const int64_t i = (int64_t)b * kBlock + threadIdx.x;
+        if (i < m) act_out[i] = act[idx[i]];
+        return;
+    }
+    b -= nb_rows;
+    const int64_t i = (int64_t)b * kBlock + threadIdx.x;
+    const int64_t cnt = min((int64_t)kBlock, m - (int64_t)b * kBlock);
+    float ai = 0.f;
+    if (i < m) {
+        const int64_t r = idx[i];
+        const float l = aux[3 * r], a = aux[3 * r + 1], ret = aux[3 * r + 2];
+        aux_out[3 * i] = l;
+        aux_out[3 * i + 1] = a;
+        aux_out[3 * i + 2] = ret;
+        ai = a;
+    }
+    if (!adv_part) return;
+    float x[1] = {ai};
+    block_sum<1>(x, sh);
+    const float mean = x[0] / (float)cnt;
+    float d = i < m ? ai - mean : 0.f;
+    float y[1] = {d * d};
+    block_sum<1>(y, sh);
+    if (threadIdx.x == 0) {
+        adv_part[3 * b + 0] = (float)cnt;
+        adv_part[3 * b + 1] = mean;
+        adv_part[3 * b + 2] = y[0];
+    }
+}
+
 // Chan et al. merge of (n, mean, M2) b into a.
 __device__ inline void chan_merge(double &n, double &mu, double &M2, double nb_, double mb,
                                   double m2b) {
@@ -520,13 +575,22 @@ __device__ inline float dot4(float4 a, float4 b) {
 // h = tanh(x W^T + b) for a narrow input (the first layer: K = obs_dim),
 // x (m,K), W (n,K), b (n), h (m,n), n % 4 == 0, n <= 256.  Memory-bound on
 // the h write; replaces an addmm + a separate tanh pass over h.
+// With gridDim.y == 2 the launch covers both MLPs (pi: blockIdx.y 0, vf: 1),
+// which share the input rows: one launch and one tail instead of two.
+struct LayerPair {
+    const float *w[2];
+    const float *b[2];
+    float *h[2];
+};
+
 template <int K>
 __global__ __launch_bounds__(kBlock) void linear_tanh_kernel(int64_t m, int n,
                                                              const float *__restrict__ x,
                                                              const int32_t *__restrict__ rows,
-                                                             const float *__restrict__ w,
-                                                             const float *__restrict__ b,
-                                                             float *__restrict__ h) {
+                                                             LayerPair lp) {
+    const float *__restrict__ w = lp.w[blockIdx.y];
+    const float *__restrict__ b = lp.b[blockIdx.y];
+    float *__restrict__ h = lp.h[blockIdx.y];
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     const int c0 = 4 * lane;
     const bool act = c0 < n;
@@ -793,14 +857,23 @@ __global__ __launch_bounds__(kBlock) void ppo_head_kernel(HeadArgs a) {
 // Partial layout per block (P = (K+1) n): [k*n + c] = dW[c][k], [K*n + c] = db[c].
 constexpr int kFirstTile = 8;
 
+// With gridDim.y == 2 the launch covers both MLPs (blockIdx.y = net); block
+// b of net j writes partial row b * gridDim.y + j, so one column-sum pass
+// over (gridDim.y * P)-wide rows reduces both nets.
+struct FirstBwdIn {
+    const float *gh[2];
+    const float *h[2];
+};
+
 template <int K>
 __global__ __launch_bounds__(kBlock) void first_layer_bwd_kernel(int64_t m, int n,
-                                                                 const float *__restrict__ gh,
-                                                                 const float *__restrict__ h,
+                                                                 FirstBwdIn in,
                                                                  const float *__restrict__ x,
                                                                  const int32_t *__restrict__ rows,
                                                                  float *__restrict__ part) {
     extern __shared__ float sh_fl[];  // 4 * P
+    const float *__restrict__ gh = in.gh[blockIdx.y];
+    const float *__restrict__ h = in.h[blockIdx.y];
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     const int c0 = 4 * lane;
     const bool act = c0 < n;
@@ -854,27 +927,37 @@ __global__ __launch_bounds__(kBlock) void first_layer_bwd_kernel(int64_t m, int 
         }
     }
     __syncthreads();
+    float *__restrict__ out = part + ((int64_t)blockIdx.x * gridDim.y + blockIdx.y) * P;
     for (int p = threadIdx.x; p < P; p += kBlock)
-        part[(int64_t)blockIdx.x * P + p] =
-            ((sh_fl[p] + sh_fl[P + p]) + sh_fl[2 * P + p]) + sh_fl[3 * P + p];
+        out[p] = ((sh_fl[p] + sh_fl[P + p]) + sh_fl[2 * P + p]) + sh_fl[3 * P + p];
 }
 
-// Sum of the grouped partials (ng rows) scattered to d W (n,K) row-major and
-// d b (n).
+// Sum of the grouped partials (ng rows of nets * P) scattered to d W (n,K)
+// row-major and d b (n) of each net.
+struct FirstBwdOut {
+    float *gw[2];
+    float *gb[2];
+};
+
 __global__ __launch_bounds__(kBlock) void first_layer_finish_kernel(int ng, int n, int K,
+                                                                    int nets,
                                                                     const float *__restrict__ part,
-                                                                    float *__restrict__ gw,
-                                                                    float *__restrict__ gb) {
-    const int P = (K + 1) * n;
-    const int p = blockIdx.x * kBlock + threadIdx.x;
-    if (p >= P) return;
+                                                                    FirstBwdOut o) {
+    const int P1 = (K + 1) * n;
+    const int P = nets * P1;
+    const int pp = blockIdx.x * kBlock + threadIdx.x;
+    if (pp >= P) return;
+    const int net = pp >= P1 ? 1 : 0;
+    const int p = pp - net * P1;
+    float *__restrict__ gw = o.gw[net];
+    float *__restrict__ gb = o.gb[net];
     float s0 = 0.f, s1 = 0.f;
     int g = 0;
     for (; g + 1 < ng; g += 2) {
-        s0 += part[(int64_t)g * P + p];
-        s1 += part[(int64_t)(g + 1) * P + p];
+        s0 += part[(int64_t)g * P + pp];
+        s1 += part[(int64_t)(g + 1) * P + pp];
     }
-    if (g < ng) s0 += part[(int64_t)g * P + p];
+    if (g < ng) s0 += part[(int64_t)g * P + pp];
     const float s = s0 + s1;
     const int k = p / n, c = p - k * n;
     if (k < K) gw[c * K + k] = s;
@@ -1106,6 +1189,25 @@ int dr_gather_rows(int64_t m, int64_t width, const int32_t *idx, const float *sr
     return check_launch("dr_gather_rows");
 }
 
+int dr_gather_minibatch(int64_t m, const int32_t *idx, int64_t obs_dim, const float *obs,
+                        const float *actions, const float *aux, float *obs_out,
+                        float *actions_out, float *aux_out, float *adv_part, void *stream) {
+    if (m < 0 || obs_dim < 1 || !idx || !obs || !actions || !aux || !obs_out || !actions_out ||
+        !aux_out)
+        return fail0(DR_ERR_INVALID, "dr_gather_minibatch: bad arguments");
+    if ((((uintptr_t)actions) | ((uintptr_t)actions_out)) & 15)
+        return fail0(DR_ERR_INVALID, "dr_gather_minibatch: action rows must be 16-byte aligned");
+    if (m == 0) return DR_OK;
+    const int64_t nb_obs = grid_for(m * obs_dim), nb_rows = grid_for(m);
+    if (nb_obs + 2 * nb_rows > INT32_MAX)
+        return fail0(DR_ERR_INVALID, "dr_gather_minibatch: m too large");
+    hipLaunchKernelGGL(gather_minibatch_kernel, dim3((unsigned)(nb_obs + 2 * nb_rows)),
+                       dim3(kBlock), 0, as_stream(stream), m, (int)obs_dim, (int)nb_obs,
+                       (int)nb_rows, idx, obs, reinterpret_cast<const float4 *>(actions), aux,
+                       obs_out, reinterpret_cast<float4 *>(actions_out), aux_out, adv_part);
+    return check_launch("dr_gather_minibatch");
+}
+
 size_t dr_tanh_backward_workspace_bytes(int64_t m, int64_t n) {
     const int64_t nb = (m + kTanhRows - 1) / kTanhRows;
     return align_up(sizeof(float) * (size_t)(nb * n));
@@ -1210,29 +1312,48 @@ int dr_clip_adam(int64_t n, float *params, float *grads, float *exp_avg, float *
 }
 
 
-int dr_linear_tanh(int64_t m, int64_t k, int64_t n, const float *x, const int32_t *rows,
-                   const float *w, const float *b, float *h, void *stream) {
-    if (m < 1 || !x || !w || !b || !h || n < 4 || n > 256 || (n & 3))
-        return fail0(DR_ERR_INVALID, "dr_linear_tanh: bad arguments (need 4 <= n <= 256, n % 4 == 0)");
-    if ((((uintptr_t)h) | ((uintptr_t)w)) & 15)
-        return fail0(DR_ERR_INVALID, "dr_linear_tanh: h and w must be 16-byte aligned");
+static int launch_linear_tanh(const char *who, int nets, int64_t m, int64_t k, int64_t n,
+                              const float *x, const int32_t *rows, const LayerPair &lp,
+                              void *stream) {
+    if (m < 1 || !x || n < 4 || n > 256 || (n & 3))
+        return fail0(DR_ERR_INVALID, std::string(who) +
+                                         ": bad arguments (need 4 <= n <= 256, n % 4 == 0)");
+    for (int j = 0; j < nets; ++j) {
+        if (!lp.w[j] || !lp.b[j] || !lp.h[j])
+            return fail0(DR_ERR_INVALID, std::string(who) + ": null weight / bias / output");
+        if ((((uintptr_t)lp.h[j]) | ((uintptr_t)lp.w[j])) & 15)
+            return fail0(DR_ERR_INVALID, std::string(who) + ": h and w must be 16-byte aligned");
+    }
     const int64_t nbl = (m + 63) / 64;    // >= 16 rows per wave
     const int nb = (int)(nbl < 1024 ? nbl : 1024);
     hipStream_t st = as_stream(stream);
     switch (k) {
 #define DR_LT_CASE(K)                                                                      \
     case K:                                                                                \
-        hipLaunchKernelGGL(linear_tanh_kernel<K>, dim3(nb), dim3(kBlock), 0, st, m, (int)n, \
-                           x, rows, w, b, h);                                              \
+        hipLaunchKernelGGL(linear_tanh_kernel<K>, dim3(nb, nets), dim3(kBlock), 0, st, m,   \
+                           (int)n, x, rows, lp);                                           \
         break;
         DR_LT_CASE(4) DR_LT_CASE(8) DR_LT_CASE(12) DR_LT_CASE(15) DR_LT_CASE(16)
         DR_LT_CASE(18) DR_LT_CASE(24) DR_LT_CASE(32)
 #undef DR_LT_CASE
         default:
             return fail0(DR_ERR_UNSUPPORTED,
-                         "dr_linear_tanh: k must be one of 4, 8, 12, 15, 16, 18, 24, 32");
+                         std::string(who) + ": k must be one of 4, 8, 12, 15, 16, 18, 24, 32");
     }
-    return check_launch("dr_linear_tanh");
+    return check_launch(who);
+}
+
+int dr_linear_tanh(int64_t m, int64_t k, int64_t n, const float *x, const int32_t *rows,
+                   const float *w, const float *b, float *h, void *stream) {
+    const LayerPair lp{{w, nullptr}, {b, nullptr}, {h, nullptr}};
+    return launch_linear_tanh("dr_linear_tanh", 1, m, k, n, x, rows, lp, stream);
+}
+
+int dr_linear_tanh2(int64_t m, int64_t k, int64_t n, const float *x, const int32_t *rows,
+                    const float *w0, const float *b0, float *h0, const float *w1,
+                    const float *b1, float *h1, void *stream) {
+    const LayerPair lp{{w0, w1}, {b0, b1}, {h0, h1}};
+    return launch_linear_tanh("dr_linear_tanh2", 2, m, k, n, x, rows, lp, stream);
 }
 
 int dr_policy_heads(int64_t m, int64_t hd, int preact, const float *h_pi, const float *h_vf,
@@ -1285,7 +1406,9 @@ int dr_ppo_head_loss_backward(int64_t m, int64_t hd, int preact, const float *h_
     float *part = reinterpret_cast<float *>(static_cast<char *>(workspace) +
                                             align_up(sizeof(float) * 3 * anb));
     hipStream_t st = as_stream(stream);
-    if (norm) {
+    // normalize_advantage == 2: dr_gather_minibatch already wrote the
+    // advantage partials to the head of the workspace
+    if (norm && normalize_advantage != 2) {
         hipLaunchKernelGGL(adv_stats_kernel, dim3(anb), dim3(kBlock), 0, st, m, aux + 1,
                            (int64_t)3, rows, adv_part);
         int rc = check_launch("dr_ppo_head_loss_backward stats");
@@ -1321,56 +1444,91 @@ static int first_blocks(int64_t m) {
     return (int)(b < 512 ? b : 512);
 }
 
-size_t dr_first_layer_backward_workspace_bytes(int64_t m, int64_t k, int64_t n) {
-    const int64_t P = (k + 1) * n;
+static size_t first_ws_bytes(int nets, int64_t m, int64_t k, int64_t n) {
+    const int64_t P = nets * (k + 1) * n;
     return align_up(sizeof(float) * (size_t)(first_blocks(m > 0 ? m : 1) * P)) +
            align_up(sizeof(float) * (size_t)(kHeadGroups * P));
 }
 
-int dr_first_layer_backward(int64_t m, int64_t k, int64_t n, const float *grad_h,
-                            const float *h, const float *x, const int32_t *rows, float *grad_w,
-                            float *grad_b, void *workspace, size_t workspace_bytes,
+size_t dr_first_layer_backward_workspace_bytes(int64_t m, int64_t k, int64_t n) {
+    return first_ws_bytes(1, m, k, n);
+}
+
+size_t dr_first_layer_backward2_workspace_bytes(int64_t m, int64_t k, int64_t n) {
+    return first_ws_bytes(2, m, k, n);
+}
+
+static int launch_first_bwd(const char *who, int nets, int64_t m, int64_t k, int64_t n,
+                            const FirstBwdIn &in, const float *x, const int32_t *rows,
+                            const FirstBwdOut &o, void *workspace, size_t workspace_bytes,
                             void *stream) {
-    if (m < 1 || !grad_h || !h || !x || !grad_w || !grad_b || n < 4 || n > 256 || (n & 3))
-        return fail0(DR_ERR_INVALID, "dr_first_layer_backward: bad arguments");
-    if ((((uintptr_t)grad_h) | ((uintptr_t)h)) & 15)
-        return fail0(DR_ERR_INVALID, "dr_first_layer_backward: grad_h / h must be 16-byte aligned");
-    if (!workspace || workspace_bytes < dr_first_layer_backward_workspace_bytes(m, k, n))
-        return fail0(DR_ERR_INVALID, "dr_first_layer_backward: workspace too small");
+    if (m < 1 || !x || n < 4 || n > 256 || (n & 3))
+        return fail0(DR_ERR_INVALID, std::string(who) + ": bad arguments");
+    for (int j = 0; j < nets; ++j) {
+        if (!in.gh[j] || !in.h[j] || !o.gw[j] || !o.gb[j])
+            return fail0(DR_ERR_INVALID, std::string(who) + ": bad arguments");
+        if ((((uintptr_t)in.gh[j]) | ((uintptr_t)in.h[j])) & 15)
+            return fail0(DR_ERR_INVALID,
+                         std::string(who) + ": grad_h / h must be 16-byte aligned");
+    }
+    if (!workspace || workspace_bytes < first_ws_bytes(nets, m, k, n))
+        return fail0(DR_ERR_INVALID, std::string(who) + ": workspace too small");
     const int nb = first_blocks(m);
-    const int P = (int)((k + 1) * n);
+    const int P1 = (int)((k + 1) * n);
+    const int P = nets * P1;
     float *part = static_cast<float *>(workspace);
     float *part2 = reinterpret_cast<float *>(static_cast<char *>(workspace) +
                                              align_up(sizeof(float) * (size_t)(nb * P)));
     hipStream_t st = as_stream(stream);
-    const size_t lds = sizeof(float) * 4 * P;
+    const size_t lds = sizeof(float) * 4 * P1;
     switch (k) {
 #define DR_FL_CASE(K)                                                                      \
     case K:                                                                                \
         if (lds > 65536)                                                                   \
             (void)hipFuncSetAttribute(reinterpret_cast<const void *>(first_layer_bwd_kernel<K>), \
                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds); \
-        hipLaunchKernelGGL(first_layer_bwd_kernel<K>, dim3(nb), dim3(kBlock), lds, st, m,   \
-                           (int)n, grad_h, h, x, rows, part);                              \
+        hipLaunchKernelGGL(first_layer_bwd_kernel<K>, dim3(nb, nets), dim3(kBlock), lds, st, \
+                           m, (int)n, in, x, rows, part);                                  \
         break;
         DR_FL_CASE(4) DR_FL_CASE(8) DR_FL_CASE(12) DR_FL_CASE(15) DR_FL_CASE(16)
         DR_FL_CASE(18) DR_FL_CASE(24) DR_FL_CASE(32)
 #undef DR_FL_CASE
         default:
             return fail0(DR_ERR_UNSUPPORTED,
-                         "dr_first_layer_backward: k must be one of 4, 8, 12, 15, 16, 18, 24, 32");
+                         std::string(who) + ": k must be one of 4, 8, 12, 15, 16, 18, 24, 32");
     }
-    int rc = check_launch("dr_first_layer_backward");
+    int rc = check_launch(who);
     if (rc) return rc;
     const int gsize = (nb + kHeadGroups - 1) / kHeadGroups;
     const int ng = (nb + gsize - 1) / gsize;
     hipLaunchKernelGGL(colsum_groups_kernel, dim3((P + kBlock - 1) / kBlock, ng), dim3(kBlock),
                        0, st, nb, P, gsize, part, part2);
-    rc = check_launch("dr_first_layer_backward groups");
+    rc = check_launch(who);
     if (rc) return rc;
     hipLaunchKernelGGL(first_layer_finish_kernel, dim3((P + kBlock - 1) / kBlock), dim3(kBlock),
-                       0, st, ng, (int)n, (int)k, part2, grad_w, grad_b);
-    return check_launch("dr_first_layer_backward finish");
+                       0, st, ng, (int)n, (int)k, nets, part2, o);
+    return check_launch(who);
+}
+
+int dr_first_layer_backward(int64_t m, int64_t k, int64_t n, const float *grad_h,
+                            const float *h, const float *x, const int32_t *rows, float *grad_w,
+                            float *grad_b, void *workspace, size_t workspace_bytes,
+                            void *stream) {
+    const FirstBwdIn in{{grad_h, nullptr}, {h, nullptr}};
+    const FirstBwdOut o{{grad_w, nullptr}, {grad_b, nullptr}};
+    return launch_first_bwd("dr_first_layer_backward", 1, m, k, n, in, x, rows, o, workspace,
+                            workspace_bytes, stream);
+}
+
+int dr_first_layer_backward2(int64_t m, int64_t k, int64_t n, const float *x,
+                             const int32_t *rows, const float *grad_h0, const float *h0,
+                             float *grad_w0, float *grad_b0, const float *grad_h1,
+                             const float *h1, float *grad_w1, float *grad_b1, void *workspace,
+                             size_t workspace_bytes, void *stream) {
+    const FirstBwdIn in{{grad_h0, grad_h1}, {h0, h1}};
+    const FirstBwdOut o{{grad_w0, grad_w1}, {grad_b0, grad_b1}};
+    return launch_first_bwd("dr_first_layer_backward2", 2, m, k, n, in, x, rows, o, workspace,
+                            workspace_bytes, stream);
 }
 
 }  // extern "C"

@@ -265,7 +265,7 @@ class FusedTrainStep:
         self._gz2 = [torch.empty(2, M, n, **f32) for n in pol.net_arch]
         self._g2 = torch.empty(2, M, max(pol.net_arch), **f32)
         self._ws2 = torch.empty(2 * self.C * max(pol.net_arch) ** 2, **f32) if self.C > 1 else None
-        self._first = self.K.FirstLayerBackward(M, pol.obs_dim, pol.net_arch[0], pol.device)
+        self._first = self.K.FirstLayerBackward2(M, pol.obs_dim, pol.net_arch[0], pol.device)
 
     def first_layer_end(self) -> int:
         """Flat offset where the first layer's parameters end (they come
@@ -288,7 +288,8 @@ class FusedTrainStep:
         torch.sum(ws.view(2, C, N, Kd), dim=1, out=out)
 
     @torch.no_grad()
-    def step(self, obs, actions, aux, head, rows=None, on_ready=None):
+    def step(self, obs, actions, aux, head, rows=None, on_ready=None, adv_ready=False,
+             stats_out=None):
         """One PPO.train minibatch on the fused path: hidden forward
         (dr_linear_tanh for the first layer, hipBLASLt addmm + tanh above),
         dr_ppo_head_loss_backward (heads, loss, backward through the heads
@@ -304,6 +305,7 @@ class FusedTrainStep:
         every parameter except the first layer's -- is final on the current
         stream, so a data-parallel caller can start that bucket's
         all-reduce while the first-layer backward still runs.
+        `adv_ready` / `stats_out` are passed to the head (HeadLossBackward).
         Returns (flat grad, stats (8))."""
         self._alloc_fused()
         pol, M = self.pol, (obs.shape[0] if rows is None else rows.numel())
@@ -316,7 +318,8 @@ class FusedTrainStep:
                      gz[0], gz[1], self.gview("action.w"),
                      self.gview("action.b"), self.gview("value.w"), self.gview("value.b"),
                      self.gview(f"pi{top}.b"), self.gview(f"vf{top}.b"),
-                     self.gview("log_std"), rows, preact=preact)
+                     self.gview("log_std"), rows, preact=preact, adv_ready=adv_ready,
+                     stats_out=stats_out)
         if depth == 1:                        # the head kernel gave grad_z of layer 0
             if rows is not None:
                 obs = obs.index_select(0, rows.long())
@@ -333,10 +336,10 @@ class FusedTrainStep:
             g = self._g2.view(-1)[:2 * M * n_in].view(2, M, n_in)
             torch.bmm(gz, pol.p2(k, "w"), out=g)
             if k == 1:
-                # first layer: tanh backward + weight/bias gradients fused
-                for j, pre in enumerate(("pi", "vf")):
-                    self._first(g[j], x[j], obs, self.gview(f"{pre}0.w"),
-                                self.gview(f"{pre}0.b"), rows)
+                # first layer of both MLPs: tanh backward + weight/bias
+                # gradients fused, one launch
+                self._first(obs, g[0], x[0], self.gview("pi0.w"), self.gview("pi0.b"),
+                            g[1], x[1], self.gview("vf0.w"), self.gview("vf0.b"), rows)
             else:
                 gz = self._gz2[k - 1]
                 for j, pre in enumerate(("pi", "vf")):
@@ -415,8 +418,8 @@ def hidden_forward(pol: ActorCritic, obs, acts, acts2=None, rows=None, top_preac
     layer is left as pre-activations z: its only consumer, the head kernel,
     applies tanh on load, so the (M, n) tanh pass is skipped."""
     from . import ppo_kernels as K
-    for j, pre in enumerate(("pi", "vf")):
-        K.linear_tanh(obs, pol.p(f"{pre}0.w"), pol.p(f"{pre}0.b"), acts[pre][0], rows)
+    K.linear_tanh2(obs, pol.p("pi0.w"), pol.p("pi0.b"), acts["pi"][0],
+                   pol.p("vf0.w"), pol.p("vf0.b"), acts["vf"][0], rows)
     for k in range(1, len(pol.net_arch)):
         for pre in ("pi", "vf"):
             torch.addmm(pol.p(f"{pre}{k}.b"), acts[pre][k - 1], pol.p(f"{pre}{k}.w").t(),

@@ -195,28 +195,34 @@ class PPOTrainer:
                 # gathered copies: the consumers then stream rows in order
                 # (reading through `rows=idx` in the kernels measured 3 %
                 # slower: 60-B random rows waste most of each cache line)
-                K.gather_rows(idx, obs_flat, out=self.mb_obs)
-                K.gather_rows(idx, act_flat, out=self.mb_act)
-                K.gather_rows(idx, self.aux, out=self.mb_aux)
                 if self.use_fused:
+                    # one launch gathers obs, actions and aux rows and the
+                    # advantage partials the head's normalisation needs
+                    K.gather_minibatch(idx, obs_flat, act_flat, self.aux, self.mb_obs,
+                                       self.mb_act, self.mb_aux, adv_part=self.head.adv_part)
+                    kw = dict(adv_ready=True, stats_out=stats[j])
                     if self.world > 1:
                         # DP: the gradient all-reduce starts while the
                         # first-layer backward is still running
                         bar = D.BucketedAllReduce(self.fused.grad, self.world, self.pg)
                         grad, st = self.fused.step(self.mb_obs, self.mb_act, self.mb_aux,
-                                                   self.head, on_ready=bar.start)
+                                                   self.head, on_ready=bar.start, **kw)
                         bar.finish()
                     else:
                         grad, st = self.fused.step(self.mb_obs, self.mb_act, self.mb_aux,
-                                                   self.head)
+                                                   self.head, **kw)
                 else:
+                    K.gather_rows(idx, obs_flat, out=self.mb_obs)
+                    K.gather_rows(idx, act_flat, out=self.mb_act)
+                    K.gather_rows(idx, self.aux, out=self.mb_aux)
                     mean, value, cache = self.fused.forward(self.mb_obs)
                     g_mean, g_ls, g_v, st = self.loss(mean, log_std, value, self.mb_act,
                                                       aux=self.mb_aux)
                     grad = self.fused.backward(self.mb_obs, cache, g_mean, g_v, g_ls)
                     self._allreduce_grad(grad)
                 self.opt.step(grad)
-                stats[j].copy_(st)
+                if st.data_ptr() != stats[j].data_ptr():
+                    stats[j].copy_(st)
                 j += 1
         self.num_updates += 1
         return stats.mean(0)

@@ -180,6 +180,32 @@ def linear_tanh(x, w, b, out, rows=None):
     return out
 
 
+def linear_tanh2(x, w0, b0, h0, w1, b1, h1, rows=None):
+    """linear_tanh for both MLPs (pi: w0/b0 -> h0, vf: w1/b1 -> h1) over the
+    same input rows, one launch."""
+    k = x.shape[1]
+    m, n = h0.shape
+    assert h1.shape == (m, n) and w0.shape == w1.shape == (n, k)
+    check(_lib.lib().dr_linear_tanh2(m, k, n, ptr(_f32(x)), _rows(rows), ptr(_f32(w0)),
+                                     ptr(_f32(b0)), ptr(h0), ptr(_f32(w1)), ptr(_f32(b1)),
+                                     ptr(h1), _s(x)))
+    return h0, h1
+
+
+def gather_minibatch(idx, obs, actions, aux, obs_out, actions_out, aux_out, adv_part=None):
+    """obs_out / actions_out / aux_out = rows idx of obs (., d) / actions
+    (., 4) / aux (., 3), one launch; with adv_part (a HeadLossBackward's
+    `adv_part`) also the advantage partials its normalisation needs."""
+    m = idx.numel()
+    assert idx.dtype == torch.int32 and idx.is_contiguous()
+    assert obs_out.shape == (m, obs.shape[1]) and actions_out.shape == (m, 4)
+    assert aux_out.shape == (m, 3) and actions.shape[1] == 4 and aux.shape[1] == 3
+    check(_lib.lib().dr_gather_minibatch(m, ptr(idx), obs.shape[1], ptr(_f32(obs)),
+                                         ptr(_f32(actions)), ptr(_f32(aux)), ptr(obs_out),
+                                         ptr(actions_out), ptr(aux_out), ptr(adv_part),
+                                         _s(obs)))
+
+
 def policy_heads(h_pi, h_vf, w_act, b_act, w_val, b_val, mean, value, preact=False):
     """mean (m,4) = h_pi w_act^T + b_act, value (m) = h_vf w_val^T + b_val;
     with preact the inputs are pre-activations and tanh is applied on load."""
@@ -204,22 +230,34 @@ class HeadLossBackward:
                               device=device)
         self.stats = torch.empty(8, dtype=torch.float32, device=device)
 
+    @property
+    def adv_part(self):
+        """Where gather_minibatch writes the advantage partials (the head of
+        the workspace) for a call with adv_ready=True."""
+        return self.ws
+
     def __call__(self, h_pi, h_vf, w_act, b_act, w_val, b_val, log_std, actions, aux,
                  gz_pi, gz_vf, g_w_act, g_b_act, g_w_val, g_b_val, g_b_pi, g_b_vf, g_log_std,
-                 rows=None, preact=False):
+                 rows=None, preact=False, adv_ready=False, stats_out=None):
         """actions (.,4) / aux (.,3) rows are read as [rows[r]] when rows
         (int32, m) is given, else the first m rows; with preact h_pi / h_vf
-        are the top layer's pre-activations (tanh applied on load)."""
+        are the top layer's pre-activations (tanh applied on load).  With
+        adv_ready the advantage partials were written by gather_minibatch
+        (adv_part=self.adv_part) for this minibatch; stats_out (8 f32)
+        receives the stats instead of self.stats."""
         assert h_pi.shape == (self.m, self.hd) and aux.shape[1] == 3
         assert rows is not None or aux.shape[0] == self.m
+        stats = self.stats if stats_out is None else stats_out
+        assert stats.numel() == 8 and stats.dtype == torch.float32 and stats.is_contiguous()
+        norm = 2 if (self.norm and adv_ready) else self.norm
         check(_lib.lib().dr_ppo_head_loss_backward(
             self.m, self.hd, int(bool(preact)), ptr(_f32(h_pi)), ptr(_f32(h_vf)), ptr(_f32(w_act)),
             ptr(_f32(b_act)), ptr(_f32(w_val)), ptr(_f32(b_val)), ptr(_f32(log_std)),
             ptr(_f32(actions)), ptr(_f32(aux)), _rows(rows), float(self.clip), float(self.ent),
-            float(self.vf), self.norm, ptr(gz_pi), ptr(gz_vf), ptr(g_w_act), ptr(g_b_act),
+            float(self.vf), norm, ptr(gz_pi), ptr(gz_vf), ptr(g_w_act), ptr(g_b_act),
             ptr(g_w_val), ptr(g_b_val), ptr(g_b_pi), ptr(g_b_vf), ptr(g_log_std),
-            ptr(self.stats), ptr(self.ws), self.ws.numel(), _s(h_pi)))
-        return self.stats
+            ptr(stats), ptr(self.ws), self.ws.numel(), _s(h_pi)))
+        return stats
 
 
 class FirstLayerBackward:
@@ -237,3 +275,23 @@ class FirstLayerBackward:
         check(_lib.lib().dr_first_layer_backward(
             self.m, self.k, self.n, ptr(_f32(grad_h)), ptr(_f32(h)), ptr(_f32(x)), _rows(rows),
             ptr(grad_w), ptr(grad_b), ptr(self.ws), self.ws.numel(), _s(h)))
+
+
+class FirstLayerBackward2:
+    """dr_first_layer_backward2: FirstLayerBackward for both MLPs over the
+    same input in one launch (bitwise the same as two single calls)."""
+
+    def __init__(self, m: int, k: int, n: int, device):
+        self.m, self.k, self.n = m, k, n
+        self.ws = torch.empty(_lib.lib().dr_first_layer_backward2_workspace_bytes(m, k, n),
+                              dtype=torch.uint8, device=device)
+
+    def __call__(self, x, grad_h0, h0, grad_w0, grad_b0, grad_h1, h1, grad_w1, grad_b1,
+                 rows=None):
+        for g, h in ((grad_h0, h0), (grad_h1, h1)):
+            assert g.shape == (self.m, self.n) and h.shape == (self.m, self.n)
+        assert x.shape[1] == self.k and (rows is not None or x.shape[0] == self.m)
+        check(_lib.lib().dr_first_layer_backward2(
+            self.m, self.k, self.n, ptr(_f32(x)), _rows(rows), ptr(_f32(grad_h0)), ptr(_f32(h0)),
+            ptr(grad_w0), ptr(grad_b0), ptr(_f32(grad_h1)), ptr(_f32(h1)), ptr(grad_w1),
+            ptr(grad_b1), ptr(self.ws), self.ws.numel(), _s(x)))

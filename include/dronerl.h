@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define DR_ABI_VERSION 4
+#define DR_ABI_VERSION 5
 
 enum dr_status {
     DR_OK = 0,
@@ -228,6 +228,19 @@ int dr_permutation(int64_t n, uint64_t seed, uint64_t counter, int32_t *out,
 int dr_gather_rows(int64_t m, int64_t width, const int32_t *idx,
                    const float *src, float *dst, void *stream);
 
+/* A whole PPO.train minibatch in one launch (RolloutBuffer.get's
+   `self.observations[batch_inds]` etc.): obs_out[r,:] = obs[idx[r],:]
+   (obs_dim floats), actions_out[r,:] = actions[idx[r],:] (4 floats, rows
+   16-byte aligned), aux_out[r,:] = aux[idx[r],:] (old_logp, advantage,
+   return).  With adv_part non-null it also writes the per-256-row
+   (count, mean, M2) partials of the gathered advantages that
+   dr_ppo_head_loss_backward's normalisation consumes: pass the head's
+   workspace and normalize_advantage = 2 there to skip its own pass. */
+int dr_gather_minibatch(int64_t m, const int32_t *idx, int64_t obs_dim,
+                        const float *obs, const float *actions,
+                        const float *aux, float *obs_out, float *actions_out,
+                        float *aux_out, float *adv_part, void *stream);
+
 /* Tanh-layer backward fused with the bias gradient (the MLP backward of
    PPO.train): grad_z = grad_h * (1 - h^2) for an (m, n) activation h =
    tanh(z), and bias_grad[j] = sum_i grad_z[i, j].  n must be a multiple of
@@ -248,6 +261,13 @@ int dr_linear_tanh(int64_t m, int64_t k, int64_t n, const float *x,
                    const int32_t *rows, const float *w, const float *b, float *h,
                    void *stream);
 
+/* dr_linear_tanh for both MLPs of the actor-critic (pi: w0/b0/h0, vf:
+   w1/b1/h1) over the same input rows, in one launch. */
+int dr_linear_tanh2(int64_t m, int64_t k, int64_t n, const float *x,
+                    const int32_t *rows, const float *w0, const float *b0,
+                    float *h0, const float *w1, const float *b1, float *h1,
+                    void *stream);
+
 /* Backward of the first layer h = tanh(x W^T + b), fused: for grad_h (m,n)
    = dLoss/dh, forms grad_z = grad_h * (1 - h^2) in registers (never stored)
    and writes grad_w (n,k) = grad_z^T x and grad_b (n) = sum_r grad_z
@@ -261,6 +281,19 @@ int dr_first_layer_backward(int64_t m, int64_t k, int64_t n, const float *grad_h
                             const float *h, const float *x, const int32_t *rows,
                             float *grad_w, float *grad_b, void *workspace,
                             size_t workspace_bytes, void *stream);
+
+/* dr_first_layer_backward for both MLPs (net 0: grad_h0/h0 -> grad_w0/
+   grad_b0, net 1: grad_h1/h1 -> grad_w1/grad_b1) over the same input x in
+   one launch (plus one column-sum and one finish launch for both).
+   Bitwise the same results as two dr_first_layer_backward calls.
+   `workspace` >= dr_first_layer_backward2_workspace_bytes(m, k, n). */
+size_t dr_first_layer_backward2_workspace_bytes(int64_t m, int64_t k, int64_t n);
+int dr_first_layer_backward2(int64_t m, int64_t k, int64_t n, const float *x,
+                             const int32_t *rows, const float *grad_h0,
+                             const float *h0, float *grad_w0, float *grad_b0,
+                             const float *grad_h1, const float *h1,
+                             float *grad_w1, float *grad_b1, void *workspace,
+                             size_t workspace_bytes, void *stream);
 
 /* Policy heads for rollouts (ActorCriticPolicy.forward's action_net /
    value_net): mean (m,4) = h_pi W_act^T + b_act, value (m) = h_vf W_val^T +
@@ -285,7 +318,9 @@ int dr_policy_heads(int64_t m, int64_t hd, int preact, const float *h_pi,
    dr_ppo_loss.  Gradient outputs are written (not accumulated); they may be
    views into one flat gradient buffer.  Deterministic (fixed-order partial
    sums).  `preact` as dr_policy_heads (h_pi / h_vf pre-activations; grad_z
-   uses tanh(z)).  `workspace` >= dr_ppo_head_workspace_bytes(m, hd). */
+   uses tanh(z)).  `workspace` >= dr_ppo_head_workspace_bytes(m, hd).
+   normalize_advantage: 0 off, 1 on, 2 on with the advantage partials
+   already written to the head of `workspace` by dr_gather_minibatch. */
 size_t dr_ppo_head_workspace_bytes(int64_t m, int64_t hd);
 int dr_ppo_head_loss_backward(int64_t m, int64_t hd, int preact, const float *h_pi,
                               const float *h_vf, const float *w_act,

@@ -290,3 +290,66 @@ def test_fused_step_rows_in_place_equals_gathered():
     r = rows.long()
     g2, s2 = fs.step(obs[r].contiguous(), act[r].contiguous(), aux[r].contiguous(), head)
     assert torch.equal(g1, g2) and torch.equal(s1, s2)
+
+
+@pytest.mark.parametrize("k,n,m", [(15, 256, 65536), (18, 128, 1001), (12, 64, 77)])
+def test_paired_first_layer_kernels_equal_single(k, n, m):
+    """dr_linear_tanh2 / dr_first_layer_backward2 (both MLPs in one launch)
+    are bitwise the single-net kernels, with and without rows=."""
+    from drone_rl_amd import ppo_kernels as K
+    g = torch.Generator(device="cuda").manual_seed(k * n + m)
+    total = m + 13
+    x = torch.randn(total, k, device="cuda", generator=g)
+    rows = torch.randperm(total, device="cuda", generator=g)[:m].to(torch.int32)
+    w = [torch.randn(n, k, device="cuda", generator=g) * 0.4 for _ in range(2)]
+    b = [torch.randn(n, device="cuda", generator=g) * 0.1 for _ in range(2)]
+    gh = [torch.randn(m, n, device="cuda", generator=g) for _ in range(2)]
+    for r in (None, rows):
+        xs = x[:m] if r is None else x
+        h1 = [torch.empty(m, n, device="cuda") for _ in range(2)]
+        for j in range(2):
+            K.linear_tanh(xs, w[j], b[j], h1[j], r)
+        h2 = [torch.empty(m, n, device="cuda") for _ in range(2)]
+        K.linear_tanh2(xs, w[0], b[0], h2[0], w[1], b[1], h2[1], r)
+        assert torch.equal(h1[0], h2[0]) and torch.equal(h1[1], h2[1])
+        single = K.FirstLayerBackward(m, k, n, "cuda")
+        ref = []
+        for j in range(2):
+            gw, gb = torch.empty(n, k, device="cuda"), torch.empty(n, device="cuda")
+            single(gh[j], h1[j], xs, gw, gb, r)
+            ref += [gw, gb]
+        out = [torch.full((n, k), float("nan"), device="cuda"),
+               torch.full((n,), float("nan"), device="cuda")] * 2
+        out = [t.clone() for t in out]
+        K.FirstLayerBackward2(m, k, n, "cuda")(xs, gh[0], h1[0], out[0], out[1],
+                                               gh[1], h1[1], out[2], out[3], r)
+        for a, c in zip(ref, out):
+            assert torch.equal(a, c)
+
+
+@pytest.mark.parametrize("m,d", [(65536, 15), (1000, 18), (300, 12)])
+def test_gather_minibatch_equals_gathers_and_adv_pass(m, d):
+    """dr_gather_minibatch == three dr_gather_rows, and the head step fed
+    its advantage partials (normalize_advantage = 2) is bitwise the head
+    step that computes them itself."""
+    from drone_rl_amd import ppo_kernels as K
+    from drone_rl_amd.policy import ActorCritic, FusedTrainStep
+    g = torch.Generator(device="cuda").manual_seed(m + d)
+    total = 2 * m + 5
+    obs = torch.randn(total, d, device="cuda", generator=g)
+    act = torch.rand(total, 4, device="cuda", generator=g) * 7.3575
+    aux = torch.randn(total, 3, device="cuda", generator=g)
+    idx = torch.randperm(total, device="cuda", generator=g)[:m].to(torch.int32)
+    o, a, x = (torch.empty(m, w, device="cuda") for w in (d, 4, 3))
+    head = K.HeadLossBackward(m, 256, "cuda", 0.2, 0.0, 0.5, True)
+    K.gather_minibatch(idx, obs, act, aux, o, a, x, adv_part=head.adv_part)
+    r = idx.long()
+    assert torch.equal(o, obs[r]) and torch.equal(a, act[r]) and torch.equal(x, aux[r])
+    pol = ActorCritic(d, 4, (256, 256), device="cuda", seed=6)
+    fs = FusedTrainStep(pol, m)
+    st_out = torch.empty(8, device="cuda")
+    g1, s1 = fs.step(o, a, x, head, adv_ready=True, stats_out=st_out)
+    assert s1.data_ptr() == st_out.data_ptr()
+    g1, s1 = g1.clone(), s1.clone()
+    g2, s2 = fs.step(o, a, x, head)          # the head's own advantage pass
+    assert torch.equal(g1, g2) and torch.equal(s1, s2)
