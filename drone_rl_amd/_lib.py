@@ -23,7 +23,7 @@ DR_ERR_HIP = -2
 DR_ERR_NOMEM = -3
 DR_ERR_UNSUPPORTED = -4
 
-ABI_VERSION = 5                 # DR_ABI_VERSION in include/dronerl.h
+ABI_VERSION = 6                 # DR_ABI_VERSION in include/dronerl.h
 DR_VARIANT_GYM = 0
 DR_VARIANT_VECTORIZED = 1
 DR_VARIANT_MOVING = 2
@@ -91,9 +91,9 @@ SIGNATURES = {
     "dr_first_layer_backward_workspace_bytes": (c_size_t, [c_int64, c_int64, c_int64]),
     "dr_first_layer_backward": (c_int, [c_int64, c_int64, c_int64, _P, _P, _P, _P, _P, _P,
                                         _P, c_size_t, _P]),
-    "dr_policy_heads": (c_int, [c_int64, c_int64, c_int, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
+    "dr_policy_heads": (c_int, [c_int64, c_int64, c_int] + [_P] * 11),
     "dr_ppo_head_workspace_bytes": (c_size_t, [c_int64, c_int64]),
-    "dr_ppo_head_loss_backward": (c_int, [c_int64, c_int64, c_int] + [_P] * 10 +
+    "dr_ppo_head_loss_backward": (c_int, [c_int64, c_int64, c_int] + [_P] * 12 +
                                   [c_float, c_float, c_float, c_int] + [_P] * 10 +
                                   [_P, c_size_t, _P]),
     "dr_ppo_loss_workspace_bytes": (c_size_t, [c_int64]),

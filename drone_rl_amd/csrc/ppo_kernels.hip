@@ -568,6 +568,11 @@ __device__ inline void st4(float *p, float4 x) {
 __device__ inline float4 tanh4(float4 v) {
     return make_float4(tanh_fast(v.x), tanh_fast(v.y), tanh_fast(v.z), tanh_fast(v.w));
 }
+// z + b, as the GEMM epilogue would have added it (z already the full dot
+// product; b = 0 adds exactly nothing)
+__device__ inline float4 add4(float4 a, float4 b) {
+    return make_float4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w);
+}
 __device__ inline float dot4(float4 a, float4 b) {
     return fmaf(a.w, b.w, fmaf(a.z, b.z, fmaf(a.y, b.y, a.x * b.x)));
 }
@@ -646,6 +651,7 @@ __global__ __launch_bounds__(kBlock) void linear_tanh_kernel(int64_t m, int n,
 // value = h_vf Wv^T + bv (m).
 __global__ __launch_bounds__(kBlock) void policy_heads_kernel(
     int64_t m, int hd, int preact, const float *__restrict__ h_pi, const float *__restrict__ h_vf,
+    const float *__restrict__ zb_pi, const float *__restrict__ zb_vf,
     const float *__restrict__ w_act, const float *__restrict__ b_act,
     const float *__restrict__ w_val, const float *__restrict__ b_val,
     float4 *__restrict__ mean, float *__restrict__ value) {
@@ -653,6 +659,9 @@ __global__ __launch_bounds__(kBlock) void policy_heads_kernel(
     const int c0 = 4 * lane;
     const bool act = c0 < hd;
     const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
+    // the top hidden layer's bias, when its GEMM left it out (zb_*)
+    const float4 zbp = (act && zb_pi) ? ld4(zb_pi + c0) : z4;
+    const float4 zbv = (act && zb_vf) ? ld4(zb_vf + c0) : z4;
     float4 wa[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) wa[j] = act ? ld4(w_act + j * hd + c0) : z4;
@@ -661,8 +670,8 @@ __global__ __launch_bounds__(kBlock) void policy_heads_kernel(
         float4 hp = act ? ld4(h_pi + r * hd + c0) : z4;
         float4 hv = act ? ld4(h_vf + r * hd + c0) : z4;
         if (preact) {         // inputs are pre-activations: the layer's tanh here
-            hp = tanh4(hp);
-            hv = tanh4(hv);
+            hp = tanh4(add4(hp, zbp));
+            hv = tanh4(add4(hv, zbv));
         }
         float d[5];
 #pragma unroll
@@ -692,6 +701,7 @@ struct HeadArgs {
     int hd;
     int preact;  // h_pi / h_vf are pre-activations z; the top tanh is applied here
     const float *h_pi, *h_vf;
+    const float *zb_pi, *zb_vf;  // nullable: top-layer bias added to z before the tanh
     const float *w_act, *b_act, *w_val, *b_val, *log_std;
     const float4 *actions;
     const float *aux;  // (m,3): old_logp, advantage, return
@@ -730,6 +740,8 @@ __global__ __launch_bounds__(kBlock) void ppo_head_kernel(HeadArgs a) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) wa[j] = act ? ld4(a.w_act + j * hd + c0) : z4;
     const float4 wv = act ? ld4(a.w_val + c0) : z4;
+    const float4 zbp = (act && a.zb_pi) ? ld4(a.zb_pi + c0) : z4;
+    const float4 zbv = (act && a.zb_vf) ? ld4(a.zb_vf + c0) : z4;
     const float ba[4] = {a.b_act[0], a.b_act[1], a.b_act[2], a.b_act[3]};
     const float bv = a.b_val[0];
     // lane-partial sums of the loss terms and of d b_act / d b_val
@@ -757,8 +769,8 @@ __global__ __launch_bounds__(kBlock) void ppo_head_kernel(HeadArgs a) {
         if (a.preact) {
 #pragma unroll
             for (int i = 0; i < kHeadTile; ++i) {
-                hp[i] = tanh4(hp[i]);
-                hv[i] = tanh4(hv[i]);
+                hp[i] = tanh4(add4(hp[i], zbp));
+                hv[i] = tanh4(add4(hv[i], zbv));
             }
         }
         // this lane's row (lane < nr): its loss inputs, loaded while the dots run
@@ -1357,7 +1369,7 @@ int dr_linear_tanh2(int64_t m, int64_t k, int64_t n, const float *x, const int32
 }
 
 int dr_policy_heads(int64_t m, int64_t hd, int preact, const float *h_pi, const float *h_vf,
-                    const float *w_act, const float *b_act, const float *w_val,
+                    const float *zb_pi, const float *zb_vf, const float *w_act, const float *b_act, const float *w_val,
                     const float *b_val, float *mean, float *value, void *stream) {
     if (m < 1 || hd < 4 || hd > 256 || (hd & 3) || !h_pi || !h_vf || !w_act || !b_act ||
         !w_val || !b_val || !mean || !value)
@@ -1365,8 +1377,13 @@ int dr_policy_heads(int64_t m, int64_t hd, int preact, const float *h_pi, const 
     if ((((uintptr_t)h_pi) | ((uintptr_t)h_vf) | ((uintptr_t)w_act) | ((uintptr_t)w_val) |
          ((uintptr_t)mean)) & 15)
         return fail0(DR_ERR_INVALID, "dr_policy_heads: buffers must be 16-byte aligned");
+    if ((zb_pi || zb_vf) && !preact)
+        return fail0(DR_ERR_INVALID, "dr_policy_heads: zb_pi / zb_vf need preact");
+    if ((((uintptr_t)zb_pi) | ((uintptr_t)zb_vf)) & 15)
+        return fail0(DR_ERR_INVALID, "dr_policy_heads: zb_pi / zb_vf must be 16-byte aligned");
     hipLaunchKernelGGL(policy_heads_kernel, dim3(head_blocks(m)), dim3(kBlock), 0,
-                       as_stream(stream), m, (int)hd, preact, h_pi, h_vf, w_act, b_act, w_val, b_val,
+                       as_stream(stream), m, (int)hd, preact, h_pi, h_vf, zb_pi, zb_vf, w_act, b_act,
+                       w_val, b_val,
                        reinterpret_cast<float4 *>(mean), value);
     return check_launch("dr_policy_heads");
 }
@@ -1380,7 +1397,7 @@ size_t dr_ppo_head_workspace_bytes(int64_t m, int64_t hd) {
 }
 
 int dr_ppo_head_loss_backward(int64_t m, int64_t hd, int preact, const float *h_pi,
-                              const float *h_vf,
+                              const float *h_vf, const float *zb_pi, const float *zb_vf,
                               const float *w_act, const float *b_act, const float *w_val,
                               const float *b_val, const float *log_std, const float *actions,
                               const float *aux, const int32_t *rows, float clip_range,
@@ -1398,6 +1415,11 @@ int dr_ppo_head_loss_backward(int64_t m, int64_t hd, int preact, const float *h_
          ((uintptr_t)actions) | ((uintptr_t)gz_pi) | ((uintptr_t)gz_vf)) & 15)
         return fail0(DR_ERR_INVALID,
                      "dr_ppo_head_loss_backward: row buffers must be 16-byte aligned");
+    if ((zb_pi || zb_vf) && !preact)
+        return fail0(DR_ERR_INVALID, "dr_ppo_head_loss_backward: zb_pi / zb_vf need preact");
+    if ((((uintptr_t)zb_pi) | ((uintptr_t)zb_vf)) & 15)
+        return fail0(DR_ERR_INVALID,
+                     "dr_ppo_head_loss_backward: zb_pi / zb_vf must be 16-byte aligned");
     if (!workspace || workspace_bytes < dr_ppo_head_workspace_bytes(m, hd))
         return fail0(DR_ERR_INVALID, "dr_ppo_head_loss_backward: workspace too small");
     const int norm = normalize_advantage && m > 1;
@@ -1416,7 +1438,7 @@ int dr_ppo_head_loss_backward(int64_t m, int64_t hd, int preact, const float *h_
     }
     const int nb = head_blocks(m);
     const int P = kHeadFixed + 7 * (int)hd;
-    HeadArgs a{m, (int)hd, preact, h_pi, h_vf, w_act, b_act, w_val, b_val, log_std,
+    HeadArgs a{m, (int)hd, preact, h_pi, h_vf, zb_pi, zb_vf, w_act, b_act, w_val, b_val, log_std,
                reinterpret_cast<const float4 *>(actions), aux, rows, clip_range, ent_coef,
                vf_coef, norm, adv_part, anb, gz_pi, gz_vf, part, P};
     hipLaunchKernelGGL(ppo_head_kernel, dim3(nb), dim3(kBlock), sizeof(float) * 4 * P, st, a);

@@ -30,13 +30,15 @@ TUNED_GEMMS_CSV = os.path.join(os.path.dirname(os.path.abspath(__file__)), "tune
 def use_tuned_gemms(path: str = TUNED_GEMMS_CSV) -> bool:
     """Load the GEMM solutions measured for this trainer's shapes on MI355X.
 
-    The three fp32 GEMM shapes of a 65,536-row 2x256 minibatch (forward
-    addmm, batched grad-input, batched split-K weight gradient) were timed by
+    The fp32 GEMM shapes of a 65,536-row 2x256 minibatch (the batched
+    top-layer forward of both MLPs, batched grad-input, batched split-K
+    weight gradient; the single-net addmm) were timed by
     PyTorch's TunableOp over every hipBLASLt and rocBLAS solution on the box
     (scripts/tune_gemm.sh); the winners are committed in `tuned/`.  This
     turns TunableOp on in lookup-only mode (no tuning at run time; shapes
     not in the file keep the library heuristic).  The grad-input GEMM goes
-    from 146 to 123 us, the weight gradient from 126 to 122 us.
+    from 146 to 123 us, the weight gradient from 126 to 122 us, the batched
+    forward takes 125 us (two heuristic addmm: 148 us).
     `DRONERL_TUNED_GEMMS=0` opts out; a caller that already enabled TunableOp
     (PYTORCH_TUNABLEOP_*) keeps its own settings.  Returns whether the file
     was loaded (False off-GPU or when its validators do not match)."""
@@ -319,7 +321,7 @@ class FusedTrainStep:
                      self.gview("action.b"), self.gview("value.w"), self.gview("value.b"),
                      self.gview(f"pi{top}.b"), self.gview(f"vf{top}.b"),
                      self.gview("log_std"), rows, preact=preact, adv_ready=adv_ready,
-                     stats_out=stats_out)
+                     stats_out=stats_out, **top_bias(pol, self._acts2))
         if depth == 1:                        # the head kernel gave grad_z of layer 0
             if rows is not None:
                 obs = obs.index_select(0, rows.long())
@@ -415,12 +417,19 @@ def hidden_forward(pol: ActorCritic, obs, acts, acts2=None, rows=None, top_preac
     acts[pre][k] (M, net_arch[k]); with acts2 (the (2, M, n) buffers that
     acts views) each layer's tanh runs once over both MLPs; with rows the
     input rows are obs[rows].  With top_preact (and depth >= 2) the top
-    layer is left as pre-activations z: its only consumer, the head kernel,
-    applies tanh on load, so the (M, n) tanh pass is skipped."""
+    layer is left as pre-activations z WITHOUT its bias: its only consumer,
+    the head kernel, adds the bias and applies tanh on load (top_bias(pol)
+    gives the pointers), so the (M, n) tanh pass is skipped and both MLPs'
+    top GEMMs run as ONE batched GEMM (no bias epilogue; 125 us against
+    2 x 74 us for two addmm at M = 65,536, MI355X-tuned solutions)."""
     from . import ppo_kernels as K
     K.linear_tanh2(obs, pol.p("pi0.w"), pol.p("pi0.b"), acts["pi"][0],
                    pol.p("vf0.w"), pol.p("vf0.b"), acts["vf"][0], rows)
+    top = len(pol.net_arch) - 1
     for k in range(1, len(pol.net_arch)):
+        if top_preact and k == top and acts2 is not None:
+            torch.bmm(acts2[k - 1], pol.p2(k, "w").transpose(1, 2), out=acts2[k])
+            continue
         for pre in ("pi", "vf"):
             torch.addmm(pol.p(f"{pre}{k}.b"), acts[pre][k - 1], pol.p(f"{pre}{k}.w").t(),
                         out=acts[pre][k])
@@ -432,6 +441,16 @@ def hidden_forward(pol: ActorCritic, obs, acts, acts2=None, rows=None, top_preac
             for pre in ("pi", "vf"):
                 torch.tanh_(acts[pre][k])
     return acts
+
+
+def top_bias(pol: ActorCritic, acts2) -> dict:
+    """zb_pi / zb_vf kwargs for the head kernels after hidden_forward(...,
+    acts2, top_preact=True): the top layer's biases (its batched GEMM left
+    them out)."""
+    if len(pol.net_arch) < 2 or acts2 is None:
+        return {}
+    top = len(pol.net_arch) - 1
+    return {"zb_pi": pol.p(f"pi{top}.b"), "zb_vf": pol.p(f"vf{top}.b")}
 
 
 class PolicyInference:
@@ -456,5 +475,5 @@ class PolicyInference:
         hs = hidden_forward(pol, obs, self.acts, self.acts2, top_preact=preact)
         K.policy_heads(hs["pi"][-1], hs["vf"][-1], pol.p("action.w"), pol.p("action.b"),
                        pol.p("value.w"), pol.p("value.b"), self.mean, self.value,
-                       preact=preact)
+                       preact=preact, **top_bias(pol, self.acts2))
         return self.mean, self.value

@@ -206,12 +206,15 @@ def gather_minibatch(idx, obs, actions, aux, obs_out, actions_out, aux_out, adv_
                                          _s(obs)))
 
 
-def policy_heads(h_pi, h_vf, w_act, b_act, w_val, b_val, mean, value, preact=False):
+def policy_heads(h_pi, h_vf, w_act, b_act, w_val, b_val, mean, value, preact=False,
+                 zb_pi=None, zb_vf=None):
     """mean (m,4) = h_pi w_act^T + b_act, value (m) = h_vf w_val^T + b_val;
-    with preact the inputs are pre-activations and tanh is applied on load."""
+    with preact the inputs are pre-activations and tanh(z + zb) is applied
+    on load (zb_pi / zb_vf: the top layer's biases, when its GEMM left them
+    out)."""
     m, hd = h_pi.shape
     check(_lib.lib().dr_policy_heads(m, hd, int(bool(preact)), ptr(_f32(h_pi)), ptr(_f32(h_vf)),
-                                     ptr(_f32(w_act)),
+                                     ptr(zb_pi), ptr(zb_vf), ptr(_f32(w_act)),
                                      ptr(_f32(b_act)), ptr(_f32(w_val)), ptr(_f32(b_val)),
                                      ptr(mean), ptr(value), _s(h_pi)))
     return mean, value
@@ -238,20 +241,23 @@ class HeadLossBackward:
 
     def __call__(self, h_pi, h_vf, w_act, b_act, w_val, b_val, log_std, actions, aux,
                  gz_pi, gz_vf, g_w_act, g_b_act, g_w_val, g_b_val, g_b_pi, g_b_vf, g_log_std,
-                 rows=None, preact=False, adv_ready=False, stats_out=None):
+                 rows=None, preact=False, adv_ready=False, stats_out=None, zb_pi=None,
+                 zb_vf=None):
         """actions (.,4) / aux (.,3) rows are read as [rows[r]] when rows
         (int32, m) is given, else the first m rows; with preact h_pi / h_vf
         are the top layer's pre-activations (tanh applied on load).  With
         adv_ready the advantage partials were written by gather_minibatch
         (adv_part=self.adv_part) for this minibatch; stats_out (8 f32)
-        receives the stats instead of self.stats."""
+        receives the stats instead of self.stats; zb_pi / zb_vf as
+        policy_heads."""
         assert h_pi.shape == (self.m, self.hd) and aux.shape[1] == 3
         assert rows is not None or aux.shape[0] == self.m
         stats = self.stats if stats_out is None else stats_out
         assert stats.numel() == 8 and stats.dtype == torch.float32 and stats.is_contiguous()
         norm = 2 if (self.norm and adv_ready) else self.norm
         check(_lib.lib().dr_ppo_head_loss_backward(
-            self.m, self.hd, int(bool(preact)), ptr(_f32(h_pi)), ptr(_f32(h_vf)), ptr(_f32(w_act)),
+            self.m, self.hd, int(bool(preact)), ptr(_f32(h_pi)), ptr(_f32(h_vf)), ptr(zb_pi),
+            ptr(zb_vf), ptr(_f32(w_act)),
             ptr(_f32(b_act)), ptr(_f32(w_val)), ptr(_f32(b_val)), ptr(_f32(log_std)),
             ptr(_f32(actions)), ptr(_f32(aux)), _rows(rows), float(self.clip), float(self.ent),
             float(self.vf), norm, ptr(gz_pi), ptr(gz_vf), ptr(g_w_act), ptr(g_b_act),

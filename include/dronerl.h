@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define DR_ABI_VERSION 5
+#define DR_ABI_VERSION 6
 
 enum dr_status {
     DR_OK = 0,
@@ -299,10 +299,12 @@ int dr_first_layer_backward2(int64_t m, int64_t k, int64_t n, const float *x,
    value_net): mean (m,4) = h_pi W_act^T + b_act, value (m) = h_vf W_val^T +
    b_val, for the top hidden activations h_pi, h_vf (m,hd), hd % 4 == 0,
    hd <= 256.  With preact != 0 the inputs are the top layer's
-   PRE-activations z and tanh(z) is applied on load (the layer's separate
-   tanh pass is then skipped).  Row buffers 16-byte aligned. */
+   PRE-activations z and tanh(z + zb) is applied on load (the layer's
+   separate tanh pass is then skipped); zb_pi / zb_vf (nullable, hd floats,
+   16-byte aligned; only with preact) are the top layer's biases when its
+   GEMM left them out.  Row buffers 16-byte aligned. */
 int dr_policy_heads(int64_t m, int64_t hd, int preact, const float *h_pi,
-                    const float *h_vf,
+                    const float *h_vf, const float *zb_pi, const float *zb_vf,
                     const float *w_act, const float *b_act, const float *w_val,
                     const float *b_val, float *mean, float *value, void *stream);
 
@@ -317,13 +319,14 @@ int dr_policy_heads(int64_t m, int64_t hd, int preact, const float *h_pi,
    the top hidden biases b_pi, b_vf (hd) and log_std (4), and stats (8) as
    dr_ppo_loss.  Gradient outputs are written (not accumulated); they may be
    views into one flat gradient buffer.  Deterministic (fixed-order partial
-   sums).  `preact` as dr_policy_heads (h_pi / h_vf pre-activations; grad_z
-   uses tanh(z)).  `workspace` >= dr_ppo_head_workspace_bytes(m, hd).
+   sums).  `preact`, zb_pi, zb_vf as dr_policy_heads (h_pi / h_vf
+   pre-activations; grad_z uses tanh(z + zb)).  `workspace` >= dr_ppo_head_workspace_bytes(m, hd).
    normalize_advantage: 0 off, 1 on, 2 on with the advantage partials
    already written to the head of `workspace` by dr_gather_minibatch. */
 size_t dr_ppo_head_workspace_bytes(int64_t m, int64_t hd);
 int dr_ppo_head_loss_backward(int64_t m, int64_t hd, int preact, const float *h_pi,
-                              const float *h_vf, const float *w_act,
+                              const float *h_vf, const float *zb_pi,
+                              const float *zb_vf, const float *w_act,
                               const float *b_act, const float *w_val,
                               const float *b_val, const float *log_std,
                               const float *actions, const float *aux,

@@ -215,6 +215,12 @@ def test_policy_heads_match_torch():
     t = torch.tanh(z)
     assert (mean - torch.addmm(ba, t, wa.t())).abs().max().item() <= 1e-5
     assert (value - torch.addmm(bv, t, wv.t()).squeeze(1)).abs().max().item() <= 1e-5
+    # top-layer biases added on load (the batched top GEMM leaves them out)
+    zp, zv = torch.randn(hd, device="cuda"), torch.randn(hd, device="cuda")
+    K.policy_heads(z, z, wa, ba, wv, bv, mean, value, preact=True, zb_pi=zp, zb_vf=zv)
+    tp, tv = torch.tanh(z + zp), torch.tanh(z + zv)
+    assert (mean - torch.addmm(ba, tp, wa.t())).abs().max().item() <= 1e-5
+    assert (value - torch.addmm(bv, tv, wv.t()).squeeze(1)).abs().max().item() <= 1e-5
 
 
 @pytest.mark.parametrize("arch,m", [((256, 256), 65536), ((64, 64), 64), ((64, 128), 1000)])
