@@ -45,6 +45,8 @@ def parse():
     ap.add_argument("--envs", type=int, default=65536, help="envs per GPU")
     ap.add_argument("--state-dtype", choices=["f64", "f32"], default="f64")
     ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--graph-warm-replays", type=int, default=1,
+                    help="untimed replays of the captured step graph before the timed one")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=1.5)
     ap.add_argument("--ppo-updates", type=int, default=3,
@@ -101,6 +103,11 @@ def time_env(args, dtype_name, n_envs, rank, world, device, steps, warmup, varia
                 for t in range(warmup, total):
                     b.step(acts[t])
         stream.wait_stream(s)
+        # untimed replays of the captured graph: its first launch uploads
+        # the graph to the device; the env simply runs K more warm-up steps
+        # on the same pre-generated actions
+        for _ in range(args.graph_warm_replays):
+            graph.replay()
     torch.cuda.synchronize(device)
     ev0 = torch.cuda.Event(enable_timing=True)
     ev1 = torch.cuda.Event(enable_timing=True)
