@@ -23,7 +23,7 @@ DR_ERR_HIP = -2
 DR_ERR_NOMEM = -3
 DR_ERR_UNSUPPORTED = -4
 
-ABI_VERSION = 6                 # DR_ABI_VERSION in include/dronerl.h
+ABI_VERSION = 7                 # DR_ABI_VERSION in include/dronerl.h
 DR_VARIANT_GYM = 0
 DR_VARIANT_VECTORIZED = 1
 DR_VARIANT_MOVING = 2
@@ -43,6 +43,20 @@ class dr_config(ctypes.Structure):
                 ("auto_reset", c_int32), ("device", c_int32),
                 ("max_steps", c_int32), ("seed", c_uint64),
                 ("env_id_offset", c_int64), ("dt", c_double)]
+
+
+class dr_grad_finish(ctypes.Structure):
+    """include/dronerl.h dr_grad_finish (deferred gradient reductions)."""
+    _fields_ = [("head_workspace", c_void_p), ("head_m", c_int64), ("head_hd", c_int64),
+                ("log_std", c_void_p), ("ent_coef", c_float), ("vf_coef", c_float),
+                ("g_w_act", c_void_p), ("g_b_act", c_void_p), ("g_w_val", c_void_p),
+                ("g_b_val", c_void_p), ("g_b_pi", c_void_p), ("g_b_vf", c_void_p),
+                ("g_log_std", c_void_p), ("stats", c_void_p),
+                ("first_workspace", c_void_p), ("first_m", c_int64), ("first_k", c_int64),
+                ("first_n", c_int64),
+                ("g_w0", c_void_p), ("g_b0", c_void_p), ("g_w1", c_void_p), ("g_b1", c_void_p),
+                ("chunks", c_void_p), ("chunk_groups", c_int64), ("chunk_count", c_int64),
+                ("chunk_size", c_int64), ("chunk_dst", c_void_p)]
 
 
 class DroneRLError(RuntimeError):
@@ -83,8 +97,8 @@ SIGNATURES = {
     "dr_gather_minibatch": (c_int, [c_int64, _P, c_int64] + [_P] * 8),
     "dr_linear_tanh2": (c_int, [c_int64, c_int64, c_int64] + [_P] * 9),
     "dr_first_layer_backward2_workspace_bytes": (c_size_t, [c_int64, c_int64, c_int64]),
-    "dr_first_layer_backward2": (c_int, [c_int64, c_int64, c_int64] + [_P] * 11 +
-                                 [c_size_t, _P]),
+    "dr_first_layer_backward2": (c_int, [c_int64, c_int64, c_int64] + [_P] * 10 +
+                                 [c_int, _P, c_size_t, _P]),
     "dr_tanh_backward_workspace_bytes": (c_size_t, [c_int64, c_int64]),
     "dr_tanh_backward": (c_int, [c_int64, c_int64, _P, _P, _P, _P, _P, c_size_t, _P]),
     "dr_linear_tanh": (c_int, [c_int64, c_int64, c_int64, _P, _P, _P, _P, _P, _P]),
@@ -95,7 +109,7 @@ SIGNATURES = {
     "dr_ppo_head_workspace_bytes": (c_size_t, [c_int64, c_int64]),
     "dr_ppo_head_loss_backward": (c_int, [c_int64, c_int64, c_int] + [_P] * 12 +
                                   [c_float, c_float, c_float, c_int] + [_P] * 10 +
-                                  [_P, c_size_t, _P]),
+                                  [c_int, _P, c_size_t, _P]),
     "dr_ppo_loss_workspace_bytes": (c_size_t, [c_int64]),
     "dr_ppo_loss": (c_int, [c_int64, _P, _P, _P, _P, _P, _P, _P, c_int64, c_float,
                             c_float, c_float, c_int, _P, _P, _P, _P, _P,
@@ -103,6 +117,10 @@ SIGNATURES = {
     "dr_adam_workspace_bytes": (c_size_t, [c_int64]),
     "dr_clip_adam": (c_int, [c_int64, _P, _P, _P, _P, c_double, c_double, c_double,
                              c_double, c_float, c_int64, _P, _P, c_size_t, _P]),
+    "dr_grad_finish_workspace_bytes": (c_size_t, [_P]),
+    "dr_grad_finish_clip_adam": (c_int, [_P, c_int64, _P, _P, _P, _P, c_double, c_double,
+                                         c_double, c_double, c_float, c_int64, _P, _P,
+                                         c_size_t, _P]),
 }
 
 _lib = None

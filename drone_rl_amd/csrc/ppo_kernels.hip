@@ -951,18 +951,16 @@ struct FirstBwdOut {
     float *gb[2];
 };
 
-__global__ __launch_bounds__(kBlock) void first_layer_finish_kernel(int ng, int n, int K,
-                                                                    int nets,
-                                                                    const float *__restrict__ part,
-                                                                    FirstBwdOut o) {
+// One thread's share of the first-layer finish (see first_layer_finish_kernel);
+// returns the square of the gradient entry it wrote.
+__device__ inline float first_finish_part(int bx, int ng, int n, int K, int nets,
+                                          const float *__restrict__ part, const FirstBwdOut &o) {
     const int P1 = (K + 1) * n;
     const int P = nets * P1;
-    const int pp = blockIdx.x * kBlock + threadIdx.x;
-    if (pp >= P) return;
+    const int pp = bx * kBlock + threadIdx.x;
+    if (pp >= P) return 0.f;
     const int net = pp >= P1 ? 1 : 0;
     const int p = pp - net * P1;
-    float *__restrict__ gw = o.gw[net];
-    float *__restrict__ gb = o.gb[net];
     float s0 = 0.f, s1 = 0.f;
     int g = 0;
     for (; g + 1 < ng; g += 2) {
@@ -972,8 +970,16 @@ __global__ __launch_bounds__(kBlock) void first_layer_finish_kernel(int ng, int 
     if (g < ng) s0 += part[(int64_t)g * P + pp];
     const float s = s0 + s1;
     const int k = p / n, c = p - k * n;
-    if (k < K) gw[c * K + k] = s;
-    else gb[c] = s;
+    if (k < K) o.gw[net][c * K + k] = s;
+    else o.gb[net][c] = s;
+    return s * s;
+}
+
+__global__ __launch_bounds__(kBlock) void first_layer_finish_kernel(int ng, int n, int K,
+                                                                    int nets,
+                                                                    const float *__restrict__ part,
+                                                                    FirstBwdOut o) {
+    (void)first_finish_part(blockIdx.x, ng, n, K, nets, part, o);
 }
 
 // Gradient outputs of the head step (finish kernel).
@@ -1000,12 +1006,18 @@ __global__ __launch_bounds__(kBlock) void colsum_groups_kernel(int nb, int P, in
     out[(int64_t)blockIdx.y * P + p] = ((s[0] + s[1]) + (s[2] + s[3])) + ((s[4] + s[5]) + (s[6] + s[7]));
 }
 
-__global__ __launch_bounds__(kBlock) void ppo_head_finish_kernel(
-    int nb, int P, int hd, int64_t m, const float *__restrict__ part,
-    const float *__restrict__ adv_ms, const float *__restrict__ log_std, float ent_coef,
-    float vf_coef, HeadOut o) {
+// One thread's share of the head-gradient finish: the level-2 sum of the
+// grouped partials, scattered to the gradient outputs; block bx == 0 also
+// forms the loss statistics and the log_std gradient.  Returns the sum of
+// squares of the gradient entries this thread wrote (for the norm).
+__device__ inline float head_finish_part(int bx, int nb, int P, int hd, int64_t m,
+                                         const float *__restrict__ part,
+                                         const float *__restrict__ adv_ms,
+                                         const float *__restrict__ log_std, float ent_coef,
+                                         float vf_coef, const HeadOut &o) {
     __shared__ float loss[kLossK];
-    const int p = blockIdx.x * kBlock + threadIdx.x;
+    float sq = 0.f;
+    const int p = bx * kBlock + threadIdx.x;
     if (p < P) {
         float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
         int b = 0;
@@ -1019,37 +1031,54 @@ __global__ __launch_bounds__(kBlock) void ppo_head_finish_kernel(
         const float s = ((s0 + s1) + s2) + s3;
         if (p < kLossK) {
             loss[p] = s;
-        } else if (p < 13) {
-            o.g_b_act[p - 9] = s;
-        } else if (p == 13) {
-            o.g_b_val[0] = s;
         } else {
-            const int q = p - kHeadFixed;
-            if (q < hd) o.g_b_pi[q] = s;
-            else if (q < 2 * hd) o.g_b_vf[q - hd] = s;
-            else if (q < 6 * hd) o.g_w_act[q - 2 * hd] = s;
-            else o.g_w_val[q - 6 * hd] = s;
+            sq = s * s;
+            if (p < 13) {
+                o.g_b_act[p - 9] = s;
+            } else if (p == 13) {
+                o.g_b_val[0] = s;
+            } else {
+                const int q = p - kHeadFixed;
+                if (q < hd) o.g_b_pi[q] = s;
+                else if (q < 2 * hd) o.g_b_vf[q - hd] = s;
+                else if (q < 6 * hd) o.g_w_act[q - 2 * hd] = s;
+                else o.g_w_val[q - 6 * hd] = s;
+            }
         }
     }
-    if (blockIdx.x != 0) return;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        const float inv_m = 1.0f / (float)m;
-        const float pl = loss[0] * inv_m;
-        const float vl = loss[1] * inv_m;
-        float H = 0.f;
-        for (int j = 0; j < 4; ++j) H += 0.5f + kLogSqrt2Pi + log_std[j];
-        const float el = -H;
-        for (int j = 0; j < 4; ++j) o.g_log_std[j] = loss[4 + j] - ent_coef;
-        o.stats[0] = pl + ent_coef * el + vf_coef * vl;
-        o.stats[1] = pl;
-        o.stats[2] = vl;
-        o.stats[3] = el;
-        o.stats[4] = loss[2] * inv_m;
-        o.stats[5] = loss[3] * inv_m;
-        o.stats[6] = adv_ms[0];
-        o.stats[7] = adv_ms[1];
+    if (bx == 0) {
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            const float inv_m = 1.0f / (float)m;
+            const float pl = loss[0] * inv_m;
+            const float vl = loss[1] * inv_m;
+            float H = 0.f;
+            for (int j = 0; j < 4; ++j) H += 0.5f + kLogSqrt2Pi + log_std[j];
+            const float el = -H;
+            for (int j = 0; j < 4; ++j) {
+                const float g = loss[4 + j] - ent_coef;
+                o.g_log_std[j] = g;
+                sq += g * g;
+            }
+            o.stats[0] = pl + ent_coef * el + vf_coef * vl;
+            o.stats[1] = pl;
+            o.stats[2] = vl;
+            o.stats[3] = el;
+            o.stats[4] = loss[2] * inv_m;
+            o.stats[5] = loss[3] * inv_m;
+            o.stats[6] = adv_ms[0];
+            o.stats[7] = adv_ms[1];
+        }
     }
+    return sq;
+}
+
+__global__ __launch_bounds__(kBlock) void ppo_head_finish_kernel(
+    int nb, int P, int hd, int64_t m, const float *__restrict__ part,
+    const float *__restrict__ adv_ms, const float *__restrict__ log_std, float ent_coef,
+    float vf_coef, HeadOut o) {
+    (void)head_finish_part(blockIdx.x, nb, P, hd, m, part, adv_ms, log_std, ent_coef, vf_coef,
+                           o);
 }
 
 constexpr int kHeadGroups = 16;  // first-level row groups of the partial sums
@@ -1075,6 +1104,77 @@ __global__ __launch_bounds__(kBlock) void sumsq_kernel(int64_t n,
     float x[1] = {acc};
     block_sum<1>(x, sh);
     if (threadIdx.x == 0) part[blockIdx.x] = x[0];
+}
+
+// Split-K chunk sum: dst[g*size + i] = sum_c chunks[(g*count + c)*size + i],
+// fixed order (16 independent accumulators, then a fixed tree); returns the
+// square of the value written.
+__device__ inline float chunk_sum_part(int bx, int64_t groups, int count, int64_t size,
+                                       const float *__restrict__ chunks,
+                                       float *__restrict__ dst) {
+    const int64_t e = (int64_t)bx * kBlock + threadIdx.x;
+    if (e >= groups * size) return 0.f;
+    const int64_t g = e / size, i = e - g * size;
+    const float *__restrict__ src = chunks + g * count * size + i;
+    float a[16];
+#pragma unroll
+    for (int u = 0; u < 16; ++u) a[u] = 0.f;
+    int c = 0;
+    for (; c + 15 < count; c += 16) {
+#pragma unroll
+        for (int u = 0; u < 16; ++u) a[u] += src[(int64_t)(c + u) * size];
+    }
+    for (; c < count; ++c) a[0] += src[(int64_t)c * size];
+#pragma unroll
+    for (int w = 8; w > 0; w >>= 1)
+#pragma unroll
+        for (int u = 0; u < w; ++u) a[u] += a[u + w];
+    dst[e] = a[0];
+    return a[0] * a[0];
+}
+
+// The whole gradient finish of one fused minibatch step in ONE launch:
+// blocks [0, bh) the head's level-2 partial sums (+ loss stats), [bh, +bf)
+// the first layer's, the rest the split-K chunk sum of the layers above.
+// Every block also writes the sum of squares of the entries it produced, the
+// norm partials clip_adam_kernel consumes (replaces 2 finishes, the chunk
+// sum and the norm pass: 4 launches).
+struct FinishArgs {
+    int bh, bf, bc;
+    // head
+    int h_ng, h_P, h_hd;
+    int64_t h_m;
+    const float *h_part2, *h_adv_ms, *log_std;
+    float ent_coef, vf_coef;
+    HeadOut ho;
+    // first layer
+    int f_ng, f_n, f_K, f_nets;
+    const float *f_part2;
+    FirstBwdOut fo;
+    // split-K chunks
+    int64_t c_groups, c_size;
+    int c_count;
+    const float *chunks;
+    float *c_dst;
+    float *sq_part;
+};
+
+__global__ __launch_bounds__(kBlock) void grad_finish_kernel(FinishArgs a) {
+    __shared__ float sh[4];
+    int b = blockIdx.x;
+    float sq;
+    if (b < a.bh) {
+        sq = head_finish_part(b, a.h_ng, a.h_P, a.h_hd, a.h_m, a.h_part2, a.h_adv_ms, a.log_std,
+                              a.ent_coef, a.vf_coef, a.ho);
+    } else if ((b -= a.bh) < a.bf) {
+        sq = first_finish_part(b, a.f_ng, a.f_n, a.f_K, a.f_nets, a.f_part2, a.fo);
+    } else {
+        b -= a.bf;
+        sq = chunk_sum_part(b, a.c_groups, a.c_count, a.c_size, a.chunks, a.c_dst);
+    }
+    float x[1] = {sq};
+    block_sum<1>(x, sh);
+    if (threadIdx.x == 0) a.sq_part[blockIdx.x] = x[0];
 }
 
 __global__ __launch_bounds__(kBlock) void clip_adam_kernel(
@@ -1292,6 +1392,32 @@ int dr_ppo_loss(int64_t m, const float *mean, const float *log_std, const float 
     return check_launch("dr_ppo_loss finish");
 }
 
+static int launch_adam(int64_t n, float *params, float *grads, float *exp_avg,
+                       float *exp_avg_sq, double lr, double beta1, double beta2, double eps,
+                       float max_grad_norm, int64_t step, float *grad_norm_out,
+                       const float *sq_part, int nsq, hipStream_t st, const char *who) {
+    // torch.optim.Adam scalars, formed in double as torch does on the host.
+    const double b1 = beta1, b2 = beta2;
+    const double bc1 = 1.0 - std::pow(b1, (double)step);
+    const double bc2 = 1.0 - std::pow(b2, (double)step);
+    const float step_size = (float)(lr / bc1);
+    const float bc2_sqrt = (float)std::sqrt(bc2);
+    hipLaunchKernelGGL(clip_adam_kernel, dim3(nblocks_stream(n)), dim3(kBlock), 0, st, n,
+                       params, grads, exp_avg, exp_avg_sq, sq_part, nsq, max_grad_norm,
+                       (float)(1.0 - b1), (float)b2, (float)(1.0 - b2), step_size, bc2_sqrt,
+                       (float)eps, grad_norm_out);
+    return check_launch(who);
+}
+
+static int first_blocks(int64_t m);
+
+// Block counts of grad_finish_kernel's three segments.
+static void finish_blocks(const dr_grad_finish *f, int &bh, int &bf, int &bc) {
+    bh = f->head_workspace ? (int)((kHeadFixed + 7 * f->head_hd + kBlock - 1) / kBlock) : 0;
+    bf = f->first_workspace ? (int)((2 * (f->first_k + 1) * f->first_n + kBlock - 1) / kBlock) : 0;
+    bc = f->chunks ? (int)((f->chunk_groups * f->chunk_size + kBlock - 1) / kBlock) : 0;
+}
+
 size_t dr_adam_workspace_bytes(int64_t n) {
     return align_up(sizeof(float) * (size_t)nblocks_stream(n > 0 ? n : 1));
 }
@@ -1310,17 +1436,91 @@ int dr_clip_adam(int64_t n, float *params, float *grads, float *exp_avg, float *
     hipLaunchKernelGGL(sumsq_kernel, dim3(nb), dim3(kBlock), 0, st, n, grads, part);
     int rc = check_launch("dr_clip_adam norm");
     if (rc) return rc;
-    // torch.optim.Adam scalars, formed in double as torch does on the host.
-    const double b1 = beta1, b2 = beta2;
-    const double bc1 = 1.0 - std::pow(b1, (double)step);
-    const double bc2 = 1.0 - std::pow(b2, (double)step);
-    const float step_size = (float)(lr / bc1);
-    const float bc2_sqrt = (float)std::sqrt(bc2);
-    hipLaunchKernelGGL(clip_adam_kernel, dim3(nb), dim3(kBlock), 0, st, n, params, grads,
-                       exp_avg, exp_avg_sq, part, nb, max_grad_norm, (float)(1.0 - b1),
-                       (float)b2, (float)(1.0 - b2), step_size, bc2_sqrt, (float)eps,
-                       grad_norm_out);
-    return check_launch("dr_clip_adam");
+    return launch_adam(n, params, grads, exp_avg, exp_avg_sq, lr, beta1, beta2, eps,
+                       max_grad_norm, step, grad_norm_out, part, nb, st, "dr_clip_adam");
+}
+
+size_t dr_grad_finish_workspace_bytes(const dr_grad_finish *f) {
+    int bh, bf, bc;
+    finish_blocks(f, bh, bf, bc);
+    return align_up(sizeof(float) * (size_t)(bh + bf + bc > 0 ? bh + bf + bc : 1));
+}
+
+int dr_grad_finish_clip_adam(const dr_grad_finish *f, int64_t n, float *params, float *grads,
+                             float *exp_avg, float *exp_avg_sq, double lr, double beta1,
+                             double beta2, double eps, float max_grad_norm, int64_t step,
+                             float *grad_norm_out, void *workspace, size_t workspace_bytes,
+                             void *stream) {
+    if (!f || n < 1 || !params || !grads || !exp_avg || !exp_avg_sq || step < 1)
+        return fail0(DR_ERR_INVALID, "dr_grad_finish_clip_adam: bad arguments");
+    if (f->head_workspace && (f->head_m < 1 || f->head_hd < 4 || f->head_hd > 256 ||
+                              !f->log_std || !f->g_w_act || !f->g_b_act || !f->g_w_val ||
+                              !f->g_b_val || !f->g_b_pi || !f->g_b_vf || !f->g_log_std ||
+                              !f->stats))
+        return fail0(DR_ERR_INVALID, "dr_grad_finish_clip_adam: bad head arguments");
+    if (f->first_workspace && (f->first_m < 1 || f->first_n < 4 || f->first_n > 256 ||
+                               f->first_k < 1 || !f->g_w0 || !f->g_b0 || !f->g_w1 || !f->g_b1))
+        return fail0(DR_ERR_INVALID, "dr_grad_finish_clip_adam: bad first-layer arguments");
+    if (f->chunks && (f->chunk_groups < 1 || f->chunk_count < 1 || f->chunk_size < 1 ||
+                      !f->chunk_dst))
+        return fail0(DR_ERR_INVALID, "dr_grad_finish_clip_adam: bad chunk arguments");
+    if (!workspace || workspace_bytes < dr_grad_finish_workspace_bytes(f))
+        return fail0(DR_ERR_INVALID, "dr_grad_finish_clip_adam: workspace too small");
+    FinishArgs a{};
+    finish_blocks(f, a.bh, a.bf, a.bc);
+    if (a.bh + a.bf + a.bc < 1)
+        return fail0(DR_ERR_INVALID, "dr_grad_finish_clip_adam: nothing to finish");
+    if (f->head_workspace) {
+        const int64_t m = f->head_m, hd = f->head_hd;
+        const int nb = head_blocks(m);
+        const int P = kHeadFixed + 7 * (int)hd;
+        const int gsize = (nb + kHeadGroups - 1) / kHeadGroups;
+        // the head workspace layout of dr_ppo_head_loss_backward
+        const float *part = reinterpret_cast<const float *>(
+            static_cast<const char *>(f->head_workspace) +
+            align_up(sizeof(float) * 3 * grid_for(m)));
+        a.h_ng = (nb + gsize - 1) / gsize;
+        a.h_P = P;
+        a.h_hd = (int)hd;
+        a.h_m = m;
+        a.h_part2 = reinterpret_cast<const float *>(reinterpret_cast<const char *>(part) +
+                                                    align_up(sizeof(float) * (size_t)(nb * P + 2)));
+        a.h_adv_ms = part + (int64_t)nb * P;
+        a.log_std = f->log_std;
+        a.ent_coef = f->ent_coef;
+        a.vf_coef = f->vf_coef;
+        a.ho = HeadOut{f->g_w_act, f->g_b_act, f->g_w_val, f->g_b_val,
+                       f->g_b_pi,  f->g_b_vf,  f->g_log_std, f->stats};
+    }
+    if (f->first_workspace) {
+        const int nb = first_blocks(f->first_m);
+        const int P = 2 * (int)((f->first_k + 1) * f->first_n);
+        const int gsize = (nb + kHeadGroups - 1) / kHeadGroups;
+        a.f_ng = (nb + gsize - 1) / gsize;
+        a.f_n = (int)f->first_n;
+        a.f_K = (int)f->first_k;
+        a.f_nets = 2;
+        a.f_part2 = reinterpret_cast<const float *>(static_cast<const char *>(f->first_workspace) +
+                                                    align_up(sizeof(float) * (size_t)(nb * P)));
+        a.fo = FirstBwdOut{{f->g_w0, f->g_w1}, {f->g_b0, f->g_b1}};
+    }
+    if (f->chunks) {
+        a.c_groups = f->chunk_groups;
+        a.c_size = f->chunk_size;
+        a.c_count = (int)f->chunk_count;
+        a.chunks = f->chunks;
+        a.c_dst = f->chunk_dst;
+    }
+    float *part = static_cast<float *>(workspace);
+    a.sq_part = part;
+    const int nb = a.bh + a.bf + a.bc;
+    hipStream_t st = as_stream(stream);
+    hipLaunchKernelGGL(grad_finish_kernel, dim3(nb), dim3(kBlock), 0, st, a);
+    int rc = check_launch("dr_grad_finish_clip_adam finish");
+    if (rc) return rc;
+    return launch_adam(n, params, grads, exp_avg, exp_avg_sq, lr, beta1, beta2, eps,
+                       max_grad_norm, step, grad_norm_out, part, nb, st,
+                       "dr_grad_finish_clip_adam");
 }
 
 
@@ -1405,8 +1605,8 @@ int dr_ppo_head_loss_backward(int64_t m, int64_t hd, int preact, const float *h_
                               float vf_coef, int normalize_advantage, float *gz_pi,
                               float *gz_vf, float *g_w_act, float *g_b_act, float *g_w_val,
                               float *g_b_val, float *g_b_pi, float *g_b_vf, float *g_log_std,
-                              float *stats, void *workspace, size_t workspace_bytes,
-                              void *stream) {
+                              float *stats, int defer, void *workspace,
+                              size_t workspace_bytes, void *stream) {
     if (m < 1 || hd < 4 || hd > 256 || (hd & 3) || !h_pi || !h_vf || !w_act || !b_act ||
         !w_val || !b_val || !log_std || !actions || !aux || !gz_pi || !gz_vf || !g_w_act ||
         !g_b_act || !g_w_val || !g_b_val || !g_b_pi || !g_b_vf || !g_log_std || !stats)
@@ -1453,6 +1653,8 @@ int dr_ppo_head_loss_backward(int64_t m, int64_t hd, int preact, const float *h_
                        0, st, nb, P, gsize, part, part2);
     rc = check_launch("dr_ppo_head_loss_backward groups");
     if (rc) return rc;
+    // defer: the level-2 sum is left to dr_grad_finish_clip_adam
+    if (defer) return DR_OK;
     HeadOut o{g_w_act, g_b_act, g_w_val, g_b_val, g_b_pi, g_b_vf, g_log_std, stats};
     hipLaunchKernelGGL(ppo_head_finish_kernel, dim3((P + kBlock - 1) / kBlock), dim3(kBlock),
                        0, st, ng, P, (int)hd, m, part2, part + (int64_t)nb * P, log_std,
@@ -1483,7 +1685,7 @@ size_t dr_first_layer_backward2_workspace_bytes(int64_t m, int64_t k, int64_t n)
 static int launch_first_bwd(const char *who, int nets, int64_t m, int64_t k, int64_t n,
                             const FirstBwdIn &in, const float *x, const int32_t *rows,
                             const FirstBwdOut &o, void *workspace, size_t workspace_bytes,
-                            void *stream) {
+                            void *stream, int defer = 0) {
     if (m < 1 || !x || n < 4 || n > 256 || (n & 3))
         return fail0(DR_ERR_INVALID, std::string(who) + ": bad arguments");
     for (int j = 0; j < nets; ++j) {
@@ -1526,7 +1728,7 @@ static int launch_first_bwd(const char *who, int nets, int64_t m, int64_t k, int
     hipLaunchKernelGGL(colsum_groups_kernel, dim3((P + kBlock - 1) / kBlock, ng), dim3(kBlock),
                        0, st, nb, P, gsize, part, part2);
     rc = check_launch(who);
-    if (rc) return rc;
+    if (rc || defer) return rc;     // defer: level 2 in dr_grad_finish_clip_adam
     hipLaunchKernelGGL(first_layer_finish_kernel, dim3((P + kBlock - 1) / kBlock), dim3(kBlock),
                        0, st, ng, (int)n, (int)k, nets, part2, o);
     return check_launch(who);
@@ -1545,12 +1747,12 @@ int dr_first_layer_backward(int64_t m, int64_t k, int64_t n, const float *grad_h
 int dr_first_layer_backward2(int64_t m, int64_t k, int64_t n, const float *x,
                              const int32_t *rows, const float *grad_h0, const float *h0,
                              float *grad_w0, float *grad_b0, const float *grad_h1,
-                             const float *h1, float *grad_w1, float *grad_b1, void *workspace,
-                             size_t workspace_bytes, void *stream) {
+                             const float *h1, float *grad_w1, float *grad_b1, int defer,
+                             void *workspace, size_t workspace_bytes, void *stream) {
     const FirstBwdIn in{{grad_h0, grad_h1}, {h0, h1}};
     const FirstBwdOut o{{grad_w0, grad_w1}, {grad_b0, grad_b1}};
     return launch_first_bwd("dr_first_layer_backward2", 2, m, k, n, in, x, rows, o, workspace,
-                            workspace_bytes, stream);
+                            workspace_bytes, stream, defer);
 }
 
 }  // extern "C"

@@ -275,9 +275,10 @@ class FusedTrainStep:
         return self.pol.offsets["pi1.w"][0] if len(self.pol.net_arch) > 1 else \
             self.grad.numel()
 
-    def _wgrad2(self, gz, x, out):
+    def _wgrad2(self, gz, x, out, defer=False):
         """out (2, N, K) = gz[j]^T x[j] for both MLPs in one batched split-K
-        GEMM over 2C row chunks, then one fixed-order sum over the chunks."""
+        GEMM over 2C row chunks, then one fixed-order sum over the chunks
+        (left to the deferred finish with defer)."""
         _, M, N = gz.shape
         Kd = x.shape[2]
         C = self.C
@@ -287,11 +288,18 @@ class FusedTrainStep:
         ws = self._ws2[:2 * C * N * Kd].view(2 * C, N, Kd)
         torch.bmm(gz.reshape(2 * C, M // C, N).transpose(1, 2), x.reshape(2 * C, M // C, Kd),
                   out=ws)
-        torch.sum(ws.view(2, C, N, Kd), dim=1, out=out)
+        if not defer:
+            torch.sum(ws.view(2, C, N, Kd), dim=1, out=out)
+
+    def can_defer(self) -> bool:
+        """Whether step(defer_finish=True) covers every gradient entry (the
+        2-hidden-layer actor-critic: head, first-layer and split-K chunk
+        reductions are the whole flat gradient)."""
+        return len(self.pol.net_arch) == 2
 
     @torch.no_grad()
     def step(self, obs, actions, aux, head, rows=None, on_ready=None, adv_ready=False,
-             stats_out=None):
+             stats_out=None, defer_finish=False):
         """One PPO.train minibatch on the fused path: hidden forward
         (dr_linear_tanh for the first layer, hipBLASLt addmm + tanh above),
         dr_ppo_head_loss_backward (heads, loss, backward through the heads
@@ -308,11 +316,17 @@ class FusedTrainStep:
         stream, so a data-parallel caller can start that bucket's
         all-reduce while the first-layer backward still runs.
         `adv_ready` / `stats_out` are passed to the head (HeadLossBackward).
+        With defer_finish (can_defer(), no on_ready) the last reductions of
+        the head, the first layer and the split-K weight gradient are left
+        for ONE launch inside ClipAdam.step_finish(grad, self.finish): the
+        returned grad and stats are final only after that call.
         Returns (flat grad, stats (8))."""
         self._alloc_fused()
         pol, M = self.pol, (obs.shape[0] if rows is None else rows.numel())
         depth, top = len(pol.net_arch), len(pol.net_arch) - 1
         preact = depth >= 2                   # top tanh applied inside the head kernel
+        if defer_finish and (not self.can_defer() or on_ready is not None):
+            raise ValueError("defer_finish needs a 2-hidden-layer net and no on_ready")
         hs = hidden_forward(pol, obs, self._acts, self._acts2, rows, top_preact=preact)
         gz = self._gz2[top]
         stats = head(hs["pi"][top], hs["vf"][top], pol.p("action.w"), pol.p("action.b"),
@@ -321,7 +335,7 @@ class FusedTrainStep:
                      self.gview("action.b"), self.gview("value.w"), self.gview("value.b"),
                      self.gview(f"pi{top}.b"), self.gview(f"vf{top}.b"),
                      self.gview("log_std"), rows, preact=preact, adv_ready=adv_ready,
-                     stats_out=stats_out, **top_bias(pol, self._acts2))
+                     stats_out=stats_out, defer=defer_finish, **top_bias(pol, self._acts2))
         if depth == 1:                        # the head kernel gave grad_z of layer 0
             if rows is not None:
                 obs = obs.index_select(0, rows.long())
@@ -331,7 +345,7 @@ class FusedTrainStep:
         for k in reversed(range(1, depth)):
             x = self._acts2[k - 1]
             n_in = x.shape[2]
-            self._wgrad2(gz, x, pol.p2(k, "w", self.grad))
+            self._wgrad2(gz, x, pol.p2(k, "w", self.grad), defer=defer_finish)
             if k == 1 and on_ready is not None:
                 # all but the first layer's gradient is final from here on
                 on_ready(self.first_layer_end(), self.grad.numel())
@@ -341,13 +355,41 @@ class FusedTrainStep:
                 # first layer of both MLPs: tanh backward + weight/bias
                 # gradients fused, one launch
                 self._first(obs, g[0], x[0], self.gview("pi0.w"), self.gview("pi0.b"),
-                            g[1], x[1], self.gview("vf0.w"), self.gview("vf0.b"), rows)
+                            g[1], x[1], self.gview("vf0.w"), self.gview("vf0.b"), rows,
+                            defer=defer_finish)
             else:
                 gz = self._gz2[k - 1]
                 for j, pre in enumerate(("pi", "vf")):
                     self.K.tanh_backward(g[j], x[j], gz[j], self.gview(f"{pre}{k - 1}.b"),
                                          self.tanh_ws)
+        if defer_finish:
+            self._describe_finish(head, stats, M)
         return self.grad, stats
+
+    def _describe_finish(self, head, stats, M):
+        """Point self.finish (a GradFinish) at this step's deferred partials."""
+        pol = self.pol
+        if getattr(self, "finish", None) is None:
+            self.finish = self.K.GradFinish()
+        d = self.finish.desc
+        gp = lambda name: self.gview(name).data_ptr()          # noqa: E731
+        d.head_workspace, d.head_m, d.head_hd = head.ws.data_ptr(), head.m, head.hd
+        d.log_std = pol.log_std.data_ptr()
+        d.ent_coef, d.vf_coef = float(head.ent), float(head.vf)
+        d.g_w_act, d.g_b_act = gp("action.w"), gp("action.b")
+        d.g_w_val, d.g_b_val = gp("value.w"), gp("value.b")
+        d.g_b_pi, d.g_b_vf, d.g_log_std = gp("pi1.b"), gp("vf1.b"), gp("log_std")
+        d.stats = stats.data_ptr()
+        d.first_workspace = self._first.ws.data_ptr()
+        d.first_m, d.first_k, d.first_n = M, pol.obs_dim, pol.net_arch[0]
+        d.g_w0, d.g_b0, d.g_w1, d.g_b1 = gp("pi0.w"), gp("pi0.b"), gp("vf0.w"), gp("vf0.b")
+        out = pol.p2(1, "w", self.grad)                        # (2, N, K), contiguous
+        N, Kd = out.shape[1], out.shape[2]
+        if self.C > 1:
+            d.chunks, d.chunk_count = self._ws2.data_ptr(), self.C
+        else:                        # the GEMM wrote the sums already: a 1-chunk pass
+            d.chunks, d.chunk_count = out.data_ptr(), 1
+        d.chunk_groups, d.chunk_size, d.chunk_dst = 2, N * Kd, out.data_ptr()
 
     @torch.no_grad()
     def forward(self, obs):

@@ -26,6 +26,7 @@ SB3-parity choices (documented deviations in DESIGN.md):
 from __future__ import annotations
 
 import dataclasses
+import os
 import time
 
 import torch
@@ -124,6 +125,10 @@ class PPOTrainer:
         # fused MLP path (first-layer linear+tanh, heads+loss+head backward)
         # when the architecture fits the kernels; else forward/loss/backward
         self.use_fused = fusable(self.policy)
+        # single-GPU fused path: the step's last reductions + norm in one
+        # launch before Adam (DRONERL_DEFER_FINISH=0: separate launches)
+        self.defer_finish = (self.use_fused and self.fused.can_defer() and
+                             os.environ.get("DRONERL_DEFER_FINISH", "1") != "0")
         if self.use_fused:
             self.head = K.HeadLossBackward(M, cfg.net_arch[-1], dev, cfg.clip_range,
                                            cfg.ent_coef, cfg.vf_coef, cfg.normalize_advantage)
@@ -208,6 +213,14 @@ class PPOTrainer:
                         grad, st = self.fused.step(self.mb_obs, self.mb_act, self.mb_aux,
                                                    self.head, on_ready=bar.start, **kw)
                         bar.finish()
+                    elif self.defer_finish:
+                        # single GPU: the head / first-layer / split-K
+                        # reductions and the norm in one launch before Adam
+                        grad, st = self.fused.step(self.mb_obs, self.mb_act, self.mb_aux,
+                                                   self.head, defer_finish=True, **kw)
+                        self.opt.step_finish(grad, self.fused.finish)
+                        j += 1
+                        continue
                     else:
                         grad, st = self.fused.step(self.mb_obs, self.mb_act, self.mb_aux,
                                                    self.head, **kw)

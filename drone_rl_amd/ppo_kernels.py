@@ -7,6 +7,8 @@ follow stable-baselines3 PPO (reference call sites
 """
 from __future__ import annotations
 
+import ctypes
+
 import torch
 
 from . import _lib
@@ -149,6 +151,23 @@ class ClipAdam:
                               device=params.device)
         self.grad_norm = torch.zeros(1, dtype=torch.float32, device=params.device)
 
+    def step_finish(self, grads: torch.Tensor, finish: "GradFinish", lr=None):
+        """step() for a gradient whose last reductions were deferred
+        (dr_grad_finish_clip_adam: the finish and the norm in one launch,
+        then clip + Adam)."""
+        self.t += 1
+        L = _lib.lib()
+        f = ctypes.byref(finish.desc)
+        need = L.dr_grad_finish_workspace_bytes(f)
+        if finish.ws is None or finish.ws.numel() < need:
+            finish.ws = torch.empty(need, dtype=torch.uint8, device=self.p.device)
+        check(L.dr_grad_finish_clip_adam(
+            f, self.p.numel(), ptr(self.p), ptr(_f32(grads)), ptr(self.m), ptr(self.v),
+            float(self.lr if lr is None else lr), float(self.b1), float(self.b2),
+            float(self.eps), float(self.max_norm), self.t, ptr(self.grad_norm),
+            ptr(finish.ws), finish.ws.numel(), _s(self.p)))
+        return self.grad_norm
+
     def step(self, grads: torch.Tensor, lr=None):
         self.t += 1
         check(_lib.lib().dr_clip_adam(
@@ -242,14 +261,15 @@ class HeadLossBackward:
     def __call__(self, h_pi, h_vf, w_act, b_act, w_val, b_val, log_std, actions, aux,
                  gz_pi, gz_vf, g_w_act, g_b_act, g_w_val, g_b_val, g_b_pi, g_b_vf, g_log_std,
                  rows=None, preact=False, adv_ready=False, stats_out=None, zb_pi=None,
-                 zb_vf=None):
+                 zb_vf=None, defer=False):
         """actions (.,4) / aux (.,3) rows are read as [rows[r]] when rows
         (int32, m) is given, else the first m rows; with preact h_pi / h_vf
         are the top layer's pre-activations (tanh applied on load).  With
         adv_ready the advantage partials were written by gather_minibatch
         (adv_part=self.adv_part) for this minibatch; stats_out (8 f32)
         receives the stats instead of self.stats; zb_pi / zb_vf as
-        policy_heads."""
+        policy_heads.  With defer the gradient / stats outputs are written
+        later by ClipAdam.step_finish (GradFinish)."""
         assert h_pi.shape == (self.m, self.hd) and aux.shape[1] == 3
         assert rows is not None or aux.shape[0] == self.m
         stats = self.stats if stats_out is None else stats_out
@@ -262,7 +282,7 @@ class HeadLossBackward:
             ptr(_f32(actions)), ptr(_f32(aux)), _rows(rows), float(self.clip), float(self.ent),
             float(self.vf), norm, ptr(gz_pi), ptr(gz_vf), ptr(g_w_act), ptr(g_b_act),
             ptr(g_w_val), ptr(g_b_val), ptr(g_b_pi), ptr(g_b_vf), ptr(g_log_std),
-            ptr(stats), ptr(self.ws), self.ws.numel(), _s(h_pi)))
+            ptr(stats), int(bool(defer)), ptr(self.ws), self.ws.numel(), _s(h_pi)))
         return stats
 
 
@@ -293,11 +313,22 @@ class FirstLayerBackward2:
                               dtype=torch.uint8, device=device)
 
     def __call__(self, x, grad_h0, h0, grad_w0, grad_b0, grad_h1, h1, grad_w1, grad_b1,
-                 rows=None):
+                 rows=None, defer=False):
         for g, h in ((grad_h0, h0), (grad_h1, h1)):
             assert g.shape == (self.m, self.n) and h.shape == (self.m, self.n)
         assert x.shape[1] == self.k and (rows is not None or x.shape[0] == self.m)
         check(_lib.lib().dr_first_layer_backward2(
             self.m, self.k, self.n, ptr(_f32(x)), _rows(rows), ptr(_f32(grad_h0)), ptr(_f32(h0)),
             ptr(grad_w0), ptr(grad_b0), ptr(_f32(grad_h1)), ptr(_f32(h1)), ptr(grad_w1),
-            ptr(grad_b1), ptr(self.ws), self.ws.numel(), _s(x)))
+            ptr(grad_b1), int(bool(defer)), ptr(self.ws), self.ws.numel(), _s(x)))
+
+
+class GradFinish:
+    """The deferred reductions of one fused minibatch step (the
+    dr_grad_finish descriptor: head / first-layer partials, split-K chunks),
+    consumed by ClipAdam.step_finish.  `desc` holds raw device pointers: the
+    tensors it points into must stay alive (FusedTrainStep owns them)."""
+
+    def __init__(self):
+        self.desc = _lib.dr_grad_finish()
+        self.ws = None

@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define DR_ABI_VERSION 6
+#define DR_ABI_VERSION 7
 
 enum dr_status {
     DR_OK = 0,
@@ -285,15 +285,18 @@ int dr_first_layer_backward(int64_t m, int64_t k, int64_t n, const float *grad_h
 /* dr_first_layer_backward for both MLPs (net 0: grad_h0/h0 -> grad_w0/
    grad_b0, net 1: grad_h1/h1 -> grad_w1/grad_b1) over the same input x in
    one launch (plus one column-sum and one finish launch for both).
-   Bitwise the same results as two dr_first_layer_backward calls.
+   Bitwise the same results as two dr_first_layer_backward calls.  defer
+   != 0 leaves the last reduction (and the grad_w / grad_b writes) to
+   dr_grad_finish_clip_adam.
    `workspace` >= dr_first_layer_backward2_workspace_bytes(m, k, n). */
 size_t dr_first_layer_backward2_workspace_bytes(int64_t m, int64_t k, int64_t n);
 int dr_first_layer_backward2(int64_t m, int64_t k, int64_t n, const float *x,
                              const int32_t *rows, const float *grad_h0,
                              const float *h0, float *grad_w0, float *grad_b0,
                              const float *grad_h1, const float *h1,
-                             float *grad_w1, float *grad_b1, void *workspace,
-                             size_t workspace_bytes, void *stream);
+                             float *grad_w1, float *grad_b1, int defer,
+                             void *workspace, size_t workspace_bytes,
+                             void *stream);
 
 /* Policy heads for rollouts (ActorCriticPolicy.forward's action_net /
    value_net): mean (m,4) = h_pi W_act^T + b_act, value (m) = h_vf W_val^T +
@@ -322,7 +325,9 @@ int dr_policy_heads(int64_t m, int64_t hd, int preact, const float *h_pi,
    sums).  `preact`, zb_pi, zb_vf as dr_policy_heads (h_pi / h_vf
    pre-activations; grad_z uses tanh(z + zb)).  `workspace` >= dr_ppo_head_workspace_bytes(m, hd).
    normalize_advantage: 0 off, 1 on, 2 on with the advantage partials
-   already written to the head of `workspace` by dr_gather_minibatch. */
+   already written to the head of `workspace` by dr_gather_minibatch.
+   defer != 0: the gradient / stats outputs are NOT written here; the
+   reduced partials stay in `workspace` for dr_grad_finish_clip_adam. */
 size_t dr_ppo_head_workspace_bytes(int64_t m, int64_t hd);
 int dr_ppo_head_loss_backward(int64_t m, int64_t hd, int preact, const float *h_pi,
                               const float *h_vf, const float *zb_pi,
@@ -336,7 +341,7 @@ int dr_ppo_head_loss_backward(int64_t m, int64_t hd, int preact, const float *h_
                               float *gz_vf, float *g_w_act, float *g_b_act,
                               float *g_w_val, float *g_b_val, float *g_b_pi,
                               float *g_b_vf, float *g_log_std, float *stats,
-                              void *workspace, size_t workspace_bytes,
+                              int defer, void *workspace, size_t workspace_bytes,
                               void *stream);
 
 /* Fused PPO loss + gradient of the loss w.r.t. the policy head outputs
@@ -374,6 +379,42 @@ int dr_clip_adam(int64_t n, float *params, float *grads, float *exp_avg,
                  double eps, float max_grad_norm, int64_t step,
                  float *grad_norm_out, void *workspace,
                  size_t workspace_bytes, void *stream);
+
+/* The deferred reductions of one fused PPO.train minibatch step (the
+   single-GPU path): the level-2 partial sums left by
+   dr_ppo_head_loss_backward(..., defer = 1) and
+   dr_first_layer_backward2(..., defer = 1), and the split-K chunk sum of
+   the weight gradients above the first layer,
+     chunk_dst[g*chunk_size + i] = sum_c chunks[(g*chunk_count + c)*chunk_size + i].
+   Any of the three sources may be NULL (segment skipped); together they
+   must write every entry of the flat gradient passed to
+   dr_grad_finish_clip_adam, whose norm they also form. */
+typedef struct dr_grad_finish {
+    const void *head_workspace;      /* dr_ppo_head_loss_backward's */
+    int64_t head_m, head_hd;
+    const float *log_std;
+    float ent_coef, vf_coef;
+    float *g_w_act, *g_b_act, *g_w_val, *g_b_val, *g_b_pi, *g_b_vf, *g_log_std;
+    float *stats;                    /* (8), as dr_ppo_head_loss_backward */
+    const void *first_workspace;     /* dr_first_layer_backward2's */
+    int64_t first_m, first_k, first_n;
+    float *g_w0, *g_b0, *g_w1, *g_b1;
+    const float *chunks;
+    int64_t chunk_groups, chunk_count, chunk_size;
+    float *chunk_dst;
+} dr_grad_finish;
+
+/* dr_clip_adam fused with the deferred gradient finish: one launch reduces
+   every deferred partial into `grads` (and the loss stats) and forms the
+   norm partials, a second applies clip_grad_norm_ + Adam.  Two launches
+   instead of six.  `workspace` >= dr_grad_finish_workspace_bytes(f). */
+size_t dr_grad_finish_workspace_bytes(const dr_grad_finish *f);
+int dr_grad_finish_clip_adam(const dr_grad_finish *f, int64_t n, float *params,
+                             float *grads, float *exp_avg, float *exp_avg_sq,
+                             double lr, double beta1, double beta2,
+                             double eps, float max_grad_norm, int64_t step,
+                             float *grad_norm_out, void *workspace,
+                             size_t workspace_bytes, void *stream);
 
 #ifdef __cplusplus
 }

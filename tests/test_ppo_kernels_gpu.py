@@ -359,3 +359,46 @@ def test_gather_minibatch_equals_gathers_and_adv_pass(m, d):
     g1, s1 = g1.clone(), s1.clone()
     g2, s2 = fs.step(o, a, x, head)          # the head's own advantage pass
     assert torch.equal(g1, g2) and torch.equal(s1, s2)
+
+
+@pytest.mark.parametrize("arch,m", [((256, 256), 65536), ((64, 64), 1000), ((64, 128), 4096)])
+def test_deferred_finish_equals_separate_finishes(arch, m):
+    """FusedTrainStep.step(defer_finish=True) + ClipAdam.step_finish (the
+    head / first-layer / split-K reductions and the norm in one launch) ==
+    the separate finish launches + ClipAdam.step: stats bitwise, clipped
+    gradient and updated parameters to f32 summation-order noise; reruns
+    bitwise."""
+    from drone_rl_amd import ppo_kernels as K
+    from drone_rl_amd.policy import ActorCritic, FusedTrainStep
+    g = torch.Generator(device="cuda").manual_seed(m)
+    obs = torch.randn(m, 15, device="cuda", generator=g)
+    act = torch.rand(m, 4, device="cuda", generator=g) * 7.3575
+    aux = torch.randn(m, 3, device="cuda", generator=g)
+
+    def run(defer):
+        pol = ActorCritic(15, 4, arch, device="cuda", seed=9)
+        with torch.no_grad():
+            pol.flat.mul_(2.0)
+        fs = FusedTrainStep(pol, m)
+        head = K.HeadLossBackward(m, arch[-1], "cuda", 0.2, 0.01, 0.5, True)
+        opt = K.ClipAdam(pol.flat.data, 3e-4, eps=1e-5, max_grad_norm=0.5)
+        st = torch.full((8,), float("nan"), device="cuda")
+        outs = []
+        for _ in range(2):                     # two optimizer steps
+            grad, s = fs.step(obs, act, aux, head, stats_out=st, defer_finish=defer)
+            if defer:
+                norm = opt.step_finish(grad, fs.finish)
+            else:
+                norm = opt.step(grad)
+            outs.append((grad.clone(), s.clone(), norm.clone()))
+        torch.cuda.synchronize()
+        return outs, pol.flat.detach().clone()
+
+    (a, pa), (b, pb), (c, pc) = run(False), run(True), run(True)
+    for (ga, sa, na), (gb, sb, nb) in zip(a, b):
+        assert torch.equal(sa, sb)
+        assert abs(na.item() - nb.item()) <= 1e-5 * na.item()
+        scale = ga.abs().max().item()
+        assert (ga - gb).abs().max().item() <= 1e-5 * scale
+    assert (pa - pb).abs().max().item() <= 1e-5
+    assert torch.equal(pb, pc) and all(torch.equal(x[0], y[0]) for x, y in zip(b, c))
