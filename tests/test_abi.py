@@ -66,3 +66,32 @@ def test_oracle_not_linked_by_product():
             if f.endswith((".py", ".hip", ".h", ".cpp")):
                 txt = open(os.path.join(dirpath, f)).read()
                 assert not re.search(r"^\s*(from|import)\s+oracle", txt, re.M), f
+
+
+def test_v5_v7_entry_points_validate_without_gpu():
+    """The minibatch-gather, paired first-layer and deferred-finish entry
+    points reject bad arguments before any HIP call."""
+    from drone_rl_amd import _lib
+    L = _lib.lib()
+    bad = _lib.DR_ERR_INVALID
+    assert L.dr_gather_minibatch(4, None, 15, None, None, None, None, None, None, None,
+                                 None) == bad
+    assert L.dr_linear_tanh2(4, 15, 6, None, None, None, None, None, None, None, None,
+                             None) == bad
+    assert L.dr_first_layer_backward2(4, 15, 256, None, None, None, None, None, None, None,
+                                      None, None, None, 0, None, 0, None) == bad
+    f = _lib.dr_grad_finish()
+    assert L.dr_grad_finish_clip_adam(None, 10, None, None, None, None, 1e-3, 0.9, 0.999,
+                                      1e-5, 0.5, 1, None, None, 0, None) == bad
+    # an empty descriptor has nothing to finish
+    assert L.dr_grad_finish_workspace_bytes(ctypes.byref(f)) > 0
+    buf = (ctypes.c_float * 16)()
+    p = ctypes.cast(buf, ctypes.c_void_p)
+    assert L.dr_grad_finish_clip_adam(ctypes.byref(f), 10, p, p, p, p, 1e-3, 0.9, 0.999,
+                                      1e-5, 0.5, 1, None, p, 4096, None) == bad
+    assert "nothing to finish" in _lib.last_error()
+    # a head segment without its outputs is refused
+    f.head_workspace, f.head_m, f.head_hd = p, 64, 256
+    assert L.dr_grad_finish_clip_adam(ctypes.byref(f), 10, p, p, p, p, 1e-3, 0.9, 0.999,
+                                      1e-5, 0.5, 1, None, p, 4096, None) == bad
+    assert "head" in _lib.last_error()
