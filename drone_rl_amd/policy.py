@@ -301,7 +301,8 @@ class FusedTrainStep:
     def step(self, obs, actions, aux, head, rows=None, on_ready=None, adv_ready=False,
              stats_out=None, defer_finish=False):
         """One PPO.train minibatch on the fused path: hidden forward
-        (dr_linear_tanh for the first layer, hipBLASLt addmm + tanh above),
+        (dr_linear_tanh2 for both first layers, one batched bias-free GEMM
+        for both top layers -- addmm + tanh for any layer in between),
         dr_ppo_head_loss_backward (heads, loss, backward through the heads
         and top tanh, head / top-bias / log_std gradients), then for the
         layers above the first ONE batched split-K weight-gradient GEMM and
