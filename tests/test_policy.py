@@ -73,3 +73,21 @@ def test_splitk_linear_matches_autograd():
     assert torch.allclose(y, torch.nn.functional.linear(x2, w2, b2), atol=1e-5)
     for a, r in ((x.grad, x2.grad), (w.grad, w2.grad), (b.grad, b2.grad)):
         assert torch.allclose(a, r, rtol=1e-4, atol=1e-3)
+
+
+def test_tuned_gemm_table_covers_the_trainer_shapes():
+    """The committed TunableOp table (policy.use_tuned_gemms) is well formed,
+    validated for this image's stack, and holds the three batched GEMM shapes
+    of a 65,536-row 2x256 minibatch."""
+    import csv
+
+    from drone_rl_amd.policy import TUNED_GEMMS_CSV
+    rows = list(csv.reader(open(TUNED_GEMMS_CSV)))
+    val = {r[1]: r[2] for r in rows if r[0] == "Validator"}
+    assert val["GCN_ARCH_NAME"].startswith("gfx950")
+    assert val["PT_VERSION"] == torch.__version__.split("+")[0]
+    sols = {r[1]: (r[2], float(r[3])) for r in rows if r[0] != "Validator"}
+    for shape in ("tn_256_65536_256_B_2", "nn_256_65536_256_B_2", "nt_256_256_1024_B_128"):
+        key = next(k for k in sols if k.startswith(shape))
+        name, ms = sols[key]
+        assert name.startswith(("Gemm_Rocblas_", "Gemm_Hipblaslt_")) and 0.05 < ms < 0.5
