@@ -159,6 +159,22 @@ __device__ inline void m_sincos3(const S x[3], S s[3], S c[3]) {
             for (int k = 0; k < 3; ++k)
                 if (!sincos_fast_range(x[k])) sincos(x[k], &s[k], &c[k]);
         }
+    } else if constexpr (DR_SINCOS3 && sizeof(S) == 4) {
+        // f32 state mode: trig.h's sincosf_medium (f64 reduction, f32
+        // polynomials, <= 2 ulp); the library sincosf only out of range
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            const SinCosF t = sincosf_medium(x[k]);
+            s[k] = t.s;
+            c[k] = t.c;
+        }
+        const bool fast = (int)sincosf_fast_range(x[0]) & (int)sincosf_fast_range(x[1]) &
+                          (int)sincosf_fast_range(x[2]);
+        if (!fast) {
+#pragma unroll
+            for (int k = 0; k < 3; ++k)
+                if (!sincosf_fast_range(x[k])) sincosf(x[k], &s[k], &c[k]);
+        }
     } else {
 #pragma unroll
         for (int k = 0; k < 3; ++k) m_sincos(x[k], &s[k], &c[k]);

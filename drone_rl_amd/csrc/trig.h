@@ -77,4 +77,40 @@ DR_HD inline SinCos sincos_medium(double x) {
     return {s, c};
 }
 
+// ---------------------------------------------------------------------------
+// f32 state mode: the same shared-reduction scheme in single precision.  The
+// reduction runs in f64 (k = rint(x 2/pi), r = x - k pi/2 with a two-part
+// pi/2: the f32 argument is exact in f64 and r is far more accurate than one
+// f32 ulp for |x| < 2^19), the polynomials in f32 on [-pi/4, pi/4] (the
+// cephes sinf / cosf minimax sets).  <= 2 ulp from the correctly rounded
+// f32 sin / cos (tests/test_trig_host.py); replaces ~3x the instructions of
+// the library sincosf, whose large-argument path it keeps for |x| >= 2^19,
+// infinities and NaN.
+struct SinCosF {
+    float s, c;
+};
+
+DR_HD inline bool sincosf_fast_range(float x) { return fabsf(x) < 524288.0f; }
+
+// Precondition: sincosf_fast_range(x).
+DR_HD inline SinCosF sincosf_medium(float xf) {
+    const double kInvPio2 = 6.36619772367581382433e-01;
+    const double P1 = 1.57079632679489655800e+00;   // RN(pi/2)
+    const double P2 = 6.12323399573676603587e-17;   // RN(pi/2 - P1)
+    const double x = (double)xf;
+    const double k = rint(x * kInvPio2);
+    const float r = (float)fma(-k, P2, fma(-k, P1, x));
+    const float z = r * r;
+    float ps = fmaf(z, -1.9515295891e-4f, 8.3321608736e-3f);
+    ps = fmaf(z, ps, -1.6666654611e-1f);
+    const float sr = fmaf(r * z, ps, r);
+    float pc = fmaf(z, 2.443315711809948e-5f, -1.388731625493765e-3f);
+    pc = fmaf(z, pc, 4.166664568298827e-2f);
+    const float cr = fmaf(z * z, pc, fmaf(-0.5f, z, 1.0f));
+    const int q = (int)k & 3;
+    const float s0 = (q & 1) ? cr : sr;
+    const float c0 = (q & 1) ? sr : cr;
+    return {(q & 2) ? -s0 : s0, ((q + 1) & 2) ? -c0 : c0};
+}
+
 }  // namespace dr

@@ -10,3 +10,11 @@ extern "C" void trig_sincos(int64_t n, const double *x, double *s, double *c) {
         c[i] = t.c;
     }
 }
+
+extern "C" void trig_sincosf(int64_t n, const float *x, float *s, float *c) {
+    for (int64_t i = 0; i < n; ++i) {
+        const dr::SinCosF t = dr::sincosf_medium(x[i]);
+        s[i] = t.s;
+        c[i] = t.c;
+    }
+}
