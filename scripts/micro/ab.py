@@ -32,11 +32,12 @@ def main():
     ap.add_argument("--dtype", default="f64")
     ap.add_argument("--k", type=int, default=200)
     ap.add_argument("--reps", type=int, default=15)
+    ap.add_argument("--variant", type=int, default=0, help="0 gym, 2 moving")
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
     n, K = a.n, a.k
     acts = torch.rand(K, n, 4, device=dev) * 7.3575
-    obs = torch.zeros(n, 15, device=dev)
+    obs = torch.zeros(n, 18 if a.variant == 2 else 15, device=dev)
     rew = torch.zeros(n, device=dev)
     done = torch.zeros(n, dtype=torch.uint8, device=dev)
     runs = []
@@ -47,7 +48,7 @@ def main():
             k, _, val = kv.partition("=")
             os.environ[k] = val
         L = load(path)
-        cfg = _lib.dr_config(num_envs=n, variant=0, state_dtype=0 if a.dtype == "f64" else 1,
+        cfg = _lib.dr_config(num_envs=n, variant=a.variant, state_dtype=0 if a.dtype == "f64" else 1,
                              rng_mode=0, auto_reset=1, device=0, max_steps=0, seed=1,
                              env_id_offset=0, dt=0.0)
         h = ctypes.c_void_p()
