@@ -1272,13 +1272,18 @@ int dr_create(const dr_config *cfg_in, dr_handle **out) {
     // (scripts/micro/ab_sweep.sh, profiles/r01_env_launch_sweep.txt):
     // [0, 384k) 64 rows/wave; [384k, 1.5M) 32 + nontemporal state loads;
     // [1.5M, 3M) 32; [3M, ...) 64 + nontemporal state loads.
-    // The moving variant (9 more f32 arrays per env) has its own sweep:
-    // always 64 rows/wave, nontemporal state loads from 384k envs up.
+    // The moving variant (9 more f32 arrays per env) and the f32 state mode
+    // have sweeps of their own: moving always 64 rows/wave, nontemporal
+    // state loads from 384k envs up; f32 state 64 rows/wave with plain loads
+    // below 3M envs, 32 + nontemporal loads from 3M up.
     {
         const int64_t n = cfg.num_envs, k = (int64_t)1 << 10;
         if (cfg.variant == DR_VARIANT_MOVING) {
             h->rpw = 64;
             h->nt_loads = n >= 384 * k;
+        } else if (cfg.state_dtype == DR_STATE_F32) {
+            h->rpw = n >= 3072 * k ? 32 : 64;
+            h->nt_loads = n >= 3072 * k;
         } else {
             h->rpw = (n >= 384 * k && n < 3072 * k) ? 32 : 64;
             h->nt_loads = (n >= 384 * k && n < 1536 * k) || n >= 3072 * k;
