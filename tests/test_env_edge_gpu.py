@@ -114,9 +114,10 @@ def test_abi_argument_errors():
         b.step(torch.zeros(63, 4, device="cuda"))
 
 
-@pytest.mark.parametrize("variant,form", [("gym", ("32", "0")), ("gym", ("64", "1")),
-                                          ("gym", ("32", "1")), ("moving", ("64", "1"))])
-def test_launch_forms_equal_default_form(variant, form, monkeypatch):
+@pytest.mark.parametrize("variant,dtype,form", [
+    ("gym", "f64", ("32", "0")), ("gym", "f64", ("64", "1")), ("gym", "f64", ("32", "1")),
+    ("moving", "f64", ("64", "1")), ("gym", "f32", ("32", "1"))])
+def test_launch_forms_equal_default_form(variant, dtype, form, monkeypatch):
     """Every launch form (32 envs per wave, nontemporal state loads; chosen
     by batch size in dr_create) computes exactly what the 64-envs-per-wave
     plain-load form does, over 60 steps with auto-resets, terminal obs and
@@ -127,7 +128,8 @@ def test_launch_forms_equal_default_form(variant, form, monkeypatch):
     for rpw, ntl in (("64", "0"), form):
         monkeypatch.setenv("DRONERL_ROWS_PER_WAVE", rpw)
         monkeypatch.setenv("DRONERL_NT_LOADS", ntl)
-        b = DroneBatch(n, variant, seed=21, keep_terminal_obs=True, monitor=True)
+        b = DroneBatch(n, variant, seed=21, keep_terminal_obs=True, monitor=True,
+                       dtype=torch.float64 if dtype == "f64" else torch.float32)
         if variant == "moving":     # moving targets (eps > 0: nonzero amplitudes)
             b.set("eps", torch.full((n,), 0.3, dtype=torch.float64))
         b.reset()
