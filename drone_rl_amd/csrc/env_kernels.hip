@@ -92,6 +92,12 @@ __device__ unsigned long long g_stamps[16384 * 8];
 // 1: per-step outputs and state are written with nontemporal stores.  They
 // stream to HBM while the kernel runs instead of sitting dirty in L2 until
 // the end-of-kernel writeback (4-9 % faster from 65,536 to 4M envs).
+// waves per workgroup of env_step_kernel (A/B builds: 1, 2, 4)
+#ifndef DR_ENV_WPB
+#define DR_ENV_WPB 4
+#endif
+constexpr int kEnvBlock = 64 * DR_ENV_WPB;
+
 #ifndef DR_NT_STORES
 #define DR_NT_STORES 1
 #endif
@@ -492,7 +498,7 @@ __device__ inline void store_obs_wave(float *sh_block, const float ob[OD],
     // DS ops of one wave execute in order; the barrier only pins the
     // compiler's schedule (no workgroup s_barrier is emitted)
     __builtin_amdgcn_wave_barrier();
-    const int64_t wbase = (int64_t)blockIdx.x * (4 * RPW) + w * RPW;
+    const int64_t wbase = (int64_t)blockIdx.x * (DR_ENV_WPB * RPW) + w * RPW;
     const int64_t nvalid = (n - wbase) < RPW ? (n - wbase) : RPW;
     if (nvalid <= 0) return;
     float *dst = dst_all + wbase * OD;
@@ -532,12 +538,12 @@ __device__ inline void store_obs_block(float *sh, const float ob[OD],
 // load: a load there would make the waitcnt pass drain every outstanding
 // store of the wave (vmcnt counts stores too) before the reset could finish.
 template <typename S, int VAR, bool MON, int RPW, bool HU, bool NTL>
-__global__ __launch_bounds__(kBlock) void env_step_kernel(EnvView<S> v,
-                                                          StepIO io) {
+__global__ __launch_bounds__(kEnvBlock) void env_step_kernel(EnvView<S> v,
+                                                             StepIO io) {
     constexpr int OD = VAR == DR_VARIANT_GYM ? 15 : (VAR == DR_VARIANT_MOVING ? 18 : 12);
     constexpr bool GYMLIKE = VAR != DR_VARIANT_VECTORIZED;
-    __shared__ float4 sh4[kBlock * OD / 4];
-    const int64_t base = (int64_t)blockIdx.x * (4 * RPW);
+    __shared__ float4 sh4[kEnvBlock * OD / 4];
+    const int64_t base = (int64_t)blockIdx.x * (DR_ENV_WPB * RPW);
     const int lane_ = threadIdx.x & 63;
     // env of this lane; lanes >= RPW of a half-populated wave own none
     const int64_t i = lane_ < RPW ? base + (threadIdx.x >> 6) * RPW + lane_ : v.n;
@@ -1170,30 +1176,32 @@ int launch_step(dr_handle *h, const StepIO &io, hipStream_t st) {
     if (!launched && VAR != DR_VARIANT_VECTORIZED && v.host_u) {   // parity mode
         if (h->rpw == 32)
             hipLaunchKernelGGL((env_step_kernel<S, VAR, MON, 32, true, false>),
-                               dim3(grid_for(h->n, 128)), dim3(kBlock), 0, st, v, io);
+                               dim3(grid_for(h->n, DR_ENV_WPB * 32)), dim3(kEnvBlock), 0, st,
+                               v, io);
         else
             hipLaunchKernelGGL((env_step_kernel<S, VAR, MON, 64, true, false>),
-                               dim3(grid_for(h->n, 256)), dim3(kBlock), 0, st, v, io);
+                               dim3(grid_for(h->n, DR_ENV_WPB * 64)), dim3(kEnvBlock), 0, st,
+                               v, io);
         launched = true;
     }
     if (!launched) {
-        const dim3 g64(grid_for(h->n, 256)), g32(grid_for(h->n, 128));
+        const dim3 g64(grid_for(h->n, DR_ENV_WPB * 64)), g32(grid_for(h->n, DR_ENV_WPB * 32));
         switch (h->rpw * 2 + (int)h->nt_loads) {
             case 64:
                 hipLaunchKernelGGL((env_step_kernel<S, VAR, MON, 32, false, false>), g32,
-                                   dim3(kBlock), 0, st, v, io);
+                                   dim3(kEnvBlock), 0, st, v, io);
                 break;
             case 65:
                 hipLaunchKernelGGL((env_step_kernel<S, VAR, MON, 32, false, true>), g32,
-                                   dim3(kBlock), 0, st, v, io);
+                                   dim3(kEnvBlock), 0, st, v, io);
                 break;
             case 129:
                 hipLaunchKernelGGL((env_step_kernel<S, VAR, MON, 64, false, true>), g64,
-                                   dim3(kBlock), 0, st, v, io);
+                                   dim3(kEnvBlock), 0, st, v, io);
                 break;
             default:
                 hipLaunchKernelGGL((env_step_kernel<S, VAR, MON, 64, false, false>), g64,
-                                   dim3(kBlock), 0, st, v, io);
+                                   dim3(kEnvBlock), 0, st, v, io);
         }
     }
     hipError_t e = hipGetLastError();
