@@ -721,6 +721,9 @@ struct HeadArgs {
 // for the whole tile lane-parallel, and the per-row gradients come back by
 // v_readlane for the backward through the heads and the top tanh.
 constexpr int kHeadTile = 8;
+#ifndef DR_HEAD_DIAG
+#define DR_HEAD_DIAG 0
+#endif
 
 __global__ __launch_bounds__(kBlock) void ppo_head_kernel(HeadArgs a) {
     extern __shared__ float sh_part[];  // 4 * P
@@ -769,8 +772,13 @@ __global__ __launch_bounds__(kBlock) void ppo_head_kernel(HeadArgs a) {
         if (a.preact) {
 #pragma unroll
             for (int i = 0; i < kHeadTile; ++i) {
+#if DR_HEAD_DIAG == 1  // timing diagnostic only (wrong results): no top tanh
+                hp[i] = add4(hp[i], zbp);
+                hv[i] = add4(hv[i], zbv);
+#else
                 hp[i] = tanh4(add4(hp[i], zbp));
                 hv[i] = tanh4(add4(hv[i], zbv));
+#endif
             }
         }
         // this lane's row (lane < nr): its loss inputs, loaded while the dots run
@@ -867,7 +875,25 @@ __global__ __launch_bounds__(kBlock) void ppo_head_kernel(HeadArgs a) {
 // Replaces tanh_backward (write of grad_z) + the split-K weight-gradient
 // GEMM (re-read of grad_z).  Tiles of kFirstTile rows per wave, loads first.
 // Partial layout per block (P = (K+1) n): [k*n + c] = dW[c][k], [K*n + c] = db[c].
-constexpr int kFirstTile = 8;
+// A/B build knobs of first_layer_bwd_kernel: rows per tile, next-tile
+// prefetch, a two-slot LDS reduction, and the cap on blocks per net
+// (scripts/micro/ab_ppo_kern.sh).  4-row tiles fit 115 VGPRs and the two-slot
+// reduction 32 KB of LDS, so 4 waves per SIMD are resident: 59.0 -> 56.3 us
+// per minibatch against 8-row tiles / four slots (152 VGPRs, 64 KB, 2 waves);
+// the prefetch needs 203 VGPRs and is slower (64.7 us).
+#ifndef DR_FL_TILE
+#define DR_FL_TILE 4
+#endif
+constexpr int kFirstTile = DR_FL_TILE;
+#ifndef DR_FL_PF
+#define DR_FL_PF 0
+#endif
+#ifndef DR_FL_LDS2
+#define DR_FL_LDS2 1
+#endif
+#ifndef DR_FL_MAXB
+#define DR_FL_MAXB 512
+#endif
 
 // With gridDim.y == 2 the launch covers both MLPs (blockIdx.y = net); block
 // b of net j writes partial row b * gridDim.y + j, so one column-sum pass
@@ -896,11 +922,10 @@ __global__ __launch_bounds__(kBlock) void first_layer_bwd_kernel(int64_t m, int 
 #pragma unroll
         for (int q = 0; q < 4; ++q) aw[k][q] = 0.f;
     const int64_t nwaves = (int64_t)gridDim.x * 4;
-    for (int64_t tile = (int64_t)blockIdx.x * 4 + wid; tile * kFirstTile < m; tile += nwaves) {
+    // loads of one tile: grad_h and h rows (float4 per lane), x row k on lane k
+    auto load_tile = [=](int64_t tile, float4 *g, float4 *y, float *xv) {
         const int64_t r0 = tile * kFirstTile;
         const int nr = (int)min((int64_t)kFirstTile, m - r0);
-        float4 g[kFirstTile], y[kFirstTile];
-        float xv[kFirstTile];
 #pragma unroll
         for (int i = 0; i < kFirstTile; ++i) {
             const bool ok = act && i < nr;
@@ -909,6 +934,8 @@ __global__ __launch_bounds__(kBlock) void first_layer_bwd_kernel(int64_t m, int 
             const int64_t xr = rows ? (int64_t)rows[min(r0 + i, m - 1)] : r0 + i;
             xv[i] = (i < nr && lane < K) ? x[xr * K + lane] : 0.f;
         }
+    };
+    auto use_tile = [&](const float4 *g, const float4 *y, const float *xv) {
 #pragma unroll
         for (int i = 0; i < kFirstTile; ++i) {
             const float gq[4] = {g[i].x, g[i].y, g[i].z, g[i].w};
@@ -927,8 +954,66 @@ __global__ __launch_bounds__(kBlock) void first_layer_bwd_kernel(int64_t m, int 
                 for (int q = 0; q < 4; ++q) aw[k][q] = fmaf(gz[q], xk, aw[k][q]);
             }
         }
+    };
+#if DR_FL_PF
+    // software-pipelined: the next tile's loads are in flight while this
+    // tile's FMAs run (rows past the end load nothing and add zeros)
+    int64_t tile = (int64_t)blockIdx.x * 4 + wid;
+    if (tile * kFirstTile < m) {
+        float4 g[kFirstTile], y[kFirstTile];
+        float xv[kFirstTile];
+        load_tile(tile, g, y, xv);
+        for (; tile * kFirstTile < m; tile += nwaves) {
+            float4 g2[kFirstTile], y2[kFirstTile];
+            float xv2[kFirstTile];
+            const bool more = (tile + nwaves) * kFirstTile < m;
+            if (more) load_tile(tile + nwaves, g2, y2, xv2);
+            use_tile(g, y, xv);
+            if (more) {
+#pragma unroll
+                for (int i = 0; i < kFirstTile; ++i) {
+                    g[i] = g2[i];
+                    y[i] = y2[i];
+                    xv[i] = xv2[i];
+                }
+            }
+        }
     }
+#else
+    for (int64_t tile = (int64_t)blockIdx.x * 4 + wid; tile * kFirstTile < m; tile += nwaves) {
+        float4 g[kFirstTile], y[kFirstTile];
+        float xv[kFirstTile];
+        load_tile(tile, g, y, xv);
+        use_tile(g, y, xv);
+    }
+#endif
     const int P = (K + 1) * n;
+    float *__restrict__ out = part + ((int64_t)blockIdx.x * gridDim.y + blockIdx.y) * P;
+#if DR_FL_LDS2
+    // two slots of P: waves 2 / 3 park their partials, waves 0 / 1 fold theirs
+    // in, then the two slots are summed (half the LDS of four slots, so the
+    // LDS no longer caps the CU at two blocks)
+    float *slot = sh_fl + (wid & 1) * P;
+    if (wid >= 2 && act) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+#pragma unroll
+            for (int k = 0; k < K; ++k) slot[k * n + c0 + q] = aw[k][q];
+            slot[K * n + c0 + q] = ab[q];
+        }
+    }
+    __syncthreads();
+    if (wid < 2 && act) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+#pragma unroll
+            for (int k = 0; k < K; ++k) slot[k * n + c0 + q] = aw[k][q] + slot[k * n + c0 + q];
+            slot[K * n + c0 + q] = ab[q] + slot[K * n + c0 + q];
+        }
+    }
+    __syncthreads();
+    for (int p = threadIdx.x; p < P; p += kBlock) out[p] = sh_fl[p] + sh_fl[P + p];
+#else
     float *mine = sh_fl + wid * P;
     if (act) {
 #pragma unroll
@@ -939,9 +1024,9 @@ __global__ __launch_bounds__(kBlock) void first_layer_bwd_kernel(int64_t m, int 
         }
     }
     __syncthreads();
-    float *__restrict__ out = part + ((int64_t)blockIdx.x * gridDim.y + blockIdx.y) * P;
     for (int p = threadIdx.x; p < P; p += kBlock)
         out[p] = ((sh_fl[p] + sh_fl[P + p]) + sh_fl[2 * P + p]) + sh_fl[3 * P + p];
+#endif
 }
 
 // Sum of the grouped partials (ng rows of nets * P) scattered to d W (n,K)
@@ -1665,7 +1750,7 @@ int dr_ppo_head_loss_backward(int64_t m, int64_t hd, int preact, const float *h_
 
 static int first_blocks(int64_t m) {
     const int64_t b = (m + 4 * kFirstTile - 1) / (4 * kFirstTile);
-    return (int)(b < 512 ? b : 512);
+    return (int)(b < DR_FL_MAXB ? b : DR_FL_MAXB);
 }
 
 static size_t first_ws_bytes(int nets, int64_t m, int64_t k, int64_t n) {
@@ -1704,7 +1789,7 @@ static int launch_first_bwd(const char *who, int nets, int64_t m, int64_t k, int
     float *part2 = reinterpret_cast<float *>(static_cast<char *>(workspace) +
                                              align_up(sizeof(float) * (size_t)(nb * P)));
     hipStream_t st = as_stream(stream);
-    const size_t lds = sizeof(float) * 4 * P1;
+    const size_t lds = sizeof(float) * (DR_FL_LDS2 ? 2 : 4) * P1;
     switch (k) {
 #define DR_FL_CASE(K)                                                                      \
     case K:                                                                                \
