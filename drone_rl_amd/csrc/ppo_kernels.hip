@@ -720,12 +720,23 @@ struct HeadArgs {
 // the row results are parked one row per lane, the PPO row loss runs once
 // for the whole tile lane-parallel, and the per-row gradients come back by
 // v_readlane for the backward through the heads and the top tanh.
-constexpr int kHeadTile = 8;
+#ifndef DR_HEAD_TILE
+#define DR_HEAD_TILE 8
+#endif
+constexpr int kHeadTile = DR_HEAD_TILE;
 #ifndef DR_HEAD_DIAG
 #define DR_HEAD_DIAG 0
 #endif
 
-__global__ __launch_bounds__(kBlock) void ppo_head_kernel(HeadArgs a) {
+#ifndef DR_HEAD_WPE
+#define DR_HEAD_WPE 0
+#endif
+#if DR_HEAD_WPE
+#define DR_HEAD_ATTR __attribute__((amdgpu_waves_per_eu(DR_HEAD_WPE)))
+#else
+#define DR_HEAD_ATTR
+#endif
+__global__ __launch_bounds__(kBlock) DR_HEAD_ATTR void ppo_head_kernel(HeadArgs a) {
     extern __shared__ float sh_part[];  // 4 * P
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     const int hd = a.hd, c0 = 4 * lane;

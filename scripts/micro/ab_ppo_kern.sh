@@ -27,4 +27,5 @@ for v in "$@"; do
     echo "$v $k: $(python3 scripts/micro/dbstats.py gpurun_out/kp_$v/run_results.db $k | head -2 | tr '\n' ' ')"
   done
   grep -o '"updates_per_s": [0-9.]*' gpurun_out/kp_$v.log | head -1
+  rm -rf gpurun_out/kp_$v   # the SQLite traces (tens of MB) stay on the box
 done
