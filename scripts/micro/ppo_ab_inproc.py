@@ -17,7 +17,11 @@ trs = []
 for sp in specs:
     tr = PPOTrainer(PPOConfig(seed=0))
     k, _, v = sp.partition("=")
-    setattr(tr, k, eval(v))
+    obj = tr
+    *path, k = k.split(".")          # e.g. fused.overlap_wgrad=True
+    for a in path:
+        obj = getattr(obj, a)
+    setattr(obj, k, eval(v))
     tr.learn_step()
     trs.append((sp, tr))
 torch.cuda.synchronize()
