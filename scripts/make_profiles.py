@@ -5,6 +5,7 @@
   profiles/<round>_pmc_<tag>.json       per-dispatch counter averages
   profiles/traffic.json                 HBM bytes per env_step launch, read
                                         by bench.py for roofline.traffic
+  profiles/<round>_bench[_extra].json   the bench.py JSON lines of the session
 Usage: python scripts/make_profiles.py r01
 """
 import json
@@ -21,6 +22,9 @@ src = os.path.join(ROOT, "gpurun_out")
 ks = os.path.join(src, "prof", "run_kernel_stats.csv")
 if os.path.exists(ks):
     shutil.copy(ks, os.path.join(out, f"{rnd}_kernel_stats.csv"))
+for name in ("bench.json", "bench_extra.json"):       # the bench lines themselves
+    if os.path.exists(os.path.join(src, name)):
+        shutil.copy(os.path.join(src, name), os.path.join(out, f"{rnd}_{name}"))
 traffic = {}
 tpath = os.path.join(out, "traffic.json")
 if os.path.exists(tpath):
