@@ -151,6 +151,57 @@ class DroneBatch:
                                  ptr(self.term_obs), s), self.handle)
         return obs, rew, done
 
+    # -- host-buffer I/O (the drop-in surfaces) ------------------------------
+    def _host_buffers(self):
+        """Pinned host buffers the kernels read / write directly (zero-copy
+        over PCIe): a host-buffer step is one launch and one stream sync, no
+        separate H2D / D2H copies."""
+        hb = getattr(self, "_hb", None)
+        if hb is None:
+            n, od = self.num_envs, self.obs_dim
+            pin = dict(device="cpu", pin_memory=True)
+            f32 = dict(dtype=torch.float32, **pin)
+            hb = {"act": torch.zeros(n, 4, **f32), "obs": torch.zeros(n, od, **f32),
+                  "rew": torch.zeros(n, **f32),
+                  "done": torch.zeros(n, dtype=torch.uint8, **pin),
+                  "term": torch.zeros(n, od, **f32) if self.term_obs is not None else None,
+                  "ep_ret": torch.zeros(n, **f32) if self.monitor else None,
+                  "ep_len": torch.zeros(n, dtype=torch.int32, **pin) if self.monitor else None}
+            hb["np"] = {k: (v.numpy() if v is not None else None) for k, v in hb.items()}
+            self._hb = hb
+        return hb
+
+    def reset_host(self) -> np.ndarray:
+        """reset() into a pinned host buffer; returns a numpy view of it
+        (overwritten by the next host-buffer call: copy to keep)."""
+        hb = self._host_buffers()
+        check(self.L.dr_reset(self.handle, ptr(hb["obs"]), _stream(self.device)), self.handle)
+        torch.cuda.current_stream(self.device).synchronize()
+        return hb["np"]["obs"]
+
+    def step_host(self, actions):
+        """step() with host buffers: `actions` any (N,4)-shaped array-like;
+        the kernel reads them from, and writes obs / rew / done (and, when
+        kept, the terminal obs and VecMonitor outputs of done rows) to, pinned
+        host memory.  Returns the numpy views {"obs", "rew", "done", "term",
+        "ep_ret", "ep_len"}, valid until the next host-buffer call."""
+        hb = self._host_buffers()
+        a = np.asarray(actions, dtype=np.float32)
+        if a.size != self.num_envs * 4:
+            raise ValueError(f"actions must be ({self.num_envs}, 4), got {a.shape}")
+        np.copyto(hb["np"]["act"], a.reshape(self.num_envs, 4))
+        s = _stream(self.device)
+        if self.monitor:
+            check(self.L.dr_step_monitored(self.handle, ptr(hb["act"]), ptr(hb["obs"]),
+                                           ptr(hb["rew"]), ptr(hb["done"]), ptr(hb["term"]),
+                                           ptr(hb["ep_ret"]), ptr(hb["ep_len"]), s),
+                  self.handle)
+        else:
+            check(self.L.dr_step(self.handle, ptr(hb["act"]), ptr(hb["obs"]), ptr(hb["rew"]),
+                                 ptr(hb["done"]), ptr(hb["term"]), s), self.handle)
+        torch.cuda.current_stream(self.device).synchronize()
+        return hb["np"]
+
     # -- state access ------------------------------------------------------
     def get(self, field: str) -> torch.Tensor:
         fid = _lib.FIELDS[field]
@@ -292,15 +343,15 @@ class DroneGymEnv:
         self.arm_length, self.k_yaw, self.max_steps = ARM_LENGTH, K_YAW, MAX_STEPS
         self.observation_space = make_box(-np.inf, np.inf, (15,), np.float32)
         self.action_space = make_box(0, MOTOR_MAX, (4,), np.float32)
-        self._act = torch.zeros(1, 4, dtype=torch.float32, device=self._b.device)
 
     def reset(self):
-        return self._b.reset()[0].cpu().numpy()
+        return self._b.reset_host()[0].copy()
 
     def step(self, action):
-        self._act.copy_(torch.as_tensor(np.asarray(action, np.float32).reshape(1, 4)))
-        obs, rew, done = self._b.step(self._act)
-        return (obs[0].cpu().numpy(), float(rew[0].item()), bool(done[0].item()), {})
+        # one launch + one sync: the kernel reads the action from and writes
+        # its outputs to pinned host memory (DroneBatch.step_host)
+        o = self._b.step_host(np.asarray(action, np.float32).reshape(1, 4))
+        return (o["obs"][0].copy(), float(o["rew"][0]), bool(o["done"][0]), {})
 
     def _vec(self, f):
         return self._b.get(f)[0].cpu().numpy()

@@ -20,6 +20,7 @@ stable_baselines3 is importable the class derives from its VecEnv so
 """
 from __future__ import annotations
 
+import itertools
 import time
 
 import numpy as np
@@ -35,6 +36,9 @@ except Exception:  # noqa: BLE001 - SB3 absent (this image)
 
 _STATE = ("pos", "vel", "euler", "omega", "target")
 _SCALAR = {"current_step": int, "ep_num": int, "eps": float}
+
+
+_INFO_TEMPLATE = {"TimeLimit.truncated": False}
 
 
 class BatchedDroneVecEnv(_VecEnvBase):
@@ -69,28 +73,30 @@ class BatchedDroneVecEnv(_VecEnvBase):
 
     # ------------------------------------------------------------- stepping
     def reset(self):
-        return self.batch.reset().cpu().numpy().copy()
+        return self.batch.reset_host().copy()
 
     def step_async(self, actions):
-        a = torch.as_tensor(np.asarray(actions, dtype=np.float32).reshape(self.num_envs, 4))
-        self._actions = a.to(self.batch.device)
+        self._actions = actions
 
     def step_wait(self):
-        obs, rew, done = self.batch.step(self._actions)
-        obs_np = obs.cpu().numpy().copy()
-        rew_np = rew.cpu().numpy().copy()
-        done_np = done.cpu().numpy().astype(bool)
-        infos = [{"TimeLimit.truncated": False} for _ in range(self.num_envs)]
+        # one launch + one sync: the kernel reads the actions from and writes
+        # obs / rewards / dones / terminal rows to pinned host memory
+        o = self.batch.step_host(self._actions)
+        obs_np = o["obs"].copy()
+        rew_np = o["rew"].copy()
+        done_np = o["done"].astype(bool)
+        # one dict per env (SB3 semantics); copying a template is the
+        # cheapest way to build N of them in CPython
+        infos = list(map(dict.copy, itertools.repeat(_INFO_TEMPLATE, self.num_envs)))
         idx = np.nonzero(done_np)[0]
         if len(idx):
-            it = torch.as_tensor(idx, device=self.batch.device)
             if self.batch.auto_reset:
-                term = self.batch.term_obs[it].cpu().numpy()
+                term = o["term"][idx]
             else:
                 term = obs_np[idx]
             if self._monitor:
-                ret = self.batch.ep_ret[it].cpu().numpy()
-                ln = self.batch.ep_len[it].cpu().numpy()
+                ret = o["ep_ret"][idx]
+                ln = o["ep_len"][idx]
                 t = round(time.time() - self._t_start, 6)
             for j, i in enumerate(idx):
                 if self.batch.auto_reset:

@@ -12,7 +12,11 @@
  *
  * Conventions
  *  - Every data pointer passed to a compute entry point is DEVICE memory
- *    (e.g. a torch tensor's data_ptr on the handle's device).  The caller owns
+ *    (e.g. a torch tensor's data_ptr on the handle's device) or, for the
+ *    per-step I/O of dr_reset / dr_step / dr_step_monitored, pinned host
+ *    memory (hipHostMalloc): the kernel then reads the actions from and
+ *    writes its outputs to host memory over PCIe (zero-copy), so a
+ *    host-buffer step is one launch and one stream sync.  The caller owns
  *    all I/O buffers; the library owns the persistent env state (SoA).
  *  - `stream` is a hipStream_t passed as void* (NULL = the null stream).
  *    Compute entry points only enqueue work: they are asynchronous with

@@ -300,3 +300,37 @@ def test_single_env_facade(golden):
     np.testing.assert_allclose(env.pos, g["o_pos"][0], rtol=1e-12)
     assert env.mass == 1.0 and env.g == 9.81
     assert env.action_space.shape == (4,) and env.observation_space.shape == (15,)
+
+
+@pytest.mark.parametrize("n,monitor", [(1, True), (1000, True), (4096, False)])
+def test_step_host_is_bitwise_the_device_step(n, monitor):
+    """DroneBatch.step_host (the kernel reading actions from and writing its
+    outputs to pinned host memory, as DroneGymEnv / BatchedDroneVecEnv use it)
+    gives bitwise the results of the device-buffer step over many steps with
+    auto-resets, including terminal obs and VecMonitor outputs of done rows."""
+    from drone_rl_amd import DroneBatch, random_actions
+    kw = dict(seed=21, auto_reset=True, keep_terminal_obs=True, monitor=monitor)
+    bd, bh = DroneBatch(n, "gym", **kw), DroneBatch(n, "gym", **kw)
+    od = bd.reset().cpu().numpy()
+    oh = bh.reset_host().copy()
+    assert np.array_equal(od, oh)
+    ndone = 0
+    for t in range(60):
+        a = random_actions(n, seed=5, step=t)
+        obs, rew, done = bd.step(a)
+        h = bh.step_host(a.cpu().numpy())
+        d = done.cpu().numpy().astype(bool)
+        assert np.array_equal(obs.cpu().numpy(), h["obs"])
+        assert np.array_equal(rew.cpu().numpy(), h["rew"])
+        assert np.array_equal(d, h["done"].astype(bool))
+        ndone += int(d.sum())
+        if d.any():
+            assert np.array_equal(bd.term_obs.cpu().numpy()[d], h["term"][d])
+            if monitor:
+                assert np.array_equal(bd.ep_ret.cpu().numpy()[d], h["ep_ret"][d])
+                assert np.array_equal(bd.ep_len.cpu().numpy()[d], h["ep_len"][d])
+    assert ndone > 0
+    for f in ("pos", "vel", "euler", "omega", "target", "current_step", "ep_num"):
+        assert torch.equal(bd.get(f), bh.get(f)), f
+    with pytest.raises(ValueError):
+        bh.step_host(np.zeros((n + 1, 4), np.float32))
