@@ -203,21 +203,35 @@ class DroneBatch:
         return hb["np"]
 
     # -- state access ------------------------------------------------------
-    def get(self, field: str) -> torch.Tensor:
-        fid = _lib.FIELDS[field]
+    def _field_out(self, field: str, **where) -> torch.Tensor:
         n = self.num_envs
         if field in _VEC_FIELDS:
-            out = torch.empty(n, 3, dtype=torch.float64, device=self.device)
-        elif field == "eps":
-            out = torch.empty(n, dtype=torch.float64, device=self.device)
-        elif field == "ep_return":
-            out = torch.empty(n, dtype=torch.float32, device=self.device)
-        elif field == "motion":
-            out = torch.empty(n, 9, dtype=torch.float32, device=self.device)
-        else:
-            out = torch.empty(n, dtype=torch.int32, device=self.device)
+            return torch.empty(n, 3, dtype=torch.float64, **where)
+        if field == "eps":
+            return torch.empty(n, dtype=torch.float64, **where)
+        if field == "ep_return":
+            return torch.empty(n, dtype=torch.float32, **where)
+        if field == "motion":
+            return torch.empty(n, 9, dtype=torch.float32, **where)
+        return torch.empty(n, dtype=torch.int32, **where)
+
+    def get(self, field: str) -> torch.Tensor:
+        fid = _lib.FIELDS[field]
+        out = self._field_out(field, device=self.device)
         check(self.L.dr_get_state(self.handle, fid, ptr(out), _stream(self.device)), self.handle)
         return out
+
+    def get_host(self, field: str) -> np.ndarray:
+        """get(field) as a fresh numpy array: the field kernel writes into a
+        pinned host buffer (one launch + one sync, no D2H copy)."""
+        fid = _lib.FIELDS[field]
+        bufs = self.__dict__.setdefault("_field_host", {})
+        out = bufs.get(field)
+        if out is None:
+            out = bufs[field] = self._field_out(field, device="cpu", pin_memory=True)
+        check(self.L.dr_get_state(self.handle, fid, ptr(out), _stream(self.device)), self.handle)
+        torch.cuda.current_stream(self.device).synchronize()
+        return out.numpy().copy()
 
     def gather(self, field: str, env_ids: torch.Tensor, out: torch.Tensor | None = None):
         """`get(field)` for the envs in env_ids (int32 device tensor), into
@@ -354,16 +368,16 @@ class DroneGymEnv:
         return (o["obs"][0].copy(), float(o["rew"][0]), bool(o["done"][0]), {})
 
     def _vec(self, f):
-        return self._b.get(f)[0].cpu().numpy()
+        return self._b.get_host(f)[0]
 
     pos = property(lambda self: self._vec("pos"))
     vel = property(lambda self: self._vec("vel"))
     euler = property(lambda self: self._vec("euler"))
     omega = property(lambda self: self._vec("omega"))
     target = property(lambda self: self._vec("target"))
-    current_step = property(lambda self: int(self._b.get("current_step")[0].item()))
-    ep_num = property(lambda self: int(self._b.get("ep_num")[0].item()))
-    eps = property(lambda self: float(self._b.get("eps")[0].item()))
+    current_step = property(lambda self: int(self._b.get_host("current_step")[0]))
+    ep_num = property(lambda self: int(self._b.get_host("ep_num")[0]))
+    eps = property(lambda self: float(self._b.get_host("eps")[0]))
 
     def render(self, mode="human", close=False):
         raise NotImplementedError("rendering is out of scope (SURVEY.md 2 #11)")

@@ -120,10 +120,10 @@ class BatchedDroneVecEnv(_VecEnvBase):
     def get_attr(self, attr_name, indices=None):
         idx = self._indices(indices)
         if attr_name in _STATE:
-            v = self.batch.get(attr_name).cpu().numpy()
+            v = self.batch.get_host(attr_name)
             return [v[i].copy() for i in idx]
         if attr_name in _SCALAR:
-            v = self.batch.get(attr_name).cpu().numpy()
+            v = self.batch.get_host(attr_name)
             return [_SCALAR[attr_name](v[i]) for i in idx]
         if attr_name in self._consts:
             return [self._consts[attr_name] for _ in idx]

@@ -55,6 +55,8 @@ def main():
     ve1.reset()
     s = timed(lambda: ve1.step(act1[None]), 2000)
     out["vecenv_1_host"] = {"us_per_step": round(s * 1e6, 2), "env_steps_per_s": round(1 / s, 1)}
+    s = timed(lambda: ve1.get_attr("pos"), 2000)
+    out["vecenv_1_get_attr_pos"] = {"us_per_call": round(s * 1e6, 2)}
     ve1.close()
 
     ve = BatchedDroneVecEnv(a.n, seed=1)

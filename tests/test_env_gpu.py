@@ -334,3 +334,17 @@ def test_step_host_is_bitwise_the_device_step(n, monitor):
         assert torch.equal(bd.get(f), bh.get(f)), f
     with pytest.raises(ValueError):
         bh.step_host(np.zeros((n + 1, 4), np.float32))
+
+
+def test_get_host_equals_get():
+    """get_host (field kernel writing pinned host memory) == get().cpu()."""
+    from drone_rl_amd import DroneBatch, random_actions
+    b = DroneBatch(777, "gym", seed=8, monitor=True)
+    b.reset()
+    for t in range(40):
+        b.step(random_actions(777, seed=2, step=t))
+    for f in ("pos", "vel", "euler", "omega", "target", "current_step", "ep_num", "eps",
+              "ep_return"):
+        h = b.get_host(f)
+        assert np.array_equal(h, b.get(f).cpu().numpy()), f
+        assert not np.shares_memory(h, b._field_host[f].numpy()), f   # a fresh array
