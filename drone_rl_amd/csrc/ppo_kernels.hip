@@ -81,11 +81,14 @@ __device__ inline void box_muller(uint32_t a, uint32_t b, float &z0, float &z1) 
 // (torch: -((a-mu)^2)/(2 var) - log(std) - log(sqrt(2 pi))); clip for env.
 __global__ __launch_bounds__(kBlock) void policy_sample_kernel(
     int64_t n, const float4 *__restrict__ mean, const float *__restrict__ log_std,
-    uint32_t k0, uint32_t k1, uint64_t counter, float lo, float hi,
-    float4 *__restrict__ a_raw, float4 *__restrict__ a_clip,
+    uint32_t k0, uint32_t k1, uint64_t counter, const uint64_t *__restrict__ counter_base,
+    float lo, float hi, float4 *__restrict__ a_raw, float4 *__restrict__ a_clip,
     float *__restrict__ logp) {
     const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     if (i >= n) return;
+    // device-resident counter base: a captured rollout graph replays with
+    // fresh noise each PPO iteration (the base advances outside the graph)
+    if (counter_base) counter += *counter_base;
     const float ls[4] = {log_std[0], log_std[1], log_std[2], log_std[3]};
     const float4 mu = mean[i];
     const u32x4 r = philox4x32_10(
@@ -1343,10 +1346,31 @@ int dr_policy_sample(int64_t n, const float *mean, const float *log_std, uint64_
     if (n == 0) return DR_OK;
     hipLaunchKernelGGL(policy_sample_kernel, dim3(grid_for(n)), dim3(kBlock), 0,
                        as_stream(stream), n, reinterpret_cast<const float4 *>(mean), log_std,
-                       (uint32_t)seed, (uint32_t)(seed >> 32), counter, lo, hi,
+                       (uint32_t)seed, (uint32_t)(seed >> 32), counter,
+                       (const uint64_t *)nullptr, lo, hi,
                        reinterpret_cast<float4 *>(actions_raw),
                        reinterpret_cast<float4 *>(actions_clipped), logp);
     return check_launch("dr_policy_sample");
+}
+
+int dr_policy_sample_dev(int64_t n, const float *mean, const float *log_std, uint64_t seed,
+                         const uint64_t *counter_base, uint64_t counter_offset, float lo,
+                         float hi, float *actions_raw, float *actions_clipped, float *logp,
+                         void *stream) {
+    if (n < 0 || !mean || !log_std || !counter_base)
+        return fail0(DR_ERR_INVALID, "dr_policy_sample_dev: bad arguments");
+    if ((((uintptr_t)mean) | ((uintptr_t)actions_raw) | ((uintptr_t)actions_clipped)) & 15)
+        return fail0(DR_ERR_INVALID,
+                     "dr_policy_sample_dev: (n,4) buffers must be 16-byte aligned");
+    if (((uintptr_t)counter_base) & 7)
+        return fail0(DR_ERR_INVALID, "dr_policy_sample_dev: counter_base must be 8-byte aligned");
+    if (n == 0) return DR_OK;
+    hipLaunchKernelGGL(policy_sample_kernel, dim3(grid_for(n)), dim3(kBlock), 0,
+                       as_stream(stream), n, reinterpret_cast<const float4 *>(mean), log_std,
+                       (uint32_t)seed, (uint32_t)(seed >> 32), counter_offset, counter_base, lo,
+                       hi, reinterpret_cast<float4 *>(actions_raw),
+                       reinterpret_cast<float4 *>(actions_clipped), logp);
+    return check_launch("dr_policy_sample_dev");
 }
 
 static size_t align_up(size_t x) { return (x + 255) & ~(size_t)255; }

@@ -136,6 +136,11 @@ class PPOTrainer:
         self.num_updates = 0
         self.num_timesteps = 0
         self._rolled = False
+        # rollout loop captured into a hipGraph after one eager warm-up
+        # iteration (DRONERL_ROLLOUT_GRAPH=0: always eager)
+        self.rollout_graph = os.environ.get("DRONERL_ROLLOUT_GRAPH", "1") != "0"
+        self._rgraph, self._rwarm = None, False
+        self._ctr = torch.zeros(1, dtype=torch.int64, device=dev)
         # optional TrajectoryTensorboardCallback equivalent (trajectory.py)
         self.trajectory = None
         self.env.reset(self.obs[0])
@@ -157,22 +162,29 @@ class PPOTrainer:
             self.obs[0].copy_(self.obs[T])
         self.dones[0].copy_(self.dones[T])          # episode_starts of step 0
         self._rolled = True
-        ls = self.policy.log_std
         fwd = self.infer if self.use_fused else self.policy
-        for t in range(T):
-            mean, value = fwd(self.obs[t])
-            self.values[t].copy_(value)
-            K.policy_sample(mean, ls, seed=cfg.seed * 7919 + self.rank,
-                            counter=self.num_updates * T + t, lo=0.0, hi=MOTOR_MAX,
-                            actions_raw=self.actions[t], actions_clipped=self.act_env,
-                            logp=self.logp[t])
-            # VecMonitor outputs land in this step's slice (done rows only)
-            self.env.ep_ret = self.ep_ret[t]
-            self.env.ep_len = self.ep_len[t]
-            self.env.step(self.act_env, obs_out=self.obs[t + 1], rew_out=self.rewards[t],
-                          done_out=self.dones[t + 1])
-            if self.trajectory is not None:
-                self.trajectory.on_step(self.dones[t + 1])
+        # noise counter of step t = num_updates * T + t, its base on the device
+        self._ctr.fill_(self.num_updates * T)
+        if not (self.rollout_graph and self.trajectory is None):
+            self._rollout_steps(fwd)
+        elif self._rgraph is not None:
+            self._rgraph.replay()
+        elif not self._rwarm:
+            self._rollout_steps(fwd)     # eager once: lazy library init
+            self._rwarm = True
+        else:
+            # the T-step loop (policy forward, sample, env step) captured once
+            # and replayed every iteration: one launch instead of ~8T from
+            # Python (matters at few envs: the reference's 1-env config)
+            cur = torch.cuda.current_stream(self.device)
+            cs = torch.cuda.Stream(self.device)
+            cs.wait_stream(cur)
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.stream(cs), torch.cuda.graph(g, stream=cs):
+                self._rollout_steps(fwd)
+            cur.wait_stream(cs)
+            g.replay()
+            self._rgraph = g
         if self.trajectory is not None:
             self.trajectory.flush()
         _, last_values = fwd(self.obs[T])
@@ -181,6 +193,23 @@ class PPOTrainer:
         torch.stack([self.logp.reshape(-1), self.adv.reshape(-1), self.ret.reshape(-1)],
                     dim=1, out=self.aux)
         self.num_timesteps += T * cfg.num_envs * self.world
+
+    def _rollout_steps(self, fwd):
+        T, ls = self.cfg.n_steps, self.policy.log_std
+        for t in range(T):
+            mean, value = fwd(self.obs[t])
+            self.values[t].copy_(value)
+            K.policy_sample_dev(mean, ls, seed=self.cfg.seed * 7919 + self.rank,
+                                counter_base=self._ctr, counter_offset=t, lo=0.0,
+                                hi=MOTOR_MAX, actions_raw=self.actions[t],
+                                actions_clipped=self.act_env, logp=self.logp[t])
+            # VecMonitor outputs land in this step's slice (done rows only)
+            self.env.ep_ret = self.ep_ret[t]
+            self.env.ep_len = self.ep_len[t]
+            self.env.step(self.act_env, obs_out=self.obs[t + 1], rew_out=self.rewards[t],
+                          done_out=self.dones[t + 1])
+            if self.trajectory is not None:
+                self.trajectory.on_step(self.dones[t + 1])
 
     @torch.no_grad()
     def train(self):

@@ -51,6 +51,20 @@ def policy_sample(mean, log_std, seed, counter, lo, hi, actions_raw=None,
     return actions_raw, actions_clipped, logp
 
 
+def policy_sample_dev(mean, log_std, seed, counter_base, counter_offset, lo, hi,
+                      actions_raw=None, actions_clipped=None, logp=None):
+    """policy_sample with counter = counter_base[0] + counter_offset, the
+    base an int64 device tensor (read by the kernel: graph-capturable)."""
+    n = mean.shape[0]
+    assert counter_base.dtype == torch.int64 and counter_base.device == mean.device
+    check(_lib.lib().dr_policy_sample_dev(n, ptr(_f32(mean)), ptr(_f32(log_std)),
+                                          seed & (2**64 - 1), ptr(counter_base),
+                                          counter_offset & (2**64 - 1), float(lo), float(hi),
+                                          ptr(actions_raw), ptr(actions_clipped), ptr(logp),
+                                          _s(mean)))
+    return actions_raw, actions_clipped, logp
+
+
 class Permuter:
     """Uniform random permutations of [0, n) (RolloutBuffer.get)."""
 

@@ -39,7 +39,7 @@
 extern "C" {
 #endif
 
-#define DR_ABI_VERSION 7
+#define DR_ABI_VERSION 8
 
 enum dr_status {
     DR_OK = 0,
@@ -219,6 +219,17 @@ int dr_policy_sample(int64_t n, const float *mean, const float *log_std,
                      uint64_t seed, uint64_t counter, float lo, float hi,
                      float *actions_raw, float *actions_clipped, float *logp,
                      void *stream);
+
+/* dr_policy_sample with counter = *counter_base + counter_offset, the base
+   read on the device (8-byte aligned u64): a rollout loop captured once
+   into a hipGraph draws fresh noise on every replay when the caller
+   advances the base between replays.  Bitwise dr_policy_sample for the same
+   counter.  (ABI v8.) */
+int dr_policy_sample_dev(int64_t n, const float *mean, const float *log_std,
+                         uint64_t seed, const uint64_t *counter_base,
+                         uint64_t counter_offset, float lo, float hi,
+                         float *actions_raw, float *actions_clipped, float *logp,
+                         void *stream);
 
 /* Uniform random permutation of [0,n) (RolloutBuffer.get's
    np.random.permutation): sort-by-random-key with a hipCUB radix sort.

@@ -161,3 +161,31 @@ def test_tuned_gemms_load_and_are_deterministic():
     assert (g1 - g3).abs().max().item() <= 1e-4 * scale
     np.testing.assert_allclose(s1.cpu(), s3.cpu(), rtol=1e-4, atol=1e-6)
     tr.close()
+
+
+@pytest.mark.parametrize("cfg", ["small", "sb3_1env"])
+def test_rollout_graph_is_bitwise_eager(cfg):
+    """The rollout loop captured into a hipGraph (after one eager warm-up
+    iteration; the policy-noise counter base lives on the device) replays to
+    bitwise the eager rollouts and updates over several PPO iterations."""
+    from drone_rl_amd.ppo import PPOConfig, PPOTrainer
+
+    def make(graph):
+        if cfg == "small":
+            tr = _trainer()
+        else:
+            tr = PPOTrainer(PPOConfig.sb3_defaults(n_steps=128, seed=3))
+        tr.rollout_graph = graph
+        return tr
+
+    a, b = make(False), make(True)
+    for _ in range(4):
+        a.learn_step()
+        b.learn_step()
+        for name in ("obs", "actions", "logp", "values", "rewards", "dones", "adv"):
+            assert torch.equal(getattr(a, name), getattr(b, name)), name
+    assert b._rgraph is not None
+    assert torch.equal(a.policy.flat.detach(), b.policy.flat.detach())
+    assert torch.equal(a.env.get("ep_num"), b.env.get("ep_num"))
+    a.close()
+    b.close()
