@@ -148,7 +148,10 @@ def time_ppo(args, rank, world, device):
     cfg = PPOConfig(num_envs=args.envs, n_steps=args.ppo_steps, batch_size=args.envs,
                     n_epochs=args.ppo_epochs, state_dtype=args.state_dtype, seed=0)
     tr = PPOTrainer(cfg, device=device, rank=rank, world_size=world)
-    tr.learn_step()                                   # warm-up iteration
+    # warm-up: the eager iteration, then the one that captures the rollout
+    # graph (replayed by every timed iteration)
+    tr.learn_step()
+    tr.learn_step()
     torch.cuda.synchronize(device)
     if world > 1:
         dist.barrier()
