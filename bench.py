@@ -48,6 +48,8 @@ def parse():
     ap.add_argument("--graph-warm-replays", type=int, default=1,
                     help="untimed replays of the captured step graph before the timed one")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-companion", action="store_true",
+                    help="skip the 4,194,304-env companion measurement")
     ap.add_argument("--cpu-seconds", type=float, default=1.5)
     ap.add_argument("--ppo-updates", type=int, default=3,
                     help="timed PPO iterations for configs[2] (0 = skip)")
@@ -257,6 +259,27 @@ def main():
                      "avg_launch_us": round(per_launch_s * 1e6, 3)},
         "mean_ep_num": round(ep, 2),
     }
+    if world == 1 and not args.no_companion:
+        # cache-busting companion of the headline: the same
+        # kernel at 4,194,304 envs, where the step is HBM-bound, not launch-
+        # and latency-bound as at 65,536 (not the bench value)
+        n4, k4 = 1 << 22, 200
+        el4, gm4, _ = time_env(args, args.state_dtype, n4, 0, 1, device, k4, 20)
+        pl4 = gm4 / 1e3 / k4
+        ach4 = n4 * bpe / pl4 / 1e9
+        tr4 = None
+        try:
+            tr4 = json.load(open(args.traffic_json))[f"{args.state_dtype}_{n4}"][
+                "hbm_bytes_per_launch"]
+        except (OSError, ValueError, KeyError):
+            pass
+        out["companion"] = {"envs": n4, "steps": k4,
+                            "env_steps_per_s": round(n4 * k4 / el4, 1),
+                            "avg_launch_us": round(pl4 * 1e6, 3),
+                            "roofline": {"bound": "hbm", "achieved": round(ach4, 1),
+                                         "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                                         "frac": round(ach4 / HBM_PEAK_GBS, 4),
+                                         "traffic": tr4}}
     if cpu is not None:
         out["cpu_baseline"] = cpu
     if args.ppo_updates > 0:

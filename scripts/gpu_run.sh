@@ -29,6 +29,6 @@ fi
 if [[ $WHAT == all || $WHAT == prof ]]; then
   export TMPDIR=/tmp
   step rocprof 600 rocprofv3 --kernel-trace --stats --output-format csv \
-      -d "$PWD/$OUT/prof" -o run -- python3 "$PWD/bench.py" --no-cpu-baseline
+      -d "$PWD/$OUT/prof" -o run -- python3 "$PWD/bench.py" --no-cpu-baseline --no-companion
 fi
 echo "== done"

@@ -15,7 +15,7 @@ for grp in "FETCH_SIZE" "WRITE_SIZE" \
   i=$((i+1))
   echo "== pass $i: $grp"
   timeout -k 10 300 rocprofv3 --pmc $grp --output-format csv -d "$OUT/p$i" -o run \
-      -- python3 "$PWD/bench.py" --no-cpu-baseline --no-graph "$@" > "$OUT/p$i.log" 2>&1
+      -- python3 "$PWD/bench.py" --no-cpu-baseline --no-companion --no-graph "$@" > "$OUT/p$i.log" 2>&1
   rc=$?
   echo "rc=$rc"; tail -2 "$OUT/p$i.log"
   if [ $rc -ge 124 ] || [ $rc -eq 134 ] || [ $rc -eq 139 ]; then exit $rc; fi

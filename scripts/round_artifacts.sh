@@ -31,7 +31,7 @@ if [ "$WHAT" = main ]; then
   export TMPDIR=/tmp
   rm -rf "$PWD/$OUT/prof"
   step rocprof 300 rocprofv3 --kernel-trace --stats --output-format csv \
-      -d "$PWD/$OUT/prof" -o run -- python3 "$PWD/bench.py" --no-cpu-baseline
+      -d "$PWD/$OUT/prof" -o run -- python3 "$PWD/bench.py" --no-cpu-baseline --no-companion
   rm -f "$PWD/$OUT"/prof/*kernel_trace.csv   # per-dispatch rows: large, not judged
 fi
 if [ "$WHAT" = pmc ]; then
