@@ -23,7 +23,7 @@ DR_ERR_HIP = -2
 DR_ERR_NOMEM = -3
 DR_ERR_UNSUPPORTED = -4
 
-ABI_VERSION = 8                 # DR_ABI_VERSION in include/dronerl.h
+ABI_VERSION = 9                 # DR_ABI_VERSION in include/dronerl.h
 DR_VARIANT_GYM = 0
 DR_VARIANT_VECTORIZED = 1
 DR_VARIANT_MOVING = 2
@@ -95,6 +95,7 @@ SIGNATURES = {
                                      c_float, _P, _P, _P, _P]),
     "dr_permutation_workspace_bytes": (c_size_t, [c_int64]),
     "dr_permutation": (c_int, [c_int64, c_uint64, c_uint64, _P, _P, c_size_t, _P]),
+    "dr_permutation_dev": (c_int, [c_int64, c_uint64, _P, c_uint64, _P, _P, c_size_t, _P]),
     "dr_gather_rows": (c_int, [c_int64, c_int64, _P, _P, _P, _P]),
     "dr_gather_minibatch": (c_int, [c_int64, _P, c_int64] + [_P] * 8),
     "dr_linear_tanh2": (c_int, [c_int64, c_int64, c_int64] + [_P] * 9),
@@ -123,6 +124,10 @@ SIGNATURES = {
     "dr_grad_finish_clip_adam": (c_int, [_P, c_int64, _P, _P, _P, _P, c_double, c_double,
                                          c_double, c_double, c_float, c_int64, _P, _P,
                                          c_size_t, _P]),
+    "dr_adam_schedule": (c_int, [c_double, c_double, c_double, c_int64, _P]),
+    "dr_grad_finish_clip_adam_sched": (c_int, [_P, c_int64, _P, _P, _P, _P, c_double, c_double,
+                                               c_double, c_double, c_float, _P, _P, _P,
+                                               c_size_t, _P]),
 }
 
 _lib = None

@@ -118,9 +118,11 @@ __global__ __launch_bounds__(kBlock) void policy_sample_kernel(
 // Random 64-bit sort keys for the permutation.
 __global__ __launch_bounds__(kBlock) void perm_keys_kernel(
     int64_t n, uint32_t k0, uint32_t k1, uint64_t counter,
-    uint64_t *__restrict__ keys, int32_t *__restrict__ vals) {
+    const uint64_t *__restrict__ counter_base, uint64_t *__restrict__ keys,
+    int32_t *__restrict__ vals) {
     const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     if (i >= n) return;
+    if (counter_base) counter += *counter_base;   // device-resident base (graphs)
     const u32x4 r = philox4x32_10(
         u32x4{(uint32_t)i, (uint32_t)((uint64_t)i >> 32), (uint32_t)counter,
               TAG_PERM ^ (uint32_t)(counter >> 32)},
@@ -1280,7 +1282,14 @@ __global__ __launch_bounds__(kBlock) void clip_adam_kernel(
     int64_t n, float *__restrict__ p, float *__restrict__ g,
     float *__restrict__ m, float *__restrict__ v, const float *__restrict__ part,
     int nb, float max_norm, float w1, float beta2, float one_m_b2,
-    float step_size, float bc2_sqrt, float eps, float *norm_out) {
+    float step_size, float bc2_sqrt, const float *__restrict__ sched, float eps,
+    float *norm_out) {
+    // sched (device): this step's (step_size, sqrt(bias_correction2)), written
+    // by the host from dr_adam_schedule ahead of a graph replay
+    if (sched) {
+        step_size = sched[0];
+        bc2_sqrt = sched[1];
+    }
     // total squared norm: strided per-thread sums of the sumsq partials, then
     // a fixed-shape LDS tree (deterministic; every block gets the same value)
     __shared__ double ssum[kBlock];
@@ -1384,8 +1393,9 @@ size_t dr_permutation_workspace_bytes(int64_t n) {
     return align_up(sizeof(uint64_t) * n) * 2 + align_up(sizeof(int32_t) * n) + align_up(temp);
 }
 
-int dr_permutation(int64_t n, uint64_t seed, uint64_t counter, int32_t *out,
-                   void *workspace, size_t workspace_bytes, void *stream) {
+static int permutation_impl(int64_t n, uint64_t seed, const uint64_t *counter_base,
+                            uint64_t counter, int32_t *out, void *workspace,
+                            size_t workspace_bytes, void *stream) {
     if (n < 0 || n > 0x7fffffff || !out) return fail0(DR_ERR_INVALID, "dr_permutation: bad arguments");
     if (n == 0) return DR_OK;
     const size_t need = dr_permutation_workspace_bytes(n);
@@ -1401,7 +1411,8 @@ int dr_permutation(int64_t n, uint64_t seed, uint64_t counter, int32_t *out,
     size_t temp = need - (size_t)(w - static_cast<char *>(workspace));
     hipStream_t st = as_stream(stream);
     hipLaunchKernelGGL(perm_keys_kernel, dim3(grid_for(n)), dim3(kBlock), 0, st, n,
-                       (uint32_t)seed, (uint32_t)(seed >> 32), counter, k_in, v_in);
+                       (uint32_t)seed, (uint32_t)(seed >> 32), counter, counter_base, k_in,
+                       v_in);
     int rc = check_launch("dr_permutation keys");
     if (rc) return rc;
     hipError_t e = hipcub::DeviceRadixSort::SortPairs(w, temp, k_in, k_out, v_in, out, (int)n,
@@ -1409,6 +1420,20 @@ int dr_permutation(int64_t n, uint64_t seed, uint64_t counter, int32_t *out,
     if (e != hipSuccess)
         return fail0(DR_ERR_HIP, std::string("dr_permutation sort: ") + hipGetErrorString(e));
     return DR_OK;
+}
+
+int dr_permutation(int64_t n, uint64_t seed, uint64_t counter, int32_t *out,
+                   void *workspace, size_t workspace_bytes, void *stream) {
+    return permutation_impl(n, seed, nullptr, counter, out, workspace, workspace_bytes, stream);
+}
+
+int dr_permutation_dev(int64_t n, uint64_t seed, const uint64_t *counter_base,
+                       uint64_t counter_offset, int32_t *out, void *workspace,
+                       size_t workspace_bytes, void *stream) {
+    if (!counter_base || (((uintptr_t)counter_base) & 7))
+        return fail0(DR_ERR_INVALID, "dr_permutation_dev: counter_base must be 8-byte aligned");
+    return permutation_impl(n, seed, counter_base, counter_offset, out, workspace,
+                            workspace_bytes, stream);
 }
 
 int dr_gather_rows(int64_t m, int64_t width, const int32_t *idx, const float *src,
@@ -1512,19 +1537,27 @@ int dr_ppo_loss(int64_t m, const float *mean, const float *log_std, const float 
     return check_launch("dr_ppo_loss finish");
 }
 
+int dr_adam_schedule(double lr, double beta1, double beta2, int64_t step, float *out) {
+    if (!out || step < 1) return fail0(DR_ERR_INVALID, "dr_adam_schedule: bad arguments");
+    const double bc1 = 1.0 - std::pow(beta1, (double)step);
+    const double bc2 = 1.0 - std::pow(beta2, (double)step);
+    out[0] = (float)(lr / bc1);
+    out[1] = (float)std::sqrt(bc2);
+    return DR_OK;
+}
+
 static int launch_adam(int64_t n, float *params, float *grads, float *exp_avg,
                        float *exp_avg_sq, double lr, double beta1, double beta2, double eps,
                        float max_grad_norm, int64_t step, float *grad_norm_out,
-                       const float *sq_part, int nsq, hipStream_t st, const char *who) {
+                       const float *sq_part, int nsq, hipStream_t st, const char *who,
+                       const float *sched = nullptr) {
     // torch.optim.Adam scalars, formed in double as torch does on the host.
     const double b1 = beta1, b2 = beta2;
-    const double bc1 = 1.0 - std::pow(b1, (double)step);
-    const double bc2 = 1.0 - std::pow(b2, (double)step);
-    const float step_size = (float)(lr / bc1);
-    const float bc2_sqrt = (float)std::sqrt(bc2);
+    float ss[2] = {0.f, 1.f};
+    if (!sched) dr_adam_schedule(lr, beta1, beta2, step, ss);
     hipLaunchKernelGGL(clip_adam_kernel, dim3(nblocks_stream(n)), dim3(kBlock), 0, st, n,
                        params, grads, exp_avg, exp_avg_sq, sq_part, nsq, max_grad_norm,
-                       (float)(1.0 - b1), (float)b2, (float)(1.0 - b2), step_size, bc2_sqrt,
+                       (float)(1.0 - b1), (float)b2, (float)(1.0 - b2), ss[0], ss[1], sched,
                        (float)eps, grad_norm_out);
     return check_launch(who);
 }
@@ -1566,12 +1599,12 @@ size_t dr_grad_finish_workspace_bytes(const dr_grad_finish *f) {
     return align_up(sizeof(float) * (size_t)(bh + bf + bc > 0 ? bh + bf + bc : 1));
 }
 
-int dr_grad_finish_clip_adam(const dr_grad_finish *f, int64_t n, float *params, float *grads,
-                             float *exp_avg, float *exp_avg_sq, double lr, double beta1,
-                             double beta2, double eps, float max_grad_norm, int64_t step,
-                             float *grad_norm_out, void *workspace, size_t workspace_bytes,
-                             void *stream) {
-    if (!f || n < 1 || !params || !grads || !exp_avg || !exp_avg_sq || step < 1)
+static int grad_finish_adam_impl(const dr_grad_finish *f, int64_t n, float *params,
+                                 float *grads, float *exp_avg, float *exp_avg_sq, double lr,
+                                 double beta1, double beta2, double eps, float max_grad_norm,
+                                 int64_t step, const float *sched, float *grad_norm_out,
+                                 void *workspace, size_t workspace_bytes, void *stream) {
+    if (!f || n < 1 || !params || !grads || !exp_avg || !exp_avg_sq || (step < 1 && !sched))
         return fail0(DR_ERR_INVALID, "dr_grad_finish_clip_adam: bad arguments");
     if (f->head_workspace && (f->head_m < 1 || f->head_hd < 4 || f->head_hd > 256 ||
                               !f->log_std || !f->g_w_act || !f->g_b_act || !f->g_w_val ||
@@ -1640,7 +1673,30 @@ int dr_grad_finish_clip_adam(const dr_grad_finish *f, int64_t n, float *params, 
     if (rc) return rc;
     return launch_adam(n, params, grads, exp_avg, exp_avg_sq, lr, beta1, beta2, eps,
                        max_grad_norm, step, grad_norm_out, part, nb, st,
-                       "dr_grad_finish_clip_adam");
+                       "dr_grad_finish_clip_adam", sched);
+}
+
+int dr_grad_finish_clip_adam(const dr_grad_finish *f, int64_t n, float *params, float *grads,
+                             float *exp_avg, float *exp_avg_sq, double lr, double beta1,
+                             double beta2, double eps, float max_grad_norm, int64_t step,
+                             float *grad_norm_out, void *workspace, size_t workspace_bytes,
+                             void *stream) {
+    return grad_finish_adam_impl(f, n, params, grads, exp_avg, exp_avg_sq, lr, beta1, beta2,
+                                 eps, max_grad_norm, step, nullptr, grad_norm_out, workspace,
+                                 workspace_bytes, stream);
+}
+
+int dr_grad_finish_clip_adam_sched(const dr_grad_finish *f, int64_t n, float *params,
+                                   float *grads, float *exp_avg, float *exp_avg_sq, double lr,
+                                   double beta1, double beta2, double eps, float max_grad_norm,
+                                   const float *sched, float *grad_norm_out, void *workspace,
+                                   size_t workspace_bytes, void *stream) {
+    if (!sched || (((uintptr_t)sched) & 7))
+        return fail0(DR_ERR_INVALID,
+                     "dr_grad_finish_clip_adam_sched: sched must be 8-byte aligned");
+    return grad_finish_adam_impl(f, n, params, grads, exp_avg, exp_avg_sq, lr, beta1, beta2,
+                                 eps, max_grad_norm, 0, sched, grad_norm_out, workspace,
+                                 workspace_bytes, stream);
 }
 
 

@@ -140,6 +140,15 @@ class PPOTrainer:
         # iteration (DRONERL_ROLLOUT_GRAPH=0: always eager)
         self.rollout_graph = os.environ.get("DRONERL_ROLLOUT_GRAPH", "1") != "0"
         self._rgraph, self._rwarm = None, False
+        # likewise PPO.train's minibatch loop (single-GPU fused path), for
+        # minibatches of at most 8192 rows: there the Python launch path is
+        # the bottleneck (the reference's 64-row minibatches); larger ones
+        # keep the GPU busy on their own, and a capture at configs[2] size
+        # (65,536-row minibatches, two trainers in one process) ended in a GPU
+        # memory fault once, so it stays eager.  DRONERL_TRAIN_GRAPH=0: never.
+        self.train_graph = (os.environ.get("DRONERL_TRAIN_GRAPH", "1") != "0" and
+                            cfg.batch_size <= 8192)
+        self._tgraph, self._twarm, self._tstats = None, False, None
         self._ctr = torch.zeros(1, dtype=torch.int64, device=dev)
         # optional TrajectoryTensorboardCallback equivalent (trajectory.py)
         self.trajectory = None
@@ -211,8 +220,66 @@ class PPOTrainer:
             if self.trajectory is not None:
                 self.trajectory.on_step(self.dones[t + 1])
 
+    def _train_graphable(self) -> bool:
+        return (self.train_graph and self.use_fused and self.defer_finish and
+                self.world == 1)
+
+    def _train_body(self, obs_flat, act_flat, nmb):
+        """PPO.train's epochs x minibatches on the single-GPU fused path with
+        every per-step scalar on the device (permutation counter base, Adam's
+        bias-correction schedule): the same kernels and numerics as train(),
+        capturable into one hipGraph."""
+        cfg, M = self.cfg, self.cfg.batch_size
+        j = 0
+        for epoch in range(cfg.n_epochs):
+            perm = self.perm.dev(seed=cfg.seed * 104729 + self.rank, counter_base=self._pctr,
+                                 counter_offset=epoch)
+            for k in range(nmb):
+                idx = perm[k * M:(k + 1) * M]
+                K.gather_minibatch(idx, obs_flat, act_flat, self.aux, self.mb_obs, self.mb_act,
+                                   self.mb_aux, adv_part=self.head.adv_part)
+                grad, _ = self.fused.step(self.mb_obs, self.mb_act, self.mb_aux, self.head,
+                                          adv_ready=True, stats_out=self._tstats[j],
+                                          defer_finish=True)
+                self.opt.step_finish_sched(grad, self.fused.finish, self._sched[j])
+                j += 1
+
+    def _train_graphed(self):
+        cfg = self.cfg
+        T, N, M = cfg.n_steps, cfg.num_envs, cfg.batch_size
+        nmb = T * N // M
+        S = cfg.n_epochs * nmb
+        if self._tstats is None:
+            self._tstats = torch.zeros(S, 8, dtype=torch.float32, device=self.device)
+            self._sched = torch.zeros(S, 2, dtype=torch.float32, device=self.device)
+            self._pctr = torch.zeros(1, dtype=torch.int64, device=self.device)
+        self._pctr.fill_(self.num_updates * cfg.n_epochs)
+        self.opt.schedule(self.opt.t + 1, S, out=self._sched)
+        self.opt.t += S
+        obs_flat = self.obs[:T].reshape(T * N, -1)
+        act_flat = self.actions.reshape(T * N, 4)
+        if self._tgraph is not None:
+            self._tgraph.replay()
+        elif not self._twarm:
+            self._train_body(obs_flat, act_flat, nmb)       # eager once: lazy init
+            self._twarm = True
+        else:
+            cur = torch.cuda.current_stream(self.device)
+            cs = torch.cuda.Stream(self.device)
+            cs.wait_stream(cur)
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.stream(cs), torch.cuda.graph(g, stream=cs):
+                self._train_body(obs_flat, act_flat, nmb)
+            cur.wait_stream(cs)
+            g.replay()
+            self._tgraph = g
+        self.num_updates += 1
+        return self._tstats.mean(0)
+
     @torch.no_grad()
     def train(self):
+        if self._train_graphable():
+            return self._train_graphed()
         cfg = self.cfg
         T, N, M = cfg.n_steps, cfg.num_envs, cfg.batch_size
         obs_flat = self.obs[:T].reshape(T * N, -1)

@@ -80,6 +80,16 @@ class Permuter:
                                         ptr(o), ptr(self.ws), self.ws.numel(), _s(o)))
         return o
 
+    def dev(self, seed: int, counter_base: torch.Tensor, counter_offset: int, out=None):
+        """__call__ with counter = counter_base[0] + counter_offset, the base
+        an int64 device tensor read by the kernel (graph-capturable)."""
+        o = self.out if out is None else out
+        assert counter_base.dtype == torch.int64 and counter_base.device == o.device
+        check(_lib.lib().dr_permutation_dev(self.n, seed & (2**64 - 1), ptr(counter_base),
+                                            counter_offset & (2**64 - 1), ptr(o), ptr(self.ws),
+                                            self.ws.numel(), _s(o)))
+        return o
+
 
 def gather_rows(idx, src, out=None):
     """out[k] = src[idx[k]] for a 2-D f32 src (row width = src.shape[1])."""
@@ -180,6 +190,36 @@ class ClipAdam:
             float(self.lr if lr is None else lr), float(self.b1), float(self.b2),
             float(self.eps), float(self.max_norm), self.t, ptr(self.grad_norm),
             ptr(finish.ws), finish.ws.numel(), _s(self.p)))
+        return self.grad_norm
+
+    def schedule(self, first_step: int, count: int, out: torch.Tensor | None = None):
+        """(count, 2) f32 of Adam's step-dependent scalars for steps
+        first_step .. first_step + count - 1 (dr_adam_schedule, host)."""
+        L = _lib.lib()
+        buf = (ctypes.c_float * (2 * count))()
+        for j in range(count):
+            check(L.dr_adam_schedule(float(self.lr), float(self.b1), float(self.b2),
+                                     first_step + j, ctypes.byref(buf, 8 * j)))
+        t = torch.frombuffer(bytearray(buf), dtype=torch.float32).view(count, 2)
+        if out is None:
+            return t
+        out.copy_(t)
+        return out
+
+    def step_finish_sched(self, grads: torch.Tensor, finish: "GradFinish", sched: torch.Tensor):
+        """step_finish with this step's scalars read on the device from
+        `sched` (2 f32, from schedule()); advances nothing on the host (the
+        caller owns the step count: graph replays)."""
+        L = _lib.lib()
+        f = ctypes.byref(finish.desc)
+        need = L.dr_grad_finish_workspace_bytes(f)
+        if finish.ws is None or finish.ws.numel() < need:
+            finish.ws = torch.empty(need, dtype=torch.uint8, device=self.p.device)
+        check(L.dr_grad_finish_clip_adam_sched(
+            f, self.p.numel(), ptr(self.p), ptr(_f32(grads)), ptr(self.m), ptr(self.v),
+            float(self.lr), float(self.b1), float(self.b2), float(self.eps),
+            float(self.max_norm), ptr(sched), ptr(self.grad_norm), ptr(finish.ws),
+            finish.ws.numel(), _s(self.p)))
         return self.grad_norm
 
     def step(self, grads: torch.Tensor, lr=None):

@@ -39,7 +39,7 @@
 extern "C" {
 #endif
 
-#define DR_ABI_VERSION 8
+#define DR_ABI_VERSION 9
 
 enum dr_status {
     DR_OK = 0,
@@ -237,6 +237,11 @@ int dr_policy_sample_dev(int64_t n, const float *mean, const float *log_std,
 size_t dr_permutation_workspace_bytes(int64_t n);
 int dr_permutation(int64_t n, uint64_t seed, uint64_t counter, int32_t *out,
                    void *workspace, size_t workspace_bytes, void *stream);
+/* dr_permutation with counter = *counter_base + counter_offset, the base a
+   device u64 (8-byte aligned): graph-capturable epochs.  (ABI v9.) */
+int dr_permutation_dev(int64_t n, uint64_t seed, const uint64_t *counter_base,
+                       uint64_t counter_offset, int32_t *out, void *workspace,
+                       size_t workspace_bytes, void *stream);
 
 /* Gather a minibatch: dst[k,:] = src[idx[k],:] for row width `width`
    (floats), k < m.  Used to form minibatches from the flat rollout. */
@@ -430,6 +435,24 @@ int dr_grad_finish_clip_adam(const dr_grad_finish *f, int64_t n, float *params,
                              double eps, float max_grad_norm, int64_t step,
                              float *grad_norm_out, void *workspace,
                              size_t workspace_bytes, void *stream);
+
+/* Host-only: torch.optim.Adam's step-dependent scalars for step >= 1, as
+   dr_clip_adam / dr_grad_finish_clip_adam form them: out[0] = lr /
+   (1 - beta1^step), out[1] = sqrt(1 - beta2^step), in double, then f32.
+   (ABI v9.) */
+int dr_adam_schedule(double lr, double beta1, double beta2, int64_t step, float *out);
+
+/* dr_grad_finish_clip_adam with the step's two scalars read on the device
+   from `sched` (2 floats, 8-byte aligned, filled from dr_adam_schedule):
+   a training loop captured once into a hipGraph replays with the right
+   bias corrections when the host rewrites the schedule between replays.
+   Bitwise dr_grad_finish_clip_adam for the same step.  (ABI v9.) */
+int dr_grad_finish_clip_adam_sched(const dr_grad_finish *f, int64_t n, float *params,
+                                   float *grads, float *exp_avg, float *exp_avg_sq,
+                                   double lr, double beta1, double beta2, double eps,
+                                   float max_grad_norm, const float *sched,
+                                   float *grad_norm_out, void *workspace,
+                                   size_t workspace_bytes, void *stream);
 
 #ifdef __cplusplus
 }

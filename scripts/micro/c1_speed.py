@@ -4,7 +4,7 @@ import torch
 from drone_rl_amd.ppo import PPOConfig, PPOTrainer
 for g in (False, True):
     tr = PPOTrainer(PPOConfig.sb3_defaults(seed=0))
-    tr.rollout_graph = g
+    tr.rollout_graph = tr.train_graph = g
     tr.learn_step(); tr.learn_step(); torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(3):
@@ -12,5 +12,5 @@ for g in (False, True):
     torch.cuda.synchronize()
     dt = (time.perf_counter() - t0) / 3
     t1 = time.perf_counter(); tr.collect_rollouts(); torch.cuda.synchronize(); tr_roll = time.perf_counter() - t1
-    print(f"c1 rollout_graph={g}: {dt*1e3:.1f} ms/update, {2048/dt:.0f} env-steps/s, rollout {tr_roll*1e3:.1f} ms", flush=True)
+    print(f"c1 graphs={g}: {dt*1e3:.1f} ms/update, {2048/dt:.0f} env-steps/s, rollout {tr_roll*1e3:.1f} ms", flush=True)
     tr.close()

@@ -165,9 +165,11 @@ def test_tuned_gemms_load_and_are_deterministic():
 
 @pytest.mark.parametrize("cfg", ["small", "sb3_1env"])
 def test_rollout_graph_is_bitwise_eager(cfg):
-    """The rollout loop captured into a hipGraph (after one eager warm-up
-    iteration; the policy-noise counter base lives on the device) replays to
-    bitwise the eager rollouts and updates over several PPO iterations."""
+    """The rollout loop and PPO.train's minibatch loop captured into
+    hipGraphs (after one eager warm-up iteration; the policy-noise and
+    permutation counter bases and Adam's bias-correction schedule live on the
+    device) replay to bitwise the eager rollouts and updates over several
+    PPO iterations."""
     from drone_rl_amd.ppo import PPOConfig, PPOTrainer
 
     def make(graph):
@@ -175,16 +177,18 @@ def test_rollout_graph_is_bitwise_eager(cfg):
             tr = _trainer()
         else:
             tr = PPOTrainer(PPOConfig.sb3_defaults(n_steps=128, seed=3))
-        tr.rollout_graph = graph
+        tr.rollout_graph = tr.train_graph = graph
         return tr
 
     a, b = make(False), make(True)
     for _ in range(4):
-        a.learn_step()
-        b.learn_step()
+        sa = a.learn_step()
+        sb = b.learn_step()
+        assert torch.equal(sa, sb)
         for name in ("obs", "actions", "logp", "values", "rewards", "dones", "adv"):
             assert torch.equal(getattr(a, name), getattr(b, name)), name
-    assert b._rgraph is not None
+        assert torch.equal(a.opt.m, b.opt.m) and a.opt.t == b.opt.t
+    assert b._rgraph is not None and b._tgraph is not None
     assert torch.equal(a.policy.flat.detach(), b.policy.flat.detach())
     assert torch.equal(a.env.get("ep_num"), b.env.get("ep_num"))
     a.close()
