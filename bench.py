@@ -61,17 +61,44 @@ def parse():
     return ap.parse_args()
 
 
+def cpu_share():
+    """(P, affinity, why): the worker count for the CPU baseline.  P is the
+    affinity count (P = len(os.sched_getaffinity(0))), lowered
+    only to the CPU share this process is actually granted: a cgroup CPU
+    quota, or the OMP_NUM_THREADS the GPU box sets to its per-GPU share
+    (there the affinity mask shows the whole machine)."""
+    aff = len(os.sched_getaffinity(0))
+    caps = {}
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            caps["cgroup cpu.max quota"] = max(1, int(int(q) / int(per)))
+    except (OSError, ValueError):
+        pass
+    omp = os.environ.get("OMP_NUM_THREADS", "")
+    if omp.isdigit() and int(omp) > 0:
+        caps["OMP_NUM_THREADS"] = int(omp)
+    p, why = aff, "sched_getaffinity"
+    for k, v in caps.items():
+        if v < p:
+            p, why = v, k
+    return p, aff, why
+
+
 def cpu_baseline(seconds):
     from oracle.cpu_baseline import c1_ppo, cpu_model, numpy_batched, run_pool, single_env
-    procs = max(1, min(16, len(os.sched_getaffinity(0))))
-    r = run_pool(procs, 64, seconds)
+    procs, aff, why = cpu_share()
+    envs = 65536 // procs       # configs[1]'s 65,536 envs split across the workers
+    r = run_pool(procs, envs, seconds)
     # BASELINE.md CPU plan (i), (iii), (iv) beside the headline (ii)
     plan = {"single_env": single_env(seconds),
             "numpy_batched_65536": numpy_batched(65536, seconds),
             "c1_ppo_sb3_defaults": c1_ppo(2, procs)}
     return {"value": round(r["value"], 1), "unit": "env-steps/s", "cores": procs,
+            "affinity_cpus": aff, "cores_limited_by": why,
             "kind": "port",
-            "sample": (f"{procs} worker processes x 64 numpy-port envs (oracle/drone_np, "
+            "sample": (f"{procs} worker processes x {envs} numpy-port envs (65,536 split "
+                       f"across the workers; oracle/drone_np, "
                        f"bit-exact vs reference), random U[0,7.3575)^4 actions, DummyVecEnv "
                        f"auto-reset, {r['elapsed']:.2f} s wall each ({r['steps']} env-steps); "
                        f"SubprocVecEnv-equivalent without pipe IPC; CPU: {cpu_model()}"),

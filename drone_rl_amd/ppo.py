@@ -139,7 +139,7 @@ class PPOTrainer:
         # rollout loop captured into a hipGraph after one eager warm-up
         # iteration (DRONERL_ROLLOUT_GRAPH=0: always eager)
         self.rollout_graph = os.environ.get("DRONERL_ROLLOUT_GRAPH", "1") != "0"
-        self._rgraph, self._rwarm = None, False
+        self._rgraph, self._rwarm, self._rkey = None, False, None
         # likewise PPO.train's minibatch loop (single-GPU fused path), for
         # minibatches of at most 8192 rows: there the Python launch path is
         # the bottleneck (the reference's 64-row minibatches); larger ones
@@ -148,7 +148,7 @@ class PPOTrainer:
         # memory fault once, so it stays eager.  DRONERL_TRAIN_GRAPH=0: never.
         self.train_graph = (os.environ.get("DRONERL_TRAIN_GRAPH", "1") != "0" and
                             cfg.batch_size <= 8192)
-        self._tgraph, self._twarm, self._tstats = None, False, None
+        self._tgraph, self._twarm, self._tstats, self._tkey = None, False, None, None
         self._ctr = torch.zeros(1, dtype=torch.int64, device=dev)
         # optional TrajectoryTensorboardCallback equivalent (trajectory.py)
         self.trajectory = None
@@ -174,6 +174,10 @@ class PPOTrainer:
         fwd = self.infer if self.use_fused else self.policy
         # noise counter of step t = num_updates * T + t, its base on the device
         self._ctr.fill_(self.num_updates * T)
+        key = self._graph_key("rollout")
+        if self._rgraph is not None and key != self._rkey:
+            self._rgraph = None       # a host scalar baked into the graph changed
+        self._rkey = key
         if not (self.rollout_graph and self.trajectory is None):
             self._rollout_steps(fwd)
         elif self._rgraph is not None:
@@ -220,6 +224,22 @@ class PPOTrainer:
             if self.trajectory is not None:
                 self.trajectory.on_step(self.dones[t + 1])
 
+    def _graph_key(self, kind: str):
+        """Every host-side value a captured graph holds as a kernel argument
+        (the rest -- noise / permutation counters, Adam's bias corrections --
+        is read from device memory on each replay).  A graph whose key no
+        longer matches is dropped and re-captured, so env.seed(), a config
+        change or a new learning rate take effect on the graph path exactly
+        as on the eager path."""
+        c = self.cfg
+        if kind == "rollout":
+            return (self.env.seed_value, c.seed, self.rank, c.num_envs, c.n_steps)
+        o = self.opt
+        return (c.seed, self.rank, c.n_epochs, c.batch_size, c.clip_range, c.ent_coef,
+                c.vf_coef, c.normalize_advantage, float(o.lr), o.b1, o.b2, o.eps,
+                o.max_norm, float(self.head.clip), float(self.head.ent), float(self.head.vf),
+                self.head.norm)
+
     def _train_graphable(self) -> bool:
         return (self.train_graph and self.use_fused and self.defer_finish and
                 self.world == 1)
@@ -258,6 +278,10 @@ class PPOTrainer:
         self.opt.t += S
         obs_flat = self.obs[:T].reshape(T * N, -1)
         act_flat = self.actions.reshape(T * N, 4)
+        key = self._graph_key("train")
+        if self._tgraph is not None and key != self._tkey:
+            self._tgraph = None
+        self._tkey = key
         if self._tgraph is not None:
             self._tgraph.replay()
         elif not self._twarm:

@@ -305,6 +305,11 @@ def load_into(trainer, path, load_env_state=True):
                 step = int(float(st["step"]))
             trainer.opt.t = step
     trainer.num_timesteps = int(ck["data"].get("num_timesteps", 0))
+    # SB3 counts optimizer passes (_n_updates = iterations x n_epochs); the
+    # trainer's iteration count keys the policy-noise and permutation Philox
+    # streams and the eps_schedule, so a resumed run continues them instead
+    # of replaying the first iterations' streams and curriculum steps
+    trainer.num_updates = int(ck["data"].get("_n_updates", 0)) // max(trainer.cfg.n_epochs, 1)
     if load_env_state and ck["env"] is not None and \
             len(ck["env"]["ep_num"]) == trainer.env.num_envs:
         trainer.env.set("ep_num", ck["env"]["ep_num"])

@@ -22,6 +22,15 @@ import torch.distributed as dist
 from .ppo import PPOConfig, PPOTrainer
 
 
+def checkpoint_path(path: str, rank: int, world: int) -> str:
+    """Per-rank checkpoint name that keeps the extension (dd.zip ->
+    dd.rank0.zip), so the SB3 / torch format choice survives the suffix."""
+    if world == 1:
+        return path
+    root, ext = os.path.splitext(path)
+    return f"{root}.rank{rank}{ext}"
+
+
 def main(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--envs", type=int, default=65536, help="envs per GPU")
@@ -46,6 +55,11 @@ def main(argv=None):
     ap.add_argument("--traj-dir", default=None,
                     help="record env 0's trajectories like traj_tb.py (every 25th episode, "
                          "blocks of 500) into this directory (npz, PNG if matplotlib)")
+    ap.add_argument("--reset-num-timesteps", action=argparse.BooleanOptionalAction,
+                    default=True,
+                    help="after a resume, train --total-steps more (SB3's default, the "
+                         "reference's behaviour); --no-reset-num-timesteps trains up to "
+                         "--total-steps in all")
     a = ap.parse_args(argv)
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -53,31 +67,35 @@ def main(argv=None):
     torch.cuda.set_device(local)
     if world > 1:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    common = dict(num_envs=a.envs, learning_rate=a.lr, seed=a.seed,
+                  state_dtype=a.state_dtype, variant=a.variant, initial_eps=a.initial_eps,
+                  eps_schedule=tuple((int(u), float(e)) for u, e in
+                                     (kv.split(":") for kv in a.eps_schedule.split(",") if kv)))
     if a.sb3_defaults:
-        cfg = PPOConfig.sb3_defaults(num_envs=a.envs, seed=a.seed, state_dtype=a.state_dtype,
-                                     variant=a.variant)
+        cfg = PPOConfig.sb3_defaults(**common)
     else:
-        cfg = PPOConfig(num_envs=a.envs, n_steps=a.n_steps, batch_size=a.batch_size,
-                        n_epochs=a.epochs, learning_rate=a.lr, net_arch=tuple(a.net),
-                        seed=a.seed, state_dtype=a.state_dtype, variant=a.variant,
-                        initial_eps=a.initial_eps,
-                        eps_schedule=tuple((int(u), float(e)) for u, e in
-                                           (kv.split(":") for kv in a.eps_schedule.split(",")
-                                            if kv)))
+        cfg = PPOConfig(n_steps=a.n_steps, batch_size=a.batch_size, n_epochs=a.epochs,
+                        net_arch=tuple(a.net), **common)
     tr = PPOTrainer(cfg, rank=rank, world_size=world)
     if a.traj_dir and rank == 0:
         from .trajectory import TrajectoryRecorder
         tr.trajectory = TrajectoryRecorder(tr.env, out_dir=a.traj_dir)
-    ck = a.checkpoint if world == 1 else f"{a.checkpoint}.rank{rank}"
+    ck = checkpoint_path(a.checkpoint, rank, world)
     # *.zip = stable-baselines3 PPO checkpoint (the reference's dd.zip,
     # train.py:10-31 / 70); anything else = this trainer's bit-exact resume file
-    sb3 = ck.endswith(".zip")
+    sb3 = a.checkpoint.endswith(".zip")
+    total = int(a.total_steps)
     if os.path.exists(ck):
         tr.load_sb3(ck) if sb3 else tr.load(ck)
         if rank == 0:
             print(json.dumps({"resumed": ck, "num_timesteps": tr.num_timesteps}), flush=True)
-    tr.learn(int(a.total_steps), log_every=a.log_every,
-             logger=lambda d: print(json.dumps(d), flush=True))
+        if a.reset_num_timesteps:
+            # SB3 learn(reset_num_timesteps=True), the reference's call
+            # (train.py:63-68): every run trains --total-steps more steps and
+            # counts from 0 (the update counter, which keys the random
+            # streams, keeps running)
+            tr.num_timesteps = 0
+    tr.learn(total, log_every=a.log_every, logger=lambda d: print(json.dumps(d), flush=True))
     tr.save_sb3(ck) if sb3 else tr.save(ck)
     tr.close()
     if world > 1:

@@ -123,6 +123,55 @@ def test_sb3_zip_roundtrip_on_gpu(tmp_path):
     b.close()
 
 
+def test_sb3_zip_resume_continues_streams_and_schedule(tmp_path):
+    """load_sb3 restores the iteration count from SB3's _n_updates: the
+    resumed run continues the policy-noise / permutation streams and does not
+    re-fire eps_schedule entries that already ran (which would overwrite the
+    curriculum the sidecar restored)."""
+    sched = ((0, 0.05), (2, 0.2))
+    a = _trainer(eps_schedule=sched)
+    a.learn_step()
+    a.learn_step()          # update 0 set eps 0.05; the next fires at update 2
+    a.env.set("eps", np.full(a.env.num_envs, 0.1))
+    path = tmp_path / "dd.zip"
+    a.save_sb3(path)
+    b = _trainer(eps_schedule=sched)
+    b.load_sb3(path)
+    assert b.num_updates == a.num_updates == 2
+    b.learn_step()          # update 2: noise counter base = 2 * T
+    assert b._ctr.item() == 2 * b.cfg.n_steps and b.num_updates == 3
+    assert (b.env.get("eps").cpu().numpy() >= 0.2).all()     # update-2 entry fired once
+    c = _trainer(eps_schedule=((0, 0.05),))
+    c.load_sb3(path)
+    c.learn_step()           # the update-0 entry must not fire again
+    assert (c.env.get("eps").cpu().numpy() >= 0.1).all()
+    for t in (a, b, c):
+        t.close()
+
+
+def test_graphs_follow_host_scalar_changes():
+    """A seed, learning-rate or loss-coefficient change after the rollout /
+    training graphs were captured takes effect on the graph path exactly as
+    on the eager path (the graphs are re-captured when a baked-in host value
+    changes)."""
+    a, b = _trainer(), _trainer()
+    a.rollout_graph = a.train_graph = False
+    b.rollout_graph = b.train_graph = True
+    for it in range(5):
+        if it == 3:
+            for t in (a, b):
+                t.env.seed(1234)
+                t.opt.lr = 1e-4
+                t.head.clip = 0.1
+        sa, sb = a.learn_step(), b.learn_step()
+        assert torch.equal(sa, sb), it
+        assert torch.equal(a.policy.flat.detach(), b.policy.flat.detach()), it
+        assert torch.equal(a.env.get("pos"), b.env.get("pos")), it
+    assert b._rgraph is not None and b._tgraph is not None
+    a.close()
+    b.close()
+
+
 def test_tuned_gemms_load_and_are_deterministic():
     """The committed TunableOp solutions (policy.use_tuned_gemms) load on the
     box, give a bitwise-reproducible minibatch gradient at the bench shape
