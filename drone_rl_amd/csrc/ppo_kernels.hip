@@ -12,9 +12,8 @@
 // Reductions are deterministic: fixed per-block partials, then a fixed-order
 // combine (no float atomics), so a rerun reproduces every bit.
 
-#include <hipcub/hipcub.hpp>
-
 #include <cmath>
+#include <cstdlib>
 #include <string>
 
 #include "common.h"
@@ -115,20 +114,202 @@ __global__ __launch_bounds__(kBlock) void policy_sample_kernel(
     if (logp) logp[i] = lp;
 }
 
-// Random 64-bit sort keys for the permutation.
-__global__ __launch_bounds__(kBlock) void perm_keys_kernel(
-    int64_t n, uint32_t k0, uint32_t k1, uint64_t counter,
-    const uint64_t *__restrict__ counter_base, uint64_t *__restrict__ keys,
-    int32_t *__restrict__ vals) {
-    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-    if (i >= n) return;
-    if (counter_base) counter += *counter_base;   // device-resident base (graphs)
+// ---------------------------------------------------------------------------
+// Minibatch permutation (RolloutBuffer.get's np.random.permutation): element
+// i gets the 64-bit Philox key K_i = (r.x << 32) | r.y of counter (i,
+// counter); the permutation is the order of (K_i, i), i.e. the stable argsort
+// of the keys.  Built from four kernels that keep no state across launches
+// (so a hipGraph replay is a fresh sort; rocPRIM's onesweep radix sort,
+// used before, faulted on the second replay of a captured graph):
+//   1. perm_hist:    B = 2^lgB buckets on the top lgB key bits (at most 1024
+//                    elements per bucket on average); per-tile bucket counts
+//                    (LDS histogram), keys written out;
+//   2. perm_scan:    per bucket, the running count over tiles (exclusive)
+//                    and the total; then one block scans the B totals;
+//   3. perm_scatter: element ids to their bucket's range (a tile's slots
+//                    of one bucket are claimed in any order -- step 4 fixes
+//                    the order);
+//   4. perm_sort:    one block per bucket sorts (key, id) with an
+//                    all-ascending bitonic network in LDS (buckets above
+//                    kPermCap elements -- probability ~e^-330 at the mean
+//                    of 1024 -- sort in global scratch with the same code).
+// Bucket order is key order, so the result is exactly the stable argsort.
+// ---------------------------------------------------------------------------
+constexpr int kPermCap = 2048;          // elements per bucket sorted in LDS
+constexpr int kPermMaxLgB = 14;         // B <= 16384 (64 KB LDS histogram)
+
+struct PermGeom {
+    int64_t n, B, tile, T;
+    int lgB;
+};
+
+PermGeom perm_geom(int64_t n) {
+    PermGeom g{};
+    g.n = n;
+    g.lgB = 0;
+    while (g.lgB < kPermMaxLgB && ((int64_t)1024 << g.lgB) < n) ++g.lgB;
+    g.B = (int64_t)1 << g.lgB;
+    g.tile = g.B * 4 > 4096 ? g.B * 4 : 4096;
+    g.T = (n + g.tile - 1) / g.tile;
+    return g;
+}
+
+__device__ inline uint64_t perm_key(int64_t i, uint32_t k0, uint32_t k1, uint64_t counter) {
     const u32x4 r = philox4x32_10(
         u32x4{(uint32_t)i, (uint32_t)((uint64_t)i >> 32), (uint32_t)counter,
               TAG_PERM ^ (uint32_t)(counter >> 32)},
         k0, k1);
-    keys[i] = ((uint64_t)r.x << 32) | r.y;
-    vals[i] = (int32_t)i;
+    return ((uint64_t)r.x << 32) | r.y;
+}
+
+__device__ inline uint32_t perm_bucket(uint64_t key, int lgB) {
+    return lgB ? (uint32_t)(key >> (64 - lgB)) : 0u;
+}
+
+__global__ __launch_bounds__(kBlock) void perm_hist_kernel(
+    PermGeom g, uint32_t k0, uint32_t k1, uint64_t counter,
+    const uint64_t *__restrict__ counter_base, uint64_t *__restrict__ keys,
+    uint32_t *__restrict__ hist) {
+    extern __shared__ uint32_t sh_cnt[];
+    if (counter_base) counter += *counter_base;     // device-resident base (graphs)
+    for (int64_t b = threadIdx.x; b < g.B; b += kBlock) sh_cnt[b] = 0;
+    __syncthreads();
+    const int64_t lo = (int64_t)blockIdx.x * g.tile;
+    const int64_t hi = lo + g.tile < g.n ? lo + g.tile : g.n;
+    for (int64_t i = lo + threadIdx.x; i < hi; i += kBlock) {
+        const uint64_t key = perm_key(i, k0, k1, counter);
+        keys[i] = key;
+        atomicAdd(&sh_cnt[perm_bucket(key, g.lgB)], 1u);   // counts: order-free
+    }
+    __syncthreads();
+    uint32_t *row = hist + (int64_t)blockIdx.x * g.B;
+    for (int64_t b = threadIdx.x; b < g.B; b += kBlock) row[b] = sh_cnt[b];
+}
+
+// hist[t][b] -> exclusive running count over t; total[b]
+__global__ __launch_bounds__(kBlock) void perm_scan_tiles_kernel(PermGeom g,
+                                                                 uint32_t *__restrict__ hist,
+                                                                 uint32_t *__restrict__ total) {
+    const int64_t b = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (b >= g.B) return;
+    uint32_t run = 0;
+    for (int64_t t = 0; t < g.T; ++t) {
+        const uint32_t c = hist[t * g.B + b];
+        hist[t * g.B + b] = run;
+        run += c;
+    }
+    total[b] = run;
+}
+
+// start[b] = exclusive scan of total, start[B] = n (one block of 1024)
+__global__ __launch_bounds__(1024) void perm_scan_buckets_kernel(PermGeom g,
+                                                                 const uint32_t *__restrict__ total,
+                                                                 uint32_t *__restrict__ start) {
+    __shared__ uint32_t part[1024];
+    const int t = threadIdx.x;
+    const int64_t per = (g.B + 1023) / 1024;
+    const int64_t lo = t * per, hi = lo + per < g.B ? lo + per : g.B;
+    uint32_t s = 0;
+    for (int64_t b = lo; b < hi; ++b) s += total[b];
+    part[t] = s;
+    __syncthreads();
+    for (int off = 1; off < 1024; off <<= 1) {          // inclusive Hillis-Steele
+        const uint32_t v = t >= off ? part[t - off] : 0u;
+        __syncthreads();
+        part[t] += v;
+        __syncthreads();
+    }
+    uint32_t run = part[t] - s;
+    for (int64_t b = lo; b < hi; ++b) {
+        start[b] = run;
+        run += total[b];
+    }
+    if (t == 1023) start[g.B] = (uint32_t)g.n;
+}
+
+__global__ __launch_bounds__(kBlock) void perm_scatter_kernel(
+    PermGeom g, const uint64_t *__restrict__ keys, const uint32_t *__restrict__ hist,
+    const uint32_t *__restrict__ start, int32_t *__restrict__ ids) {
+    extern __shared__ uint32_t sh_cur[];
+    const uint32_t *row = hist + (int64_t)blockIdx.x * g.B;
+    for (int64_t b = threadIdx.x; b < g.B; b += kBlock) sh_cur[b] = start[b] + row[b];
+    __syncthreads();
+    const int64_t lo = (int64_t)blockIdx.x * g.tile;
+    const int64_t hi = lo + g.tile < g.n ? lo + g.tile : g.n;
+    for (int64_t i = lo + threadIdx.x; i < hi; i += kBlock) {
+        const uint32_t pos = atomicAdd(&sh_cur[perm_bucket(keys[i], g.lgB)], 1u);
+        ids[pos] = (int32_t)i;
+    }
+}
+
+__device__ inline bool perm_greater(uint64_t ka, int32_t ia, uint64_t kb, int32_t ib) {
+    return ka > kb || (ka == kb && ia > ib);
+}
+
+// All-ascending bitonic sort of (key, id) pairs at [0, s), padded virtually
+// to the next power of two with +inf: every comparator puts the minimum at
+// the lower index, so padding (the suffix) never moves and is never read.
+template <typename KP, typename IP>
+__device__ inline void bitonic_sort_pairs(KP key, IP id, int64_t s) {
+    int64_t P = 1;
+    while (P < s) P <<= 1;
+    for (int64_t k = 2; k <= P; k <<= 1) {
+        for (int64_t j = k >> 1; j >= 1; j >>= 1) {
+            for (int64_t p = threadIdx.x; p < P / 2; p += kBlock) {
+                int64_t lo, hi;
+                if (j == (k >> 1)) {         // first merge step: mirrored pairs
+                    const int64_t blk = p / j, off = p - blk * j;
+                    lo = blk * k + off;
+                    hi = blk * k + k - 1 - off;
+                } else {
+                    lo = (p / j) * 2 * j + (p % j);
+                    hi = lo + j;
+                }
+                if (hi < s) {
+                    const uint64_t ka = key[lo], kb = key[hi];
+                    const int32_t ia = id[lo], ib = id[hi];
+                    if (perm_greater(ka, ia, kb, ib)) {
+                        key[lo] = kb;
+                        key[hi] = ka;
+                        id[lo] = ib;
+                        id[hi] = ia;
+                    }
+                }
+            }
+            __syncthreads();
+        }
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void perm_sort_kernel(
+    PermGeom g, uint32_t k0, uint32_t k1, uint64_t counter,
+    const uint64_t *__restrict__ counter_base, const uint32_t *__restrict__ start,
+    int32_t *__restrict__ ids, uint64_t *__restrict__ gkeys, int32_t *__restrict__ out,
+    int lds_cap) {
+    __shared__ uint64_t sk[kPermCap];
+    __shared__ int32_t si[kPermCap];
+    if (counter_base) counter += *counter_base;
+    const int64_t b = blockIdx.x;
+    const int64_t base = start[b], s = (int64_t)start[b + 1] - base;
+    if (s <= lds_cap) {
+        for (int64_t k = threadIdx.x; k < s; k += kBlock) {
+            const int32_t e = ids[base + k];
+            si[k] = e;
+            sk[k] = perm_key(e, k0, k1, counter);
+        }
+        __syncthreads();
+        bitonic_sort_pairs(sk, si, s);
+        for (int64_t k = threadIdx.x; k < s; k += kBlock) out[base + k] = si[k];
+    } else {
+        // practically unreachable: the same network over global scratch
+        // (the keys array is free again after the scatter)
+        uint64_t *kk = gkeys + base;
+        int32_t *ii = ids + base;
+        for (int64_t k = threadIdx.x; k < s; k += kBlock) kk[k] = perm_key(ii[k], k0, k1, counter);
+        __syncthreads();
+        bitonic_sort_pairs(kk, ii, s);
+        for (int64_t k = threadIdx.x; k < s; k += kBlock) out[base + k] = ii[k];
+    }
 }
 
 // dst[k, j] = src[idx[k], j]; one thread per output element (coalesced
@@ -1386,11 +1567,10 @@ static size_t align_up(size_t x) { return (x + 255) & ~(size_t)255; }
 
 size_t dr_permutation_workspace_bytes(int64_t n) {
     if (n <= 0) return 0;
-    size_t temp = 0;
-    (void)hipcub::DeviceRadixSort::SortPairs(nullptr, temp, (uint64_t *)nullptr,
-                                       (uint64_t *)nullptr, (int32_t *)nullptr,
-                                       (int32_t *)nullptr, (int)n, 0, 64, (hipStream_t)0);
-    return align_up(sizeof(uint64_t) * n) * 2 + align_up(sizeof(int32_t) * n) + align_up(temp);
+    const PermGeom g = perm_geom(n);
+    return align_up(sizeof(uint64_t) * n) + align_up(sizeof(int32_t) * n) +
+           align_up(sizeof(uint32_t) * g.T * g.B) + align_up(sizeof(uint32_t) * g.B) +
+           align_up(sizeof(uint32_t) * (g.B + 1));
 }
 
 static int permutation_impl(int64_t n, uint64_t seed, const uint64_t *counter_base,
@@ -1401,25 +1581,42 @@ static int permutation_impl(int64_t n, uint64_t seed, const uint64_t *counter_ba
     const size_t need = dr_permutation_workspace_bytes(n);
     if (!workspace || workspace_bytes < need)
         return fail0(DR_ERR_INVALID, "dr_permutation: workspace too small");
+    const PermGeom g = perm_geom(n);
     char *w = static_cast<char *>(workspace);
-    uint64_t *k_in = reinterpret_cast<uint64_t *>(w);
+    uint64_t *keys = reinterpret_cast<uint64_t *>(w);
     w += align_up(sizeof(uint64_t) * n);
-    uint64_t *k_out = reinterpret_cast<uint64_t *>(w);
-    w += align_up(sizeof(uint64_t) * n);
-    int32_t *v_in = reinterpret_cast<int32_t *>(w);
+    int32_t *ids = reinterpret_cast<int32_t *>(w);
     w += align_up(sizeof(int32_t) * n);
-    size_t temp = need - (size_t)(w - static_cast<char *>(workspace));
+    uint32_t *hist = reinterpret_cast<uint32_t *>(w);
+    w += align_up(sizeof(uint32_t) * g.T * g.B);
+    uint32_t *total = reinterpret_cast<uint32_t *>(w);
+    w += align_up(sizeof(uint32_t) * g.B);
+    uint32_t *start = reinterpret_cast<uint32_t *>(w);
     hipStream_t st = as_stream(stream);
-    hipLaunchKernelGGL(perm_keys_kernel, dim3(grid_for(n)), dim3(kBlock), 0, st, n,
-                       (uint32_t)seed, (uint32_t)(seed >> 32), counter, counter_base, k_in,
-                       v_in);
-    int rc = check_launch("dr_permutation keys");
+    const uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
+    const size_t lds = sizeof(uint32_t) * (size_t)g.B;
+    hipLaunchKernelGGL(perm_hist_kernel, dim3((unsigned)g.T), dim3(kBlock), lds, st, g, k0, k1,
+                       counter, counter_base, keys, hist);
+    int rc = check_launch("dr_permutation hist");
     if (rc) return rc;
-    hipError_t e = hipcub::DeviceRadixSort::SortPairs(w, temp, k_in, k_out, v_in, out, (int)n,
-                                                      0, 64, st);
-    if (e != hipSuccess)
-        return fail0(DR_ERR_HIP, std::string("dr_permutation sort: ") + hipGetErrorString(e));
-    return DR_OK;
+    hipLaunchKernelGGL(perm_scan_tiles_kernel, dim3(grid_for(g.B)), dim3(kBlock), 0, st, g,
+                       hist, total);
+    if ((rc = check_launch("dr_permutation scan"))) return rc;
+    hipLaunchKernelGGL(perm_scan_buckets_kernel, dim3(1), dim3(1024), 0, st, g, total, start);
+    if ((rc = check_launch("dr_permutation scan"))) return rc;
+    hipLaunchKernelGGL(perm_scatter_kernel, dim3((unsigned)g.T), dim3(kBlock), lds, st, g, keys,
+                       hist, start, ids);
+    if ((rc = check_launch("dr_permutation scatter"))) return rc;
+    // DRONERL_PERM_LDS_CAP (tests only) lowers the LDS capacity so that the
+    // global-scratch path of perm_sort_kernel runs on ordinary sizes
+    int cap = kPermCap;
+    if (const char *e = std::getenv("DRONERL_PERM_LDS_CAP")) {
+        const int v = std::atoi(e);
+        if (v >= 0 && v < kPermCap) cap = v;
+    }
+    hipLaunchKernelGGL(perm_sort_kernel, dim3((unsigned)g.B), dim3(kBlock), 0, st, g, k0, k1,
+                       counter, counter_base, start, ids, keys, out, cap);
+    return check_launch("dr_permutation sort");
 }
 
 int dr_permutation(int64_t n, uint64_t seed, uint64_t counter, int32_t *out,

@@ -140,14 +140,14 @@ class PPOTrainer:
         # iteration (DRONERL_ROLLOUT_GRAPH=0: always eager)
         self.rollout_graph = os.environ.get("DRONERL_ROLLOUT_GRAPH", "1") != "0"
         self._rgraph, self._rwarm, self._rkey = None, False, None
-        # likewise PPO.train's minibatch loop (single-GPU fused path), for
-        # minibatches of at most 8192 rows: there the Python launch path is
-        # the bottleneck (the reference's 64-row minibatches); larger ones
-        # keep the GPU busy on their own, and a capture at configs[2] size
-        # (65,536-row minibatches, two trainers in one process) ended in a GPU
-        # memory fault once, so it stays eager.  DRONERL_TRAIN_GRAPH=0: never.
-        self.train_graph = (os.environ.get("DRONERL_TRAIN_GRAPH", "1") != "0" and
-                            cfg.batch_size <= 8192)
+        # likewise PPO.train's minibatch loop (single-GPU fused path): one
+        # replay per iteration instead of ~15 launches per optimizer step from
+        # Python (the reference's 64-row minibatches are launch-bound).  Every
+        # kernel in it keeps no state across launches (the permutation is this
+        # library's bucket sort: rocPRIM's onesweep radix sort, used in round
+        # 1, faulted on the second replay of a captured graph at configs[2]
+        # size).  DRONERL_TRAIN_GRAPH=0: always eager.
+        self.train_graph = os.environ.get("DRONERL_TRAIN_GRAPH", "1") != "0"
         self._tgraph, self._twarm, self._tstats, self._tkey = None, False, None, None
         self._ctr = torch.zeros(1, dtype=torch.int64, device=dev)
         # optional TrajectoryTensorboardCallback equivalent (trajectory.py)

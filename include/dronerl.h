@@ -232,8 +232,10 @@ int dr_policy_sample_dev(int64_t n, const float *mean, const float *log_std,
                          void *stream);
 
 /* Uniform random permutation of [0,n) (RolloutBuffer.get's
-   np.random.permutation): sort-by-random-key with a hipCUB radix sort.
-   dr_permutation_workspace_bytes gives the scratch size for n. */
+   np.random.permutation): the stable argsort of 64-bit Philox keys, by a
+   bucket pass on the top key bits plus per-bucket bitonic sorts (no state
+   kept across launches: graph-capturable).  dr_permutation_workspace_bytes
+   gives the scratch size for n. */
 size_t dr_permutation_workspace_bytes(int64_t n);
 int dr_permutation(int64_t n, uint64_t seed, uint64_t counter, int32_t *out,
                    void *workspace, size_t workspace_bytes, void *stream);

@@ -131,3 +131,33 @@ def gae(rew, val, starts, last_val, last_done, gamma, lam):
                          _p(last_val), _p(last_done), ctypes.c_double(gamma),
                          ctypes.c_double(lam), _p(adv), _p(ret))
     return adv, ret
+
+
+def philox_np(ctr, key):
+    """Philox4x32-10 over rows of counters: ctr (n,4) uint32, key (2,) ->
+    (n,4) uint32; the vectorised form of `philox` (numpy, for large test
+    vectors), following drone_rl_amd/csrc/common.h philox4x32_10."""
+    c = np.array(ctr, np.uint64).reshape(-1, 4) & 0xffffffff
+    k0, k1 = np.uint64(key[0] & 0xffffffff), np.uint64(key[1] & 0xffffffff)
+    m0, m1 = np.uint64(0xD2511F53), np.uint64(0xCD9E8D57)
+    w0, w1 = np.uint64(0x9E3779B9), np.uint64(0xBB67AE85)
+    mask, sh = np.uint64(0xffffffff), np.uint64(32)
+    x, y, z, w = c[:, 0], c[:, 1], c[:, 2], c[:, 3]
+    for _ in range(10):
+        p0, p1 = m0 * x, m1 * z
+        x, y, z, w = ((p1 >> sh) ^ y ^ k0) & mask, p1 & mask, ((p0 >> sh) ^ w ^ k1) & mask, \
+            p0 & mask
+        k0, k1 = (k0 + w0) & mask, (k1 + w1) & mask
+    return np.stack([x, y, z, w], 1).astype(np.uint32)
+
+
+def permutation_np(n, seed, counter):
+    """dr_permutation's result restated: the stable argsort of the 64-bit
+    Philox keys (r.x << 32 | r.y) of counters (i, counter, TAG_PERM)."""
+    i = np.arange(n, dtype=np.uint64)
+    ctr = np.stack([i & np.uint64(0xffffffff), i >> np.uint64(32),
+                    np.full(n, counter & 0xffffffff, np.uint64),
+                    np.full(n, 0x50000000 ^ (counter >> 32), np.uint64)], 1)
+    r = philox_np(ctr, [seed & 0xffffffff, seed >> 32]).astype(np.uint64)
+    keys = (r[:, 0] << np.uint64(32)) | r[:, 1]
+    return np.argsort(keys, kind="stable").astype(np.int32)

@@ -212,18 +212,22 @@ def test_tuned_gemms_load_and_are_deterministic():
     tr.close()
 
 
-@pytest.mark.parametrize("cfg", ["small", "sb3_1env"])
+@pytest.mark.parametrize("cfg", ["small", "sb3_1env", "configs2"])
 def test_rollout_graph_is_bitwise_eager(cfg):
     """The rollout loop and PPO.train's minibatch loop captured into
     hipGraphs (after one eager warm-up iteration; the policy-noise and
     permutation counter bases and Adam's bias-correction schedule live on the
     device) replay to bitwise the eager rollouts and updates over several
-    PPO iterations."""
+    PPO iterations -- including configs[2] itself (65,536 envs, 2x256,
+    65,536-row minibatches x 32 x 10 epochs per graph), where round 1's
+    rocPRIM-sorted permutation faulted on the second replay."""
     from drone_rl_amd.ppo import PPOConfig, PPOTrainer
 
     def make(graph):
         if cfg == "small":
             tr = _trainer()
+        elif cfg == "configs2":
+            tr = PPOTrainer(PPOConfig(seed=3))
         else:
             tr = PPOTrainer(PPOConfig.sb3_defaults(n_steps=128, seed=3))
         tr.rollout_graph = tr.train_graph = graph

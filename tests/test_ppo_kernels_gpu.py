@@ -68,6 +68,61 @@ def test_permutation_valid_and_matches_philox_sort():
                        torch.arange(1 << 21, device="cuda"))
 
 
+@pytest.mark.parametrize("n", [1, 2, 1000, 1025, 4097, 70001, 1 << 21])
+def test_permutation_is_the_stable_key_argsort(n):
+    """Bucket pass + per-bucket bitonic sorts == the stable argsort of the
+    64-bit Philox keys (oracle/cref.permutation_np), at ragged sizes and at
+    configs[2]'s 32 x 65,536 rollout rows; bitwise deterministic."""
+    from drone_rl_amd import ppo_kernels as K
+    p = K.Permuter(n, "cuda")
+    got = p(seed=0x1234567890, counter=(7 << 32) + 5).cpu().numpy()
+    np.testing.assert_array_equal(got, cref.permutation_np(n, 0x1234567890, (7 << 32) + 5))
+    again = p(seed=0x1234567890, counter=(7 << 32) + 5, out=torch.empty_like(p.out))
+    assert np.array_equal(again.cpu().numpy(), got)
+
+
+def test_permutation_global_scratch_path(monkeypatch):
+    """Buckets above the LDS capacity sort in global scratch (forced here by
+    DRONERL_PERM_LDS_CAP; unreachable in practice at a mean of <= 1024)."""
+    from drone_rl_amd import ppo_kernels as K
+    for cap in ("0", "700"):
+        monkeypatch.setenv("DRONERL_PERM_LDS_CAP", cap)
+        n = 9000
+        got = K.Permuter(n, "cuda")(seed=3, counter=11).cpu().numpy()
+        np.testing.assert_array_equal(got, cref.permutation_np(n, 3, 11))
+
+
+def test_permutation_graph_replays_are_fresh():
+    """The permutation captured into a hipGraph (counter base on the device)
+    replays to the eager permutation of each new counter, at configs[2]'s
+    2,097,152 rows and 10 epochs per graph (rocPRIM's radix sort faulted on
+    the second replay of such a graph; the bucket sort keeps no state)."""
+    from drone_rl_amd import ppo_kernels as K
+    n, E = 1 << 21, 10
+    p = K.Permuter(n, "cuda")
+    ctr = torch.zeros(1, dtype=torch.int64, device="cuda")
+    outs = torch.zeros(E, n, dtype=torch.int32, device="cuda")
+
+    def body():
+        for e in range(E):
+            p.dev(seed=7, counter_base=ctr, counter_offset=e, out=outs[e])
+    body()
+    torch.cuda.synchronize()
+    cs = torch.cuda.Stream()
+    cs.wait_stream(torch.cuda.current_stream())
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.stream(cs), torch.cuda.graph(g, stream=cs):
+        body()
+    torch.cuda.current_stream().wait_stream(cs)
+    for it in range(3):
+        ctr.fill_(it * E)
+        g.replay()
+        torch.cuda.synchronize()
+        for e in (0, E - 1):
+            ref = p(seed=7, counter=it * E + e, out=torch.empty_like(p.out))
+            assert torch.equal(ref, outs[e]), (it, e)
+
+
 def test_gather_rows_exact():
     from drone_rl_amd import ppo_kernels as K
     src = torch.randn(100_000, 15, device="cuda")
