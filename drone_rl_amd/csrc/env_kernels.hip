@@ -43,7 +43,8 @@ constexpr double kDt = 0.02;
 
 // DR_ABLATE (diagnostic builds only, scripts/micro/ablate.sh; never set in
 // the product build): 1 = f32 trig, 2 = no auto-reset, 3 = no LDS obs
-// staging, 4 = divides by reciprocal multiplies, 5 = constant reset draws.
+// staging, 4 = divides by reciprocal multiplies, 5 = constant reset draws,
+// 6 = no physics.
 #ifndef DR_ABLATE
 #define DR_ABLATE 0
 #endif
@@ -223,6 +224,35 @@ struct EnvView {
     __host__ __device__ S *field(int k) const { return f + k * stride; }
 };
 
+// Byte offsets of the per-env arrays inside a handle's one allocation of
+// `sp` (stride) elements per array: F_N state arrays of S, then eps (f64),
+// step, ep_num (i32), the VecMonitor return (f32) and length (i32), then the
+// moving variant's 9 f32 motion arrays.  Shared by view_of and the step
+// kernel, which forms its array bases from (f, stride) in scalar registers.
+template <typename S>
+struct Layout {
+    __host__ __device__ static int64_t eps(int64_t sp) { return (int64_t)F_N * sp * sizeof(S); }
+    __host__ __device__ static int64_t step(int64_t sp) { return eps(sp) + sp * 8; }
+    __host__ __device__ static int64_t ep_num(int64_t sp) { return step(sp) + sp * 4; }
+    __host__ __device__ static int64_t ep_ret(int64_t sp) { return ep_num(sp) + sp * 4; }
+    __host__ __device__ static int64_t ep_len(int64_t sp) { return ep_ret(sp) + sp * 4; }
+    __host__ __device__ static int64_t mot(int64_t sp) { return ep_len(sp) + sp * 4; }
+};
+
+// The step kernel's per-field base pointers (f + k * stride), passed as
+// separate uniform kernel arguments so each SoA access is an SGPR base plus
+// one shared 32-bit lane offset (the compiler folds f + k*stride + i*8 into
+// per-field 64-bit VGPR address arithmetic otherwise).  Kernel-argument
+// preloading into SGPRs (gfx950) was measured as the alternative: slower by
+// 0.1 us at 65,536 envs (the scalar address chain it needs costs more than
+// the one scalar-load round trip it saves).
+template <typename S>
+struct FieldPtrs {
+    S *p[F_N];
+    int32_t *step, *ep_num;
+    double *eps;
+};
+
 struct StepIO {
     const float *actions;
     float *obs;
@@ -400,6 +430,13 @@ __device__ inline void make_obs(const S st[F_N], float ob[OD],
 template <typename S, int VAR>
 __device__ inline S physics_step(S st[F_N], float4 act, S dt, bool &crash) {
     const float a0 = act.x, a1 = act.y, a2 = act.z, a3 = act.w;
+#if DR_ABLATE == 6
+    // diagnostic: no physics (loads / stores / reset / obs as built)
+#pragma unroll
+    for (int k = 0; k < 12; ++k) st[k] += (S)a0 * (S)1e-300;
+    crash = st[F_POS + 2] < (S)0;
+    return (S)a1;
+#endif
     // thrust / torques (drone.py:106, 113-117): f32 sums, f64 factor product,
     // the yaw torque stays f32.
     const float thr = ((a0 + a1) + a2) + a3;
@@ -533,146 +570,193 @@ __device__ inline void store_obs_block(float *sh, const float ob[OD],
     }
 }
 
+// Element i of a per-env array at a uniform (SGPR) base: the byte offset
+// i * sizeof(T) is formed in 32 bits (dr_create caps a handle at 2^28 envs),
+// so every SoA access of a wave is one `global_load/store ... v_off, s[base]`
+// sharing ONE offset VGPR per element size, with no per-field 64-bit address
+// arithmetic ahead of the loads.
+template <typename T>
+__device__ inline T *at(T *base, int64_t i) {
+    return reinterpret_cast<T *>(reinterpret_cast<char *>(base) +
+                                 (uint32_t)((uint32_t)i * (uint32_t)sizeof(T)));
+}
+template <typename T>
+__device__ inline const T *at(const T *base, int64_t i) {
+    return reinterpret_cast<const T *>(reinterpret_cast<const char *>(base) +
+                                       (uint32_t)((uint32_t)i * (uint32_t)sizeof(T)));
+}
+
 // HU: reset draws from the host-uniform ring (parity mode).  A template
 // parameter, not a runtime branch, so the Philox reset path holds no global
 // load: a load there would make the waitcnt pass drain every outstanding
 // store of the wave (vmcnt counts stores too) before the reset could finish.
+//
+// Entry: lanes past the batch end (ragged n, half-populated waves) load the
+// last env's row instead of branching around the loads and only their
+// stores are masked, so the kernel's first basic block holds every
+// kernel-argument load and every state load: one scalar-load round trip
+// before the first global load is issued, not two.
 template <typename S, int VAR, bool MON, int RPW, bool HU, bool NTL>
 __global__ __launch_bounds__(kEnvBlock) void env_step_kernel(EnvView<S> v,
-                                                             StepIO io) {
+                                                             StepIO io, FieldPtrs<S> fp) {
     constexpr int OD = VAR == DR_VARIANT_GYM ? 15 : (VAR == DR_VARIANT_MOVING ? 18 : 12);
     constexpr bool GYMLIKE = VAR != DR_VARIANT_VECTORIZED;
     __shared__ float4 sh4[kEnvBlock * OD / 4];
+    // Every kernel argument the state loads need is materialised here, in
+    // ONE batch of scalar loads: the compiler otherwise issues them in three
+    // dependent rounds (n, then the field pointers, then the rest), each a
+    // full scalar-memory round trip ahead of the first state load.
+    asm volatile("" ::"s"(v.n), "s"(fp.p[0]), "s"(fp.p[1]), "s"(fp.p[2]), "s"(fp.p[3]),
+                 "s"(fp.p[4]), "s"(fp.p[5]), "s"(fp.p[6]), "s"(fp.p[7]), "s"(fp.p[8]),
+                 "s"(fp.p[9]), "s"(fp.p[10]), "s"(fp.p[11]), "s"(fp.p[12]), "s"(fp.p[13]),
+                 "s"(fp.p[14]), "s"(io.actions), "s"(fp.step), "s"(fp.ep_num), "s"(fp.eps));
+    __builtin_amdgcn_sched_barrier(0);
+    const int64_t n_ = v.n;
+    const float4 *const actions = reinterpret_cast<const float4 *>(io.actions);
+    int32_t *const p_step = fp.step;
+    int32_t *const p_epn = fp.ep_num;
+    double *const p_eps = fp.eps;
     const int64_t base = (int64_t)blockIdx.x * (DR_ENV_WPB * RPW);
     const int lane_ = threadIdx.x & 63;
     // env of this lane; lanes >= RPW of a half-populated wave own none
-    const int64_t i = lane_ < RPW ? base + (threadIdx.x >> 6) * RPW + lane_ : v.n;
+    const int64_t i_own = lane_ < RPW ? base + (threadIdx.x >> 6) * RPW + lane_ : n_;
+    const bool live = i_own < n_;
+    const int64_t i = live ? i_own : n_ - 1;           // in-bounds row for dead lanes
     DR_STAMP(0);
     float ob[OD];
-    if (i < v.n) {
-        S st[F_N];
-        int32_t ep_old = 0;
-        if constexpr (GYMLIKE && DR_HOIST_RESET) ep_old = v.ep_num[i];
-        // Issue order = landing order: euler and omega first so the three
-        // sincos range reductions start while pos / vel / target are still
-        // in flight (s_waitcnt vmcnt counts oldest-first).
+    S st[F_N];
+    int32_t ep_old = 0;
+    if constexpr (GYMLIKE && DR_HOIST_RESET) ep_old = *at(p_epn, i);
+    // Issue order = landing order: euler and omega first so the three
+    // sincos range reductions start while pos / vel / target are still in
+    // flight (s_waitcnt vmcnt counts oldest-first).
 #pragma unroll
-        for (int k = F_EUL; k < F_EUL + 6; ++k) st[k] = ld_in<NTL>(&v.field(k)[i]);
-        const float4 act = reinterpret_cast<const float4 *>(io.actions)[i];
+    for (int k = F_EUL; k < F_EUL + 3; ++k) st[k] = ld_in<NTL>(at(fp.p[k], i));
+    __builtin_amdgcn_sched_barrier(0);     // keep the issue order (euler first)
 #pragma unroll
-        for (int k = 0; k < F_EUL; ++k) st[k] = ld_in<NTL>(&v.field(k)[i]);
-        S cen[3];
-        float mp[9], tvel[3];
-        if constexpr (VAR == DR_VARIANT_GYM) {
+    for (int k = F_OMG; k < F_OMG + 3; ++k) st[k] = ld_in<NTL>(at(fp.p[k], i));
+    const float4 act = *at(actions, i);
+    __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-            for (int k = F_TGT; k < F_N; ++k) st[k] = ld_in<NTL>(&v.field(k)[i]);
-        } else if constexpr (VAR == DR_VARIANT_MOVING) {
+    for (int k = 0; k < F_EUL; ++k) st[k] = ld_in<NTL>(at(fp.p[k], i));
+    S cen[3];
+    float mp[9], tvel[3];
+    if constexpr (VAR == DR_VARIANT_GYM) {
 #pragma unroll
-            for (int k = 0; k < 3; ++k) cen[k] = v.field(F_TGT + k)[i];
+        for (int k = F_TGT; k < F_N; ++k) st[k] = ld_in<NTL>(at(fp.p[k], i));
+    } else if constexpr (VAR == DR_VARIANT_MOVING) {
 #pragma unroll
-            for (int k = 0; k < 9; ++k) mp[k] = v.mot[k * v.stride + i];
-        } else {
-            st[F_TGT + 0] = (S)0;
-            st[F_TGT + 1] = (S)0;
-            st[F_TGT + 2] = (S)10.0;
-        }
-        int32_t step = ld_in<NTL>(&v.step[i]);
-        // needed only if this env resets; loaded up front so a reset does
-        // not stall the wave on a dependent global load (+12 B per step,
-        // counted in the measured traffic, not in the 305 B algorithmic)
-        double eps_old = 0.0;
-        if constexpr (GYMLIKE) {
-            if (!DR_HOIST_RESET) ep_old = v.ep_num[i];
-            if (DR_PREFETCH_EPS) eps_old = v.eps[i];
-        }
-        // VecMonitor counters: also loaded up front (a load after the
-        // physics would put one more full memory latency on every wave)
-        float ret0 = 0.f;
-        int32_t len0 = 0;
-        if constexpr (MON) {
-            ret0 = v.ep_ret[i];
-            len0 = v.ep_len[i];
-        }
-        // Every load is issued before any arithmetic: without this the
-        // scheduler interleaves the first sincos with the loads and its
-        // s_waitcnt holds back the issue of the remaining ones by a full
-        // memory latency.
-        __builtin_amdgcn_sched_barrier(0);
-        u32x4 pre0{};
-        if constexpr (VAR == DR_VARIANT_GYM && DR_HOIST_RESET) {
-            if constexpr (!HU) {
-                const uint64_t gid = (uint64_t)(v.env_id_offset + i);
-                pre0 = philox4x32_10(u32x4{(uint32_t)(ep_old + 1), (uint32_t)gid,
-                                           (uint32_t)(gid >> 32), TAG_RESET},
-                                     v.seed_lo, v.seed_hi);
-            }
-        }
-        if constexpr (VAR == DR_VARIANT_MOVING) {
-            // the reward and obs of this step see the target at the NEW step
-            moving_target(cen, mp, step + 1, (float)v.dt, &st[F_TGT], tvel);
-        }
-
-        bool crash;
-        const S r = physics_step<S, VAR>(st, act, v.dt, crash);
-        DR_STAMP(2);
-        step += 1;                                         // (155)
-        bool done = crash || (step >= v.max_steps);        // (156-157)
-        const float rf = (float)r;                         // SB3 f32 buffer
-        st_out(&io.rew[i], rf);
-        st_out(&io.done[i], (uint8_t)done);
-        make_obs<S, OD>(st, ob, tvel);
-
-        float ret = 0.f;
-        int32_t len = 0;
-        if constexpr (MON) {
-            ret = ret0 + rf;                               // VecMonitor
-            len = len0 + 1;
-        }
-        if constexpr (GYMLIKE) {
-            if (done && io.auto_reset && DR_ABLATE != 2) {
-                // DummyVecEnv: keep the terminal obs, reset in the same step.
-                if (io.term_obs) {
+        for (int k = 0; k < 3; ++k) cen[k] = *at(fp.p[F_TGT + k], i);
 #pragma unroll
-                    for (int k = 0; k < OD; ++k) io.term_obs[i * OD + k] = ob[k];
-                }
-                step = 0;
-                if constexpr (VAR == DR_VARIANT_GYM) {
-                    gym_reset_regs(v, i, HU ? 1 : 0, st, ep_old, eps_old,
-                                   DR_HOIST_RESET ? &pre0 : nullptr);
-#pragma unroll
-                    for (int k = F_TGT; k < F_N; ++k) v.field(k)[i] = st[k];
-                } else {
-                    moving_reset_regs(v, i, HU ? 1 : 0, st, cen, mp, ep_old, eps_old);
-#pragma unroll
-                    for (int k = 0; k < 3; ++k) v.field(F_TGT + k)[i] = cen[k];
-#pragma unroll
-                    for (int k = 0; k < 9; ++k) v.mot[k * v.stride + i] = mp[k];
-                    moving_target(cen, mp, 0, (float)v.dt, &st[F_TGT], tvel);
-                }
-                make_obs<S, OD>(st, ob, tvel);
-            }
-        }
-        if constexpr (MON) {
-            if (done) {           // VecMonitor: report, then restart counters
-                io.ep_ret_out[i] = ret;
-                io.ep_len_out[i] = len;
-                ret = 0.f;
-                len = 0;
-            }
-            v.ep_ret[i] = ret;
-            v.ep_len[i] = len;
-        }
-        DR_STAMP(3);
-#pragma unroll
-        for (int k = 0; k < 12; ++k) st_out(&v.field(k)[i], st[k]);
-        st_out(&v.step[i], step);
-        DR_STAMP(4);
+        for (int k = 0; k < 9; ++k) mp[k] = *at(v.mot + k * v.stride, i);
     } else {
+        st[F_TGT + 0] = (S)0;
+        st[F_TGT + 1] = (S)0;
+        st[F_TGT + 2] = (S)10.0;
+    }
+    int32_t step = ld_in<NTL>(at(p_step, i));
+    // needed only if this env resets; loaded up front so a reset does not
+    // stall the wave on a dependent global load (+12 B per step, counted in
+    // the measured traffic, not in the 305 B algorithmic)
+    double eps_old = 0.0;
+    if constexpr (GYMLIKE) {
+        if (!DR_HOIST_RESET) ep_old = *at(p_epn, i);
+        if (DR_PREFETCH_EPS) eps_old = *at(p_eps, i);
+    }
+    // VecMonitor counters: also loaded up front (a load after the physics
+    // would put one more full memory latency on every wave)
+    float ret0 = 0.f;
+    int32_t len0 = 0;
+    if constexpr (MON) {
+        ret0 = *at(v.ep_ret, i);
+        len0 = *at(v.ep_len, i);
+    }
+    // Every load is issued before any arithmetic: without this the
+    // scheduler interleaves the first sincos with the loads and its
+    // s_waitcnt holds back the issue of the remaining ones by a full memory
+    // latency.
+    __builtin_amdgcn_sched_barrier(0);
+    u32x4 pre0{};
+    if constexpr (VAR == DR_VARIANT_GYM && DR_HOIST_RESET) {
+        if constexpr (!HU) {
+            const uint64_t gid = (uint64_t)(v.env_id_offset + i);
+            pre0 = philox4x32_10(u32x4{(uint32_t)(ep_old + 1), (uint32_t)gid,
+                                       (uint32_t)(gid >> 32), TAG_RESET},
+                                 v.seed_lo, v.seed_hi);
+        }
+    }
+    if constexpr (VAR == DR_VARIANT_MOVING) {
+        // the reward and obs of this step see the target at the NEW step
+        moving_target(cen, mp, step + 1, (float)v.dt, &st[F_TGT], tvel);
+    }
+
+    bool crash;
+    const S r = physics_step<S, VAR>(st, act, v.dt, crash);
+    DR_STAMP(2);
+    step += 1;                                             // (155)
+    const bool done = live && (crash || (step >= v.max_steps));   // (156-157)
+    const float rf = (float)r;                             // SB3 f32 buffer
+    if (live) {
+        st_out(at(io.rew, i), rf);
+        st_out(at(io.done, i), (uint8_t)done);
+    }
+    make_obs<S, OD>(st, ob, tvel);
+
+    float ret = 0.f;
+    int32_t len = 0;
+    if constexpr (MON) {
+        ret = ret0 + rf;                                   // VecMonitor
+        len = len0 + 1;
+    }
+    if constexpr (GYMLIKE) {
+        if (done && io.auto_reset && DR_ABLATE != 2) {
+            // DummyVecEnv: keep the terminal obs, reset in the same step.
+            if (io.term_obs) {
+#pragma unroll
+                for (int k = 0; k < OD; ++k) io.term_obs[i * OD + k] = ob[k];
+            }
+            step = 0;
+            if constexpr (VAR == DR_VARIANT_GYM) {
+                gym_reset_regs(v, i, HU ? 1 : 0, st, ep_old, eps_old,
+                               DR_HOIST_RESET ? &pre0 : nullptr);
+#pragma unroll
+                for (int k = F_TGT; k < F_N; ++k) *at(fp.p[k], i) = st[k];
+            } else {
+                moving_reset_regs(v, i, HU ? 1 : 0, st, cen, mp, ep_old, eps_old);
+#pragma unroll
+                for (int k = 0; k < 3; ++k) *at(fp.p[F_TGT + k], i) = cen[k];
+#pragma unroll
+                for (int k = 0; k < 9; ++k) *at(v.mot + k * v.stride, i) = mp[k];
+                moving_target(cen, mp, 0, (float)v.dt, &st[F_TGT], tvel);
+            }
+            make_obs<S, OD>(st, ob, tvel);
+        }
+    }
+    if constexpr (MON) {
+        if (done) {               // VecMonitor: report, then restart counters
+            *at(io.ep_ret_out, i) = ret;
+            *at(io.ep_len_out, i) = len;
+            ret = 0.f;
+            len = 0;
+        }
+        if (live) {
+            *at(v.ep_ret, i) = ret;
+            *at(v.ep_len, i) = len;
+        }
+    }
+    DR_STAMP(3);
+    if (live) {
+#pragma unroll
+        for (int k = 0; k < 12; ++k) st_out(at(fp.p[k], i), st[k]);
+        st_out(at(p_step, i), step);
+    }
+    DR_STAMP(4);
+    if (!live) {
 #pragma unroll
         for (int k = 0; k < OD; ++k) ob[k] = 0.f;
     }
 #if DR_ABLATE == 3
-    if (i < v.n) {
+    if (live) {
 #pragma unroll
         for (int k = 0; k < OD; ++k) io.obs[i * OD + k] = ob[k];
     }
@@ -1107,18 +1191,13 @@ EnvView<S> view_of(const dr_handle *h) {
     const int64_t sp = h->stride;
     v.f = reinterpret_cast<S *>(m);
     v.stride = sp;
-    m += (size_t)F_N * sp * sizeof(S);
-    v.eps = reinterpret_cast<double *>(m);
-    m += sp * sizeof(double);
-    v.step = reinterpret_cast<int32_t *>(m);
-    m += sp * sizeof(int32_t);
-    v.ep_num = reinterpret_cast<int32_t *>(m);
-    m += sp * sizeof(int32_t);
-    v.ep_ret = reinterpret_cast<float *>(m);
-    m += sp * sizeof(float);
-    v.ep_len = reinterpret_cast<int32_t *>(m);
-    m += sp * sizeof(int32_t);
-    v.mot = h->cfg.variant == DR_VARIANT_MOVING ? reinterpret_cast<float *>(m) : nullptr;
+    v.eps = reinterpret_cast<double *>(m + Layout<S>::eps(sp));
+    v.step = reinterpret_cast<int32_t *>(m + Layout<S>::step(sp));
+    v.ep_num = reinterpret_cast<int32_t *>(m + Layout<S>::ep_num(sp));
+    v.ep_ret = reinterpret_cast<float *>(m + Layout<S>::ep_ret(sp));
+    v.ep_len = reinterpret_cast<int32_t *>(m + Layout<S>::ep_len(sp));
+    v.mot = h->cfg.variant == DR_VARIANT_MOVING ? reinterpret_cast<float *>(m + Layout<S>::mot(sp))
+                                                 : nullptr;
     v.n = h->n;
     v.env_id_offset = h->cfg.env_id_offset;
     v.host_u = h->host_u;
@@ -1165,6 +1244,11 @@ int dispatch_reset(dr_handle *h, const uint8_t *mask, float *obs, int mode,
 template <typename S, int VAR, bool MON>
 int launch_step(dr_handle *h, const StepIO &io, hipStream_t st) {
     EnvView<S> v = view_of<S>(h);
+    FieldPtrs<S> fp;
+    for (int k = 0; k < F_N; ++k) fp.p[k] = v.field(k);
+    fp.step = v.step;
+    fp.ep_num = v.ep_num;
+    fp.eps = v.eps;
     bool launched = false;
     if constexpr (VAR != DR_VARIANT_MOVING) {  // the quad A/B kernel has no moving form
         if (h->quad) {
@@ -1177,11 +1261,11 @@ int launch_step(dr_handle *h, const StepIO &io, hipStream_t st) {
         if (h->rpw == 32)
             hipLaunchKernelGGL((env_step_kernel<S, VAR, MON, 32, true, false>),
                                dim3(grid_for(h->n, DR_ENV_WPB * 32)), dim3(kEnvBlock), 0, st,
-                               v, io);
+                               v, io, fp);
         else
             hipLaunchKernelGGL((env_step_kernel<S, VAR, MON, 64, true, false>),
                                dim3(grid_for(h->n, DR_ENV_WPB * 64)), dim3(kEnvBlock), 0, st,
-                               v, io);
+                               v, io, fp);
         launched = true;
     }
     if (!launched) {
@@ -1189,19 +1273,19 @@ int launch_step(dr_handle *h, const StepIO &io, hipStream_t st) {
         switch (h->rpw * 2 + (int)h->nt_loads) {
             case 64:
                 hipLaunchKernelGGL((env_step_kernel<S, VAR, MON, 32, false, false>), g32,
-                                   dim3(kEnvBlock), 0, st, v, io);
+                                   dim3(kEnvBlock), 0, st, v, io, fp);
                 break;
             case 65:
                 hipLaunchKernelGGL((env_step_kernel<S, VAR, MON, 32, false, true>), g32,
-                                   dim3(kEnvBlock), 0, st, v, io);
+                                   dim3(kEnvBlock), 0, st, v, io, fp);
                 break;
             case 129:
                 hipLaunchKernelGGL((env_step_kernel<S, VAR, MON, 64, false, true>), g64,
-                                   dim3(kEnvBlock), 0, st, v, io);
+                                   dim3(kEnvBlock), 0, st, v, io, fp);
                 break;
             default:
                 hipLaunchKernelGGL((env_step_kernel<S, VAR, MON, 64, false, false>), g64,
-                                   dim3(kEnvBlock), 0, st, v, io);
+                                   dim3(kEnvBlock), 0, st, v, io, fp);
         }
     }
     hipError_t e = hipGetLastError();
@@ -1249,8 +1333,10 @@ int dr_create(const dr_config *cfg_in, dr_handle **out) {
         return fail(nullptr, DR_ERR_INVALID, "dr_create: unknown state_dtype");
     if (cfg.rng_mode != DR_RNG_PHILOX && cfg.rng_mode != DR_RNG_HOST_UNIFORMS)
         return fail(nullptr, DR_ERR_INVALID, "dr_create: unknown rng_mode");
-    if (cfg.num_envs > (int64_t)1 << 31)
-        return fail(nullptr, DR_ERR_INVALID, "dr_create: num_envs above 2^31 per handle");
+    // 32-bit per-array byte offsets in the step kernel (float4 actions:
+    // 16 B x 2^28 = 4 GiB); shard larger batches over several handles
+    if (cfg.num_envs > (int64_t)1 << 28)
+        return fail(nullptr, DR_ERR_INVALID, "dr_create: num_envs above 2^28 per handle");
     if (cfg.max_steps == 0) cfg.max_steps = cfg.variant == DR_VARIANT_VECTORIZED ? 1000 : 200;
     if (cfg.max_steps < 0) return fail(nullptr, DR_ERR_INVALID, "dr_create: max_steps < 0");
     if (cfg.dt == 0.0) cfg.dt = kDt;

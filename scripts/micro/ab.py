@@ -20,8 +20,9 @@ from drone_rl_amd import _lib  # noqa: E402
 def load(path):
     L = ctypes.CDLL(path)
     for name, (res, args) in _lib.SIGNATURES.items():
-        f = getattr(L, name)
-        f.restype, f.argtypes = res, args
+        f = getattr(L, name, None)       # env-only diagnostic builds lack the PPO ABI
+        if f is not None:
+            f.restype, f.argtypes = res, args
     return L
 
 
