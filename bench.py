@@ -54,6 +54,8 @@ def parse():
     ap.add_argument("--ppo-updates", type=int, default=3,
                     help="timed PPO iterations for configs[2] (0 = skip)")
     ap.add_argument("--ppo-epochs", type=int, default=10)
+    ap.add_argument("--grad-buckets", type=int, choices=[1, 2], default=1,
+                    help="data-parallel gradient all-reduces per optimizer step")
     ap.add_argument("--ppo-steps", type=int, default=32, help="rollout length T")
     ap.add_argument("--extra", action="store_true",
                     help="also time the f32-state mode and the 4M-env size")
@@ -175,7 +177,8 @@ def time_ppo(args, rank, world, device):
 
     from drone_rl_amd.ppo import PPOConfig, PPOTrainer
     cfg = PPOConfig(num_envs=args.envs, n_steps=args.ppo_steps, batch_size=args.envs,
-                    n_epochs=args.ppo_epochs, state_dtype=args.state_dtype, seed=0)
+                    n_epochs=args.ppo_epochs, state_dtype=args.state_dtype, seed=0,
+                    grad_buckets=args.grad_buckets)
     tr = PPOTrainer(cfg, device=device, rank=rank, world_size=world)
     # warm-up: the eager iteration, then the one that captures the rollout
     # graph (replayed by every timed iteration)
@@ -212,8 +215,10 @@ def time_ppo(args, rank, world, device):
                                 if tr.tuned_gemms else "hipBLASLt heuristic"),
                        "grad_allreduce": ({"nccl": "rccl"}.get(dist.get_backend(),
                                                                dist.get_backend())
-                                          + " (2 buckets, overlapped with the "
-                                            "first-layer backward)") if world > 1
+                                          + (" (2 buckets, the first overlapped with the "
+                                             "first-layer backward)" if cfg.grad_buckets == 2
+                                             else " (1 all-reduce of the flat gradient per "
+                                                  "optimizer step)")) if world > 1
                        else "none"},
             "last_update_stats": stats, "episodes": es}
 

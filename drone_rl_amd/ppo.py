@@ -66,6 +66,12 @@ class PPOConfig:
     eps_schedule: tuple = ()
     # look up the MI355X-tuned GEMM solutions (policy.use_tuned_gemms)
     tuned_gemms: bool = True
+    # data parallel (world > 1): RCCL all-reduces of the flat gradient per
+    # optimizer step.  1 = one all-reduce of the whole 564 KB buffer after
+    # the backward; 2 = everything but the first layer
+    # started asynchronously as soon as the fused backward finished it
+    # (overlapping the first-layer backward), the first layer at the end
+    grad_buckets: int = 1
 
     @classmethod
     def sb3_defaults(cls, **kw):
@@ -88,6 +94,8 @@ class PPOTrainer:
         N, T = cfg.num_envs, cfg.n_steps
         if (N * T) % cfg.batch_size:
             raise ValueError("num_envs * n_steps must be a multiple of batch_size")
+        if cfg.grad_buckets not in (1, 2):
+            raise ValueError("grad_buckets must be 1 or 2")
         dev = self.device
         self.tuned_gemms = use_tuned_gemms() if cfg.tuned_gemms else False
         self.env = DroneBatch(N, cfg.variant, device=dev, seed=cfg.seed,
@@ -327,11 +335,13 @@ class PPOTrainer:
                                        self.mb_act, self.mb_aux, adv_part=self.head.adv_part)
                     kw = dict(adv_ready=True, stats_out=stats[j])
                     if self.world > 1:
-                        # DP: the gradient all-reduce starts while the
-                        # first-layer backward is still running
+                        # DP: one all-reduce of the flat gradient, or (2
+                        # buckets) the early bucket started while the
+                        # first-layer backward still runs
                         bar = D.BucketedAllReduce(self.fused.grad, self.world, self.pg)
+                        early = bar.start if self.cfg.grad_buckets == 2 else None
                         grad, st = self.fused.step(self.mb_obs, self.mb_act, self.mb_aux,
-                                                   self.head, on_ready=bar.start, **kw)
+                                                   self.head, on_ready=early, **kw)
                         bar.finish()
                     elif self.defer_finish:
                         # single GPU: the head / first-layer / split-K

@@ -55,6 +55,9 @@ def main(argv=None):
     ap.add_argument("--traj-dir", default=None,
                     help="record env 0's trajectories like traj_tb.py (every 25th episode, "
                          "blocks of 500) into this directory (npz, PNG if matplotlib)")
+    ap.add_argument("--grad-buckets", type=int, choices=[1, 2], default=1,
+                    help="data parallel: 1 = one gradient all-reduce per optimizer step; "
+                         "2 = an early bucket overlapped with the first-layer backward")
     ap.add_argument("--reset-num-timesteps", action=argparse.BooleanOptionalAction,
                     default=True,
                     help="after a resume, train --total-steps more (SB3's default, the "
@@ -67,7 +70,7 @@ def main(argv=None):
     torch.cuda.set_device(local)
     if world > 1:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    common = dict(num_envs=a.envs, learning_rate=a.lr, seed=a.seed,
+    common = dict(num_envs=a.envs, learning_rate=a.lr, seed=a.seed, grad_buckets=a.grad_buckets,
                   state_dtype=a.state_dtype, variant=a.variant, initial_eps=a.initial_eps,
                   eps_schedule=tuple((int(u), float(e)) for u, e in
                                      (kv.split(":") for kv in a.eps_schedule.split(",") if kv)))

@@ -6,7 +6,7 @@ import subprocess
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB = os.path.join(_HERE, "build", "liboracle.so")
+LIB = os.environ.get("ORACLE_LIB", os.path.join(_HERE, "build", "liboracle.so"))
 _lib = None
 
 

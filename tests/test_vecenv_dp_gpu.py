@@ -109,13 +109,18 @@ def _free_port():
     return p
 
 
-def test_ppo_data_parallel_two_ranks():
+@pytest.mark.parametrize("worker", ["dp_worker.py", "dp_grad_worker.py"])
+def test_ppo_data_parallel_two_ranks(worker):
+    """dp_worker: two DP PPO iterations keep the ranks' parameters identical
+    on disjoint env shards; dp_grad_worker: the fused-kernel 2x256 gradient
+    all-reduced over 2 ranks x 16,384 rows (1 and 2 buckets) equals the
+    union-minibatch gradient."""
     port = str(_free_port())
     procs = []
     for r in range(2):
         env = dict(os.environ, RANK=str(r), WORLD_SIZE="2", LOCAL_RANK="0",
                    MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
-        procs.append(subprocess.Popen([sys.executable, os.path.join(ROOT, "tests", "dp_worker.py")],
+        procs.append(subprocess.Popen([sys.executable, os.path.join(ROOT, "tests", worker)],
                                       env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT))
     outs = []
     for p in procs:
