@@ -186,19 +186,45 @@ __global__ __launch_bounds__(kBlock) void perm_hist_kernel(
     for (int64_t b = threadIdx.x; b < g.B; b += kBlock) row[b] = sh_cnt[b];
 }
 
-// hist[t][b] -> exclusive running count over t; total[b]
+// hist[t][b] -> exclusive running count over t; total[b].  A block owns 64
+// buckets (coalesced 256 B rows of hist) and splits the tiles four ways; each
+// thread reads its counts in chunks of 16 independent loads (the in-place
+// rewrite would otherwise serialise every load behind the previous store).
+constexpr int kScanChunk = 16;
 __global__ __launch_bounds__(kBlock) void perm_scan_tiles_kernel(PermGeom g,
                                                                  uint32_t *__restrict__ hist,
                                                                  uint32_t *__restrict__ total) {
-    const int64_t b = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-    if (b >= g.B) return;
-    uint32_t run = 0;
-    for (int64_t t = 0; t < g.T; ++t) {
-        const uint32_t c = hist[t * g.B + b];
-        hist[t * g.B + b] = run;
-        run += c;
+    __shared__ uint32_t part[4][64];
+    const int bl = threadIdx.x & 63, grp = threadIdx.x >> 6;
+    const int64_t b = (int64_t)blockIdx.x * 64 + bl;
+    const int64_t tg = (g.T + 3) / 4;
+    const int64_t t0 = grp * tg, t1 = t0 + tg < g.T ? t0 + tg : g.T;
+    const bool ok = b < g.B;
+    uint32_t s = 0;
+    for (int64_t t = t0; t < t1; t += kScanChunk) {
+        uint32_t c[kScanChunk];
+#pragma unroll
+        for (int q = 0; q < kScanChunk; ++q)
+            c[q] = (ok && t + q < t1) ? hist[(t + q) * g.B + b] : 0u;
+#pragma unroll
+        for (int q = 0; q < kScanChunk; ++q) s += c[q];
     }
-    total[b] = run;
+    part[grp][bl] = s;
+    __syncthreads();
+    uint32_t run = 0;
+    for (int q = 0; q < grp; ++q) run += part[q][bl];
+    if (ok && grp == 3) total[b] = run + s;
+    for (int64_t t = t0; t < t1; t += kScanChunk) {
+        uint32_t c[kScanChunk];
+#pragma unroll
+        for (int q = 0; q < kScanChunk; ++q)
+            c[q] = (ok && t + q < t1) ? hist[(t + q) * g.B + b] : 0u;
+#pragma unroll
+        for (int q = 0; q < kScanChunk; ++q) {
+            if (ok && t + q < t1) hist[(t + q) * g.B + b] = run;
+            run += c[q];
+        }
+    }
 }
 
 // start[b] = exclusive scan of total, start[B] = n (one block of 1024)
@@ -249,36 +275,63 @@ __device__ inline bool perm_greater(uint64_t ka, int32_t ia, uint64_t kb, int32_
 // All-ascending bitonic sort of (key, id) pairs at [0, s), padded virtually
 // to the next power of two with +inf: every comparator puts the minimum at
 // the lower index, so padding (the suffix) never moves and is never read.
-template <typename KP, typename IP>
-__device__ inline void bitonic_sort_pairs(KP key, IP id, int64_t s) {
-    int64_t P = 1;
-    while (P < s) P <<= 1;
-    for (int64_t k = 2; k <= P; k <<= 1) {
-        for (int64_t j = k >> 1; j >= 1; j >>= 1) {
-            for (int64_t p = threadIdx.x; p < P / 2; p += kBlock) {
-                int64_t lo, hi;
-                if (j == (k >> 1)) {         // first merge step: mirrored pairs
-                    const int64_t blk = p / j, off = p - blk * j;
-                    lo = blk * k + off;
-                    hi = blk * k + k - 1 - off;
-                } else {
-                    lo = (p / j) * 2 * j + (p % j);
-                    hi = lo + j;
-                }
-                if (hi < s) {
-                    const uint64_t ka = key[lo], kb = key[hi];
-                    const int32_t ia = id[lo], ib = id[hi];
-                    if (perm_greater(ka, ia, kb, ib)) {
-                        key[lo] = kb;
-                        key[hi] = ka;
-                        id[lo] = ib;
-                        id[hi] = ia;
-                    }
-                }
+// In LDS, the steps whose pairs stay inside aligned 64-element segments (the
+// first merge step while k <= 64, every later one with j <= 32) run wave-local
+// -- each wave always owns the same segments and one wave's LDS operations
+// execute in order -- so only the steps that cross segments pay a workgroup
+// barrier (10 of 55 at 1,024 elements).  In global scratch every step ends
+// with a barrier.
+template <bool LDS, typename KP, typename IP>
+__device__ inline void bitonic_sort_pairs(KP key, IP id, int64_t s64) {
+    // k and j are powers of two: pair indices by shifts and masks (an int64
+    // division per comparator cost more than the whole comparator)
+    const int s = (int)s64;
+    int lp = 0;
+    while ((1 << lp) < s) ++lp;
+    const int P = 1 << lp;
+    auto cmpswap = [&](int lk, int lj, int p) {
+        int lo, hi;
+        if (lj == lk - 1) {          // first merge step: mirrored pairs
+            const int blk = p >> lj, off = p & ((1 << lj) - 1);
+            lo = (blk << lk) + off;
+            hi = (blk << lk) + (1 << lk) - 1 - off;
+        } else {
+            lo = ((p >> lj) << (lj + 1)) + (p & ((1 << lj) - 1));
+            hi = lo + (1 << lj);
+        }
+        if (hi < s) {
+            const uint64_t ka = key[lo], kb = key[hi];
+            const int32_t ia = id[lo], ib = id[hi];
+            if (perm_greater(ka, ia, kb, ib)) {
+                key[lo] = kb;
+                key[hi] = ka;
+                id[lo] = ib;
+                id[hi] = ia;
             }
-            __syncthreads();
+        }
+    };
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int nseg = (P + 63) / 64, seg_pairs = P < 64 ? P / 2 : 32;
+    bool pending = false;            // wave-local writes not yet seen block-wide
+    for (int lk = 1; lk <= lp; ++lk) {
+        for (int lj = lk - 1; lj >= 0; --lj) {
+            const bool local = LDS && (lj == lk - 1 ? lk <= 6 : lj <= 5);
+            if (local) {
+                // wave w: segments 2w + (lane >> 5) + 8 i, one pair per lane
+                for (int seg = 2 * w + (lane >> 5); seg < nseg; seg += 2 * (kBlock / 64))
+                    if ((lane & 31) < seg_pairs) cmpswap(lk, lj, seg * 32 + (lane & 31));
+                __builtin_amdgcn_wave_barrier();
+                asm volatile("" ::: "memory");   // no LDS access moves across
+                pending = true;
+            } else {
+                if (pending) __syncthreads();
+                pending = false;
+                for (int p = threadIdx.x; p < P / 2; p += kBlock) cmpswap(lk, lj, p);
+                __syncthreads();
+            }
         }
     }
+    if (pending) __syncthreads();
 }
 
 __global__ __launch_bounds__(kBlock) void perm_sort_kernel(
@@ -298,7 +351,7 @@ __global__ __launch_bounds__(kBlock) void perm_sort_kernel(
             sk[k] = perm_key(e, k0, k1, counter);
         }
         __syncthreads();
-        bitonic_sort_pairs(sk, si, s);
+        bitonic_sort_pairs<true>(sk, si, s);
         for (int64_t k = threadIdx.x; k < s; k += kBlock) out[base + k] = si[k];
     } else {
         // practically unreachable: the same network over global scratch
@@ -307,7 +360,7 @@ __global__ __launch_bounds__(kBlock) void perm_sort_kernel(
         int32_t *ii = ids + base;
         for (int64_t k = threadIdx.x; k < s; k += kBlock) kk[k] = perm_key(ii[k], k0, k1, counter);
         __syncthreads();
-        bitonic_sort_pairs(kk, ii, s);
+        bitonic_sort_pairs<false>(kk, ii, s);
         for (int64_t k = threadIdx.x; k < s; k += kBlock) out[base + k] = ii[k];
     }
 }
@@ -1599,7 +1652,7 @@ static int permutation_impl(int64_t n, uint64_t seed, const uint64_t *counter_ba
                        counter, counter_base, keys, hist);
     int rc = check_launch("dr_permutation hist");
     if (rc) return rc;
-    hipLaunchKernelGGL(perm_scan_tiles_kernel, dim3(grid_for(g.B)), dim3(kBlock), 0, st, g,
+    hipLaunchKernelGGL(perm_scan_tiles_kernel, dim3((unsigned)((g.B + 63) / 64)), dim3(kBlock), 0, st, g,
                        hist, total);
     if ((rc = check_launch("dr_permutation scan"))) return rc;
     hipLaunchKernelGGL(perm_scan_buckets_kernel, dim3(1), dim3(1024), 0, st, g, total, start);
