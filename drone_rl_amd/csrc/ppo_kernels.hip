@@ -679,6 +679,47 @@ __device__ inline void ppo_row(const RowLossConst &c, const float mu[4], const f
     }
 }
 
+// ppo_row's policy part (acc 0, 2, 3, 4..7 and gm) and value part (acc 1 and
+// gv), operation for operation, for kernels that evaluate them on different
+// waves.
+__device__ inline void ppo_row_policy(const RowLossConst &c, const float mu[4],
+                                      const float ac[4], float old_lp, float A, float gm[4],
+                                      float acc[kLossK]) {
+    float lp = 0.f, zz[4], dd[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const float d = ac[j] - mu[j];
+        dd[j] = d;
+        zz[j] = d / c.var[j];
+        lp += (-(d * d) / (2.0f * c.var[j]) - c.logsd[j]) - kLogSqrt2Pi;
+    }
+    if (c.normalize) A = (A - c.amean) / (c.astd + 1e-8f);
+    const float logr = lp - old_lp;
+    const float r = expf(logr);
+    const float rc = fminf(fmaxf(r, c.lo), c.hi);
+    const float l1 = A * r, l2 = A * rc;
+    acc[0] += -fminf(l1, l2);
+    const float g1 = l1 < l2 ? 1.f : (l1 == l2 ? 0.5f : 0.f);
+    const float g2 = l2 < l1 ? 1.f : (l1 == l2 ? 0.5f : 0.f);
+    const float dclamp = (r >= c.lo && r <= c.hi) ? 1.f : 0.f;
+    const float dr = -(g1 * A + g2 * A * dclamp) * c.inv_m;
+    const float dlp = dr * r;
+    acc[2] += (fabsf(r - 1.0f) > c.clip) ? 1.f : 0.f;
+    acc[3] += (r - 1.0f) - logr;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        gm[j] = dlp * zz[j];
+        acc[4 + j] += dlp * ((dd[j] * dd[j]) / c.var[j] - 1.0f);
+    }
+}
+
+__device__ inline void ppo_row_value(const RowLossConst &c, float R, float v, float &gv,
+                                     float acc[kLossK]) {
+    const float e = R - v;
+    acc[1] += e * e;
+    gv = c.vf_coef * (2.0f * (v - R)) * c.inv_m;
+}
+
 __global__ __launch_bounds__(kBlock) void ppo_loss_kernel(LossArgs a) {
     __shared__ float sh[kLossK * 4];
     const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
@@ -954,28 +995,168 @@ struct HeadArgs {
     int P;
 };
 
-// Rows are processed in tiles of kHeadTile per wave: the tile's activations
-// stay in registers, the 5 head dot products per row are wave reductions,
-// the row results are parked one row per lane, the PPO row loss runs once
-// for the whole tile lane-parallel, and the per-row gradients come back by
-// v_readlane for the backward through the heads and the top tanh.
+// Roles: waves 0-1 of a block run the policy head (4 mean outputs, the
+// clipped-surrogate terms, log_std), waves 2-3 the value head, each over its
+// own net's top activations only (the two heads share no row data once the
+// advantage statistics are known).  Per wave, rows come in tiles of
+// kHeadTile: the tile's activations stay in registers, the head dot products
+// are wave reductions, the row results are parked one row per lane, the row
+// loss runs once for the whole tile lane-parallel, and the per-row gradients
+// come back by v_readlane for the backward through the head and the top
+// tanh.  Splitting the nets by wave, with 4-row tiles, brings a wave to 126
+// VGPRs (243 with both nets and 8-row tiles), so 4 waves per SIMD stay
+// resident instead of 2: 66.4 -> 57.5 us per 65,536-row minibatch
+// (rocprofv3, scripts/micro/ppo_prof.sh; 8-row tiles with the split: 65.6).
 #ifndef DR_HEAD_TILE
-#define DR_HEAD_TILE 8
+#define DR_HEAD_TILE 4
 #endif
 constexpr int kHeadTile = DR_HEAD_TILE;
 #ifndef DR_HEAD_DIAG
 #define DR_HEAD_DIAG 0
 #endif
 
-#ifndef DR_HEAD_WPE
-#define DR_HEAD_WPE 0
-#endif
-#if DR_HEAD_WPE
-#define DR_HEAD_ATTR __attribute__((amdgpu_waves_per_eu(DR_HEAD_WPE)))
+// policy waves: accumulate u[0], u[2..7] (loss terms), u[9..12] (d b_act),
+// and per lane d b_pi (4 columns) and d W_act (4 x 4)
+__device__ inline void head_policy_wave(const HeadArgs &a, const RowLossConst &c, int lane,
+                                        int64_t tile0, int64_t tstride, float u[kHeadFixed],
+                                        float sb[4], float sw[4][4]) {
+    const int hd = a.hd, c0 = 4 * lane;
+    const bool act = c0 < hd;
+    const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
+    float4 wa[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) wa[j] = act ? ld4(a.w_act + j * hd + c0) : z4;
+    const float4 zb = (act && a.zb_pi) ? ld4(a.zb_pi + c0) : z4;
+    const float ba[4] = {a.b_act[0], a.b_act[1], a.b_act[2], a.b_act[3]};
+    for (int64_t tile = tile0; tile * kHeadTile < a.m; tile += tstride) {
+        const int64_t r0 = tile * kHeadTile;
+        const int nr = (int)min((int64_t)kHeadTile, a.m - r0);
+        float4 h[kHeadTile];
+#pragma unroll
+        for (int i = 0; i < kHeadTile; ++i)
+            h[i] = (act && i < nr) ? ld4(a.h_pi + (r0 + i) * hd + c0) : z4;
+        // this lane's row (lane < nr): its loss inputs, loaded while the dots run
+        const bool own = lane < nr;
+        const int64_t rr = r0 + (own ? lane : 0);
+        const int64_t ro = a.rows ? (int64_t)a.rows[rr] : rr;
+        const float4 ac4 = a.actions[ro];
+        const float lp_old = a.aux[3 * ro], A = a.aux[3 * ro + 1];
+        if (a.preact) {
+#pragma unroll
+            for (int i = 0; i < kHeadTile; ++i)
+#if DR_HEAD_DIAG == 1  // timing diagnostic only (wrong results): no top tanh
+                h[i] = add4(h[i], zb);
 #else
-#define DR_HEAD_ATTR
+                h[i] = tanh4(add4(h[i], zb));
 #endif
-__global__ __launch_bounds__(kBlock) DR_HEAD_ATTR void ppo_head_kernel(HeadArgs a) {
+        }
+        float mu[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int i = 0; i < kHeadTile; ++i) {
+            const bool me = lane == i;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const float mj = wave_allsum(dot4(h[i], wa[j])) + ba[j];
+                mu[j] = me ? mj : mu[j];
+            }
+        }
+        float gm[4] = {0.f, 0.f, 0.f, 0.f};
+        if (own) {
+            const float ac[4] = {ac4.x, ac4.y, ac4.z, ac4.w};
+            ppo_row_policy(c, mu, ac, lp_old, A, gm, u);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) u[9 + j] += gm[j];
+        }
+        const float wq[4][4] = {{wa[0].x, wa[0].y, wa[0].z, wa[0].w},
+                                {wa[1].x, wa[1].y, wa[1].z, wa[1].w},
+                                {wa[2].x, wa[2].y, wa[2].z, wa[2].w},
+                                {wa[3].x, wa[3].y, wa[3].z, wa[3].w}};
+#pragma unroll
+        for (int i = 0; i < kHeadTile; ++i) {
+            // rows past the end (last tile only) carry zero activations and
+            // zero gradients (gm = 0 on lanes >= nr): no effect on the sums
+            float g[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+                g[j] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(gm[j]), i));
+            const float hq[4] = {h[i].x, h[i].y, h[i].z, h[i].w};
+            float gz[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const float gh = fmaf(g[3], wq[3][q], fmaf(g[2], wq[2][q],
+                                      fmaf(g[1], wq[1][q], g[0] * wq[0][q])));
+                gz[q] = gh * (1.0f - hq[q] * hq[q]);
+                sb[q] += gz[q];
+#pragma unroll
+                for (int j = 0; j < 4; ++j) sw[j][q] = fmaf(g[j], hq[q], sw[j][q]);
+            }
+            if (act && i < nr)
+                st4(a.gz_pi + (r0 + i) * hd + c0, make_float4(gz[0], gz[1], gz[2], gz[3]));
+        }
+    }
+}
+
+// value waves: accumulate u[1] (value-loss term), u[13] (d b_val), and per
+// lane d b_vf (4 columns) and d W_val (4)
+__device__ inline void head_value_wave(const HeadArgs &a, const RowLossConst &c, int lane,
+                                       int64_t tile0, int64_t tstride, float u[kHeadFixed],
+                                       float sb[4], float sw[4]) {
+    const int hd = a.hd, c0 = 4 * lane;
+    const bool act = c0 < hd;
+    const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
+    const float4 wv = act ? ld4(a.w_val + c0) : z4;
+    const float4 zb = (act && a.zb_vf) ? ld4(a.zb_vf + c0) : z4;
+    const float bv = a.b_val[0];
+    const float wvq[4] = {wv.x, wv.y, wv.z, wv.w};
+    for (int64_t tile = tile0; tile * kHeadTile < a.m; tile += tstride) {
+        const int64_t r0 = tile * kHeadTile;
+        const int nr = (int)min((int64_t)kHeadTile, a.m - r0);
+        float4 h[kHeadTile];
+#pragma unroll
+        for (int i = 0; i < kHeadTile; ++i)
+            h[i] = (act && i < nr) ? ld4(a.h_vf + (r0 + i) * hd + c0) : z4;
+        const bool own = lane < nr;
+        const int64_t rr = r0 + (own ? lane : 0);
+        const int64_t ro = a.rows ? (int64_t)a.rows[rr] : rr;
+        const float R = a.aux[3 * ro + 2];
+        if (a.preact) {
+#pragma unroll
+            for (int i = 0; i < kHeadTile; ++i)
+#if DR_HEAD_DIAG == 1
+                h[i] = add4(h[i], zb);
+#else
+                h[i] = tanh4(add4(h[i], zb));
+#endif
+        }
+        float v = 0.f;
+#pragma unroll
+        for (int i = 0; i < kHeadTile; ++i) {
+            const float vv = wave_allsum(dot4(h[i], wv)) + bv;
+            v = lane == i ? vv : v;
+        }
+        float gv = 0.f;
+        if (own) {
+            ppo_row_value(c, R, v, gv, u);
+            u[13] += gv;
+        }
+#pragma unroll
+        for (int i = 0; i < kHeadTile; ++i) {
+            const float gvi = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(gv), i));
+            const float hq[4] = {h[i].x, h[i].y, h[i].z, h[i].w};
+            float gz[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                gz[q] = (gvi * wvq[q]) * (1.0f - hq[q] * hq[q]);
+                sb[q] += gz[q];
+                sw[q] = fmaf(gvi, hq[q], sw[q]);
+            }
+            if (act && i < nr)
+                st4(a.gz_vf + (r0 + i) * hd + c0, make_float4(gz[0], gz[1], gz[2], gz[3]));
+        }
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void ppo_head_kernel(HeadArgs a) {
     extern __shared__ float sh_part[];  // 4 * P
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     const int hd = a.hd, c0 = 4 * lane;
@@ -988,108 +1169,18 @@ __global__ __launch_bounds__(kBlock) DR_HEAD_ATTR void ppo_head_kernel(HeadArgs 
     }
     const RowLossConst c = row_loss_const(a.log_std, a.clip, a.vf_coef, a.m, a.normalize,
                                           amean, astd);
-    const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
-    float4 wa[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) wa[j] = act ? ld4(a.w_act + j * hd + c0) : z4;
-    const float4 wv = act ? ld4(a.w_val + c0) : z4;
-    const float4 zbp = (act && a.zb_pi) ? ld4(a.zb_pi + c0) : z4;
-    const float4 zbv = (act && a.zb_vf) ? ld4(a.zb_vf + c0) : z4;
-    const float ba[4] = {a.b_act[0], a.b_act[1], a.b_act[2], a.b_act[3]};
-    const float bv = a.b_val[0];
     // lane-partial sums of the loss terms and of d b_act / d b_val
     float u[kHeadFixed];
 #pragma unroll
     for (int k = 0; k < kHeadFixed; ++k) u[k] = 0.f;
-    float sbp[4] = {0.f, 0.f, 0.f, 0.f}, sbv[4] = {0.f, 0.f, 0.f, 0.f};
-    float swa[4][4] = {}, swv[4] = {0.f, 0.f, 0.f, 0.f};
-    const float wq[4][4] = {{wa[0].x, wa[0].y, wa[0].z, wa[0].w},
-                            {wa[1].x, wa[1].y, wa[1].z, wa[1].w},
-                            {wa[2].x, wa[2].y, wa[2].z, wa[2].w},
-                            {wa[3].x, wa[3].y, wa[3].z, wa[3].w}};
-    const float wvq[4] = {wv.x, wv.y, wv.z, wv.w};
-    const int64_t nwaves = (int64_t)gridDim.x * 4;
-    for (int64_t tile = (int64_t)blockIdx.x * 4 + wid; tile * kHeadTile < a.m; tile += nwaves) {
-        const int64_t r0 = tile * kHeadTile;
-        const int nr = (int)min((int64_t)kHeadTile, a.m - r0);
-        float4 hp[kHeadTile], hv[kHeadTile];
-#pragma unroll
-        for (int i = 0; i < kHeadTile; ++i) {
-            const bool ok = act && i < nr;
-            hp[i] = ok ? ld4(a.h_pi + (r0 + i) * hd + c0) : z4;
-            hv[i] = ok ? ld4(a.h_vf + (r0 + i) * hd + c0) : z4;
-        }
-        if (a.preact) {
-#pragma unroll
-            for (int i = 0; i < kHeadTile; ++i) {
-#if DR_HEAD_DIAG == 1  // timing diagnostic only (wrong results): no top tanh
-                hp[i] = add4(hp[i], zbp);
-                hv[i] = add4(hv[i], zbv);
-#else
-                hp[i] = tanh4(add4(hp[i], zbp));
-                hv[i] = tanh4(add4(hv[i], zbv));
-#endif
-            }
-        }
-        // this lane's row (lane < nr): its loss inputs, loaded while the dots run
-        const bool own = lane < nr;
-        const int64_t rr = r0 + (own ? lane : 0);
-        const int64_t ro = a.rows ? (int64_t)a.rows[rr] : rr;
-        const float4 ac4 = a.actions[ro];
-        const float lp_old = a.aux[3 * ro], A = a.aux[3 * ro + 1], R = a.aux[3 * ro + 2];
-        float mu[4] = {0.f, 0.f, 0.f, 0.f}, v = 0.f;
-#pragma unroll
-        for (int i = 0; i < kHeadTile; ++i) {
-            const float m0 = wave_allsum(dot4(hp[i], wa[0])) + ba[0];
-            const float m1 = wave_allsum(dot4(hp[i], wa[1])) + ba[1];
-            const float m2 = wave_allsum(dot4(hp[i], wa[2])) + ba[2];
-            const float m3 = wave_allsum(dot4(hp[i], wa[3])) + ba[3];
-            const float vv = wave_allsum(dot4(hv[i], wv)) + bv;
-            const bool me = lane == i;
-            mu[0] = me ? m0 : mu[0];
-            mu[1] = me ? m1 : mu[1];
-            mu[2] = me ? m2 : mu[2];
-            mu[3] = me ? m3 : mu[3];
-            v = me ? vv : v;
-        }
-        float gm[4] = {0.f, 0.f, 0.f, 0.f}, gv = 0.f;
-        if (own) {
-            const float ac[4] = {ac4.x, ac4.y, ac4.z, ac4.w};
-            ppo_row(c, mu, ac, lp_old, A, R, v, gm, gv, u);
-#pragma unroll
-            for (int j = 0; j < 4; ++j) u[9 + j] += gm[j];
-            u[13] += gv;
-        }
-#pragma unroll
-        for (int i = 0; i < kHeadTile; ++i) {
-            // rows past the end (last tile only) carry zero activations and
-            // zero gradients (gm, gv = 0 on lanes >= nr): no effect on sums
-            float g[4];
-#pragma unroll
-            for (int j = 0; j < 4; ++j)
-                g[j] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(gm[j]), i));
-            const float gvi = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(gv), i));
-            const float hpq[4] = {hp[i].x, hp[i].y, hp[i].z, hp[i].w};
-            const float hvq[4] = {hv[i].x, hv[i].y, hv[i].z, hv[i].w};
-            float gzp[4], gzv[4];
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                const float gh = fmaf(g[3], wq[3][q], fmaf(g[2], wq[2][q],
-                                      fmaf(g[1], wq[1][q], g[0] * wq[0][q])));
-                gzp[q] = gh * (1.0f - hpq[q] * hpq[q]);
-                gzv[q] = (gvi * wvq[q]) * (1.0f - hvq[q] * hvq[q]);
-                sbp[q] += gzp[q];
-                sbv[q] += gzv[q];
-#pragma unroll
-                for (int j = 0; j < 4; ++j) swa[j][q] = fmaf(g[j], hpq[q], swa[j][q]);
-                swv[q] = fmaf(gvi, hvq[q], swv[q]);
-            }
-            if (act && i < nr) {
-                st4(a.gz_pi + (r0 + i) * hd + c0, make_float4(gzp[0], gzp[1], gzp[2], gzp[3]));
-                st4(a.gz_vf + (r0 + i) * hd + c0, make_float4(gzv[0], gzv[1], gzv[2], gzv[3]));
-            }
-        }
-    }
+    float sb[4] = {0.f, 0.f, 0.f, 0.f};
+    float sw[4][4] = {};
+    const bool policy = wid < 2;
+    const int64_t tile0 = (int64_t)blockIdx.x * 2 + (wid & 1), tstride = (int64_t)gridDim.x * 2;
+    if (policy)
+        head_policy_wave(a, c, lane, tile0, tstride, u, sb, sw);
+    else
+        head_value_wave(a, c, lane, tile0, tstride, u, sb, sw[0]);
     // the lane-partial scalars to wave totals (fixed butterfly order)
 #pragma unroll
     for (int k = 0; k < kHeadFixed; ++k) u[k] = wave_allsum(u[k]);
@@ -1101,11 +1192,12 @@ __global__ __launch_bounds__(kBlock) DR_HEAD_ATTR void ppo_head_kernel(HeadArgs 
     if (act) {
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-            mine[kHeadFixed + c0 + q] = sbp[q];
-            mine[kHeadFixed + hd + c0 + q] = sbv[q];
+            mine[kHeadFixed + c0 + q] = policy ? sb[q] : 0.f;
+            mine[kHeadFixed + hd + c0 + q] = policy ? 0.f : sb[q];
 #pragma unroll
-            for (int j = 0; j < 4; ++j) mine[kHeadFixed + 2 * hd + j * hd + c0 + q] = swa[j][q];
-            mine[kHeadFixed + 6 * hd + c0 + q] = swv[q];
+            for (int j = 0; j < 4; ++j)
+                mine[kHeadFixed + 2 * hd + j * hd + c0 + q] = policy ? sw[j][q] : 0.f;
+            mine[kHeadFixed + 6 * hd + c0 + q] = policy ? 0.f : sw[0][q];
         }
     }
     __syncthreads();
@@ -1421,6 +1513,12 @@ constexpr int kHeadGroups = 16;  // first-level row groups of the partial sums
 inline int head_blocks(int64_t m) {
     const int64_t b = (m + 4 * kHeadTile - 1) / (4 * kHeadTile);  // >= 1 tile per wave
     return (int)(b < 512 ? b : 512);
+}
+
+// ppo_head_kernel: 2 row tiles per block and round (one per wave of a role)
+inline int loss_head_blocks(int64_t m) {
+    const int64_t b = (m + 2 * kHeadTile - 1) / (2 * kHeadTile);
+    return (int)(b < 1024 ? b : 1024);
 }
 
 // ---------------------------------------------------------------------------
@@ -1875,7 +1973,7 @@ static int grad_finish_adam_impl(const dr_grad_finish *f, int64_t n, float *para
         return fail0(DR_ERR_INVALID, "dr_grad_finish_clip_adam: nothing to finish");
     if (f->head_workspace) {
         const int64_t m = f->head_m, hd = f->head_hd;
-        const int nb = head_blocks(m);
+        const int nb = loss_head_blocks(m);
         const int P = kHeadFixed + 7 * (int)hd;
         const int gsize = (nb + kHeadGroups - 1) / kHeadGroups;
         // the head workspace layout of dr_ppo_head_loss_backward
@@ -2018,7 +2116,7 @@ size_t dr_ppo_head_workspace_bytes(int64_t m, int64_t hd) {
     const int64_t nb = (m + kBlock - 1) / kBlock;
     const int64_t P = kHeadFixed + 7 * hd;
     return align_up(sizeof(float) * 3 * nb) +
-           align_up(sizeof(float) * (size_t)(head_blocks(m > 0 ? m : 1) * P + 2)) +
+           align_up(sizeof(float) * (size_t)(loss_head_blocks(m > 0 ? m : 1) * P + 2)) +
            align_up(sizeof(float) * (size_t)(kHeadGroups * P));
 }
 
@@ -2062,7 +2160,7 @@ int dr_ppo_head_loss_backward(int64_t m, int64_t hd, int preact, const float *h_
         int rc = check_launch("dr_ppo_head_loss_backward stats");
         if (rc) return rc;
     }
-    const int nb = head_blocks(m);
+    const int nb = loss_head_blocks(m);
     const int P = kHeadFixed + 7 * (int)hd;
     HeadArgs a{m, (int)hd, preact, h_pi, h_vf, zb_pi, zb_vf, w_act, b_act, w_val, b_val, log_std,
                reinterpret_cast<const float4 *>(actions), aux, rows, clip_range, ent_coef,
