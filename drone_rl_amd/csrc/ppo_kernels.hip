@@ -868,6 +868,14 @@ struct LayerPair {
     float *h[2];
 };
 
+// 1: the input row through scalar loads (A/B knob, see the kernel body)
+#ifndef DR_LT_SCALAR
+#define DR_LT_SCALAR 1
+#endif
+// blocks per net of linear_tanh_kernel (A/B knob)
+#ifndef DR_LT_MAXB
+#define DR_LT_MAXB 1024
+#endif
 template <int K>
 __global__ __launch_bounds__(kBlock) void linear_tanh_kernel(int64_t m, int n,
                                                              const float *__restrict__ x,
@@ -901,6 +909,41 @@ __global__ __launch_bounds__(kBlock) void linear_tanh_kernel(int64_t m, int n,
             for (int k = 0; k < K; ++k) wr[q][k] = flat[q * K + k];
         }
     }
+#if DR_LT_SCALAR
+    // rows are wave-strided; row r is wave-uniform, so its K inputs are
+    // scalar loads straight into SGPRs (no per-lane load + K readlanes), the
+    // next row's issued before this row's arithmetic
+    const int64_t stride = (int64_t)gridDim.x * 4;
+    int64_t r = (int64_t)blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(wid);
+    auto xrow = [&](int64_t q) -> int64_t { return rows ? (int64_t)rows[q] : q; };
+    float xn[K];
+    if (r < m) {
+        const float *xr = x + xrow(r) * K;
+#pragma unroll
+        for (int k = 0; k < K; ++k) xn[k] = xr[k];
+    }
+    for (; r < m; r += stride) {
+        float xv[K];
+#pragma unroll
+        for (int k = 0; k < K; ++k) xv[k] = xn[k];
+        const int64_t rn = r + stride;
+        if (rn < m) {
+            const float *xr = x + xrow(rn) * K;
+#pragma unroll
+            for (int k = 0; k < K; ++k) xn[k] = xr[k];
+        }
+        float acc[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) acc[q] = fmaf(xv[k], wr[q][k], acc[q]);
+        }
+        if (act)
+            st4(h + r * n + c0,
+                make_float4(tanh_fast(acc[0] + bb[0]), tanh_fast(acc[1] + bb[1]),
+                            tanh_fast(acc[2] + bb[2]), tanh_fast(acc[3] + bb[3])));
+    }
+#else
     // rows are wave-strided; the next row's input is loaded before this
     // row's arithmetic (software pipelining hides the load latency)
     const int64_t stride = (int64_t)gridDim.x * 4;
@@ -925,6 +968,7 @@ __global__ __launch_bounds__(kBlock) void linear_tanh_kernel(int64_t m, int n,
                 make_float4(tanh_fast(acc[0] + bb[0]), tanh_fast(acc[1] + bb[1]),
                             tanh_fast(acc[2] + bb[2]), tanh_fast(acc[3] + bb[3])));
     }
+#endif
 }
 
 // Policy heads for inference (rollouts): mean = h_pi Wa^T + ba (m,4),
@@ -2061,7 +2105,7 @@ static int launch_linear_tanh(const char *who, int nets, int64_t m, int64_t k, i
             return fail0(DR_ERR_INVALID, std::string(who) + ": h and w must be 16-byte aligned");
     }
     const int64_t nbl = (m + 63) / 64;    // >= 16 rows per wave
-    const int nb = (int)(nbl < 1024 ? nbl : 1024);
+    const int nb = (int)(nbl < DR_LT_MAXB ? nbl : DR_LT_MAXB);
     hipStream_t st = as_stream(stream);
     switch (k) {
 #define DR_LT_CASE(K)                                                                      \
