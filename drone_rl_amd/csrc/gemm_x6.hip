@@ -1,0 +1,413 @@
+// fp32-accurate GEMM on the bf16 matrix cores for the PPO MLP's 256 x 256
+// layer (MI355X, gfx950).
+//
+// gfx950 has no xf32 MFMA and its f32-input MFMA runs at 1/16 of the bf16
+// rate, so the hipBLASLt fp32 GEMMs of the 256 x 256 layer cap at 157 TF/s.
+// This kernel keeps fp32 accuracy on the bf16 MFMA instead:
+//
+//   * every fp32 operand x is split EXACTLY into three bf16 planes,
+//     x = h + m + l (8 + 8 + 8 significant bits, RNE at each level: x - h
+//     and (x - h) - m are exact in fp32, and the last remainder fits a bf16);
+//   * a product a*b is formed from the six plane products whose weight is
+//     >= 2^-16 of the leading one (h*h, h*m, m*h, h*l, l*h, m*m), each exact
+//     in the MFMA; the three dropped ones (m*l, l*m, l*l) are <= 2^-23 of
+//     |a*b| together -- below one fp32 rounding of the product;
+//   * h*h accumulates in its own fp32 accumulator and the five small
+//     products in a second one, added once at the end, so the small terms'
+//     roundings are 2^-8 smaller than the leading chain's.
+//
+// Measured against an f64 GEMM on the same inputs this is slightly MORE
+// accurate than the f32 MFMA chain (tests/test_gemm_x6_gpu.py), at 6 bf16
+// MFMAs per product: 2.67x the f32 MFMA rate in peak terms.
+//
+// Shape: C[b] = A[b] . B[b]^T, b < batch (the pi and vf MLPs), A (m, 256) f32
+// row-major, B given as a pre-split image (dr_gemm_x6_split_weights: the
+// layer weight W for the forward z = h W^T, or W^T for grad_h = grad_z W),
+// C (m, 256) f32.  One 512-thread block owns 128 full rows (all 256
+// columns), so A is read from HBM exactly once; the weight image (384 KB per
+// net) streams from L2.
+//
+// Pipeline per 32-deep k stage (two LDS stages of 72 KB): the weight image
+// arrives by global_load_lds (the global image is stored in the LDS layout,
+// 1 KB per wave-instruction, lane-linear), A is loaded as f32 into
+// registers, split by VALU and written to LDS as three bf16 planes while the
+// waves run the previous stage's MFMAs.  8 waves as 2 (rows) x 4 (columns),
+// each owning a 64 x 64 output tile = 2 x 2 v_mfma_f32_32x32x16_bf16 tiles.
+//
+// LDS image of a plane: rows of 32 k (64 B = four 16-B chunks), chunk c of
+// row r stored at chunk c ^ ((r >> 2) & 3): the 16 lanes of every
+// ds_read_b128 lane group then hit 16 distinct 16-B bank slots.
+//
+// Reference: the MLP layers of SB3's ActorCriticPolicy (MlpExtractor,
+// net_arch [256, 256], /root/reference/train.py:36-43) -- torch fp32 Linear.
+
+#include "common.h"
+
+#pragma clang fp contract(off)
+// glds16 clobbers m0 (reserved: the compiler sets it before each own use)
+#pragma clang diagnostic ignored "-Winline-asm"
+
+namespace dr {
+namespace {
+
+// DR_X6_ABL (diagnostic builds only, scripts/micro/gemm_x6_ablate.sh; results
+// are wrong by construction): 1 = no split (raw f32 bits as bf16), 2 = no
+// fragment reads in the k loop, 3 = no global_load_lds in the k loop.
+#ifndef DR_X6_ABL
+#define DR_X6_ABL 0
+#endif
+// 1: raise the wave's issue priority around its MFMA cluster (A/B knob)
+#ifndef DR_X6_PRIO
+#define DR_X6_PRIO 0
+#endif
+
+constexpr int XK = 256;                 // reduction length (hidden width)
+constexpr int XN = 256;                 // output columns
+constexpr int XBM = 128;                // rows per block
+constexpr int XBK = 32;                 // k per LDS stage
+constexpr int XKC = XK / XBK;           // 8 stages
+constexpr int XWAVES = 8;
+constexpr int XTHREADS = 64 * XWAVES;
+constexpr int A_PLANE = XBM * 64;       // 8 KB: 128 rows x 32 bf16
+constexpr int B_PLANE = XN * 64;        // 16 KB: 256 rows x 32 bf16
+constexpr int B_STAGE = 3 * B_PLANE;    // 48 KB
+constexpr int64_t W_IMG = (int64_t)XKC * B_STAGE;  // 384 KB per net
+
+typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+typedef float f32x2_t __attribute__((ext_vector_type(2)));
+typedef float f32x16_t __attribute__((ext_vector_type(16)));
+typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
+
+__device__ inline uint32_t pk_bf16(float a, float b) {
+    return __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2_t){a, b}, bf16x2_t));
+}
+__device__ inline float lo_f(uint32_t p) { return __uint_as_float(p << 16); }
+__device__ inline float hi_f(uint32_t p) { return __uint_as_float(p & 0xffff0000u); }
+
+// x[0..7] = h + m + l exactly, packed as 8 bf16 per plane (element j in
+// bits 16j of the 128-bit value).
+__device__ inline void split8(const float x[8], u32x4_t &h, u32x4_t &m, u32x4_t &l) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const float a = x[2 * q], b = x[2 * q + 1];
+        const uint32_t ph = pk_bf16(a, b);
+        const float ra = a - lo_f(ph), rb = b - hi_f(ph);
+        const uint32_t pm = pk_bf16(ra, rb);
+        const float sa = ra - lo_f(pm), sb = rb - hi_f(pm);
+        h[q] = ph;
+        m[q] = pm;
+        l[q] = pk_bf16(sa, sb);
+    }
+}
+
+__device__ inline int swz(int row, int chunk) {
+    return row * 64 + ((chunk ^ ((row >> 2) & 3)) << 4);
+}
+
+// Weight image of `batch` nets: img[b][kc][plane][n][64 B] holds
+// Bt[n][kc*32 .. +32) with Bt = W (transpose 0) or W^T (transpose 1),
+// W (256, 256) row-major per net.  One thread per (b, kc, n, chunk).
+__global__ __launch_bounds__(256) void split_weights_kernel(const float *__restrict__ w,
+                                                            int transpose, int batch,
+                                                            uint8_t *__restrict__ img) {
+    const int t = blockIdx.x * 256 + threadIdx.x;
+    if (t >= batch * XKC * XN * 4) return;
+    const int c = t & 3, n = (t >> 2) & (XN - 1), kc = (t >> 10) & (XKC - 1), b = t >> 13;
+    const float *wb = w + (int64_t)b * XN * XK;
+    const int k0 = kc * XBK + c * 8;
+    float x[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+        x[j] = transpose ? wb[(int64_t)(k0 + j) * XN + n] : wb[(int64_t)n * XK + k0 + j];
+    u32x4_t h, m, l;
+    split8(x, h, m, l);
+    uint8_t *base = img + (int64_t)b * W_IMG + (int64_t)kc * B_STAGE + swz(n, c);
+    *reinterpret_cast<u32x4_t *>(base) = h;
+    *reinterpret_cast<u32x4_t *>(base + B_PLANE) = m;
+    *reinterpret_cast<u32x4_t *>(base + 2 * B_PLANE) = l;
+}
+
+typedef __attribute__((address_space(3))) void lds_void;
+
+// LDS: weight image stages WB[2] (48 KB each, bf16 planes), A stages A32[3]
+// (16 KB each, f32 rows of 32 k: 128 B, 16-B chunk c of row r at c ^ ((r >>
+// 1) & 7), conflict-free for the fragment reads).  144 KB: one block per CU.
+constexpr int A32_STAGE = XBM * XBK * 4;             // 16 KB
+constexpr int LDS_WB = 0;
+constexpr int LDS_A32 = 2 * B_STAGE;
+constexpr int LDS_TOTAL = 2 * B_STAGE + 3 * A32_STAGE;
+
+// global_load_lds_dwordx4 by inline asm: lane l's 16 bytes land at LDS
+// byte lds_base + 16 l.  Issued by hand because hipcc's waitcnt pass drains
+// every pending LDS DMA (vmcnt(0)) before any ds_read it cannot prove
+// disjoint from it -- once per stage here; the waits are counted by hand.
+__device__ inline void glds16(const void *gptr, uint32_t lds_base) {
+    asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off"
+                 ::"v"(gptr), "s"(lds_base)
+                 : "memory", "m0");
+}
+__device__ inline uint32_t lds_addr(const uint8_t *p) {
+    return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) uint8_t *)p;
+}
+
+__device__ inline int swz32(int row, int chunk) {
+    return row * 128 + ((chunk ^ ((row >> 1) & 7)) << 4);
+}
+
+// Persistent: block blockIdx.x owns tiles blockIdx.x, + gridDim.x, ...; its
+// (tile, stage) pairs form ONE stream of stages g = 0 .. 8 * tiles - 1, so
+// the loads of the next tile's first stages overlap the current tile's last
+// MFMAs and its output stores (no per-tile pipeline fill / drain).  Both
+// operands arrive by global_load_lds: stage g's weight image one stage ahead
+// (from L2), its A rows (f32, from HBM) two stages ahead.  Each wave splits
+// the f32 A fragments it reads from LDS into the three bf16 planes in
+// registers, right before its MFMAs.  Waits are counted by hand (vmcnt
+// retires in issue order), with a raw s_barrier per stage.
+__global__ __launch_bounds__(XTHREADS) void gemm_x6_kernel(const float *__restrict__ A,
+                                                           const uint8_t *__restrict__ img,
+                                                           float *__restrict__ C, int64_t m,
+                                                           int ntiles) {
+    __shared__ __attribute__((aligned(16))) uint8_t sh[LDS_TOTAL];
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wm = wid >> 2, wn = wid & 3;
+    const int tiles_per_net = (int)(m / XBM);
+    const int nmine = (ntiles - (int)blockIdx.x + (int)gridDim.x - 1) / (int)gridDim.x;
+    const int G = nmine * XKC;
+
+    auto tile_of = [&](int g) { return (int)blockIdx.x + (g >> 3) * (int)gridDim.x; };
+    auto net_of = [&](int t) { return t / tiles_per_net; };
+    auto issue_b = [&](int g) {
+        const uint8_t *src = img + (int64_t)net_of(tile_of(g)) * W_IMG + (g & 7) * B_STAGE;
+        uint8_t *dst = sh + LDS_WB + (g & 1) * B_STAGE;
+#pragma unroll
+        for (int i = 0; i < B_STAGE / 1024 / XWAVES; ++i) {
+            const int ins = wid + XWAVES * i;
+            glds16(src + ins * 1024 + lane * 16, lds_addr(dst + ins * 1024));
+        }
+    };
+    // A stage: 16 wave-instructions of 1 KB = 8 rows each; lane L fills LDS
+    // chunk L & 7 of row 8 ins + (L >> 3), i.e. global chunk (L & 7) ^ swizzle
+    const int a_row_l = lane >> 3, a_chk_l = lane & 7;
+    auto issue_a = [&](int g) {
+        const int t = tile_of(g), b = net_of(t);
+        const float *src = A + ((int64_t)b * m + (int64_t)(t - b * tiles_per_net) * XBM) * XK +
+                           (g & 7) * XBK;
+        uint8_t *dst = sh + LDS_A32 + (g % 3) * A32_STAGE;
+#pragma unroll
+        for (int i = 0; i < A32_STAGE / 1024 / XWAVES; ++i) {
+            const int ins = wid + XWAVES * i;
+            const int row = ins * 8 + a_row_l;
+            const int chunk = a_chk_l ^ ((row >> 1) & 7);
+            glds16(src + (int64_t)row * XK + chunk * 4, lds_addr(dst + ins * 1024));
+        }
+    };
+
+    // fragment offsets: tile row fr = lane & 31, k half fh = lane >> 5
+    const int fr = lane & 31, fh = lane >> 5;
+    int a_off[2][2][2], b_off[2][2];
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            // 8 consecutive k of A row r: chunks 4s + 2fh and 4s + 2fh + 1
+            a_off[i][s][0] = swz32(wm * 64 + i * 32 + fr, 4 * s + 2 * fh);
+            a_off[i][s][1] = swz32(wm * 64 + i * 32 + fr, 4 * s + 2 * fh + 1);
+            b_off[i][s] = swz(wn * 64 + i * 32 + fr, 2 * s + fh);
+        }
+    }
+
+    // Raw fragments of one k16 step: the f32 A rows (split later) and the
+    // three weight planes.
+    struct Frag {
+        float4 a[2][2];
+        bf16x8_t b[2][3];
+    };
+    auto read_frag = [&](int g, int s, Frag &f) {
+        if (DR_X6_ABL == 2 && g > 0) {
+            f.a[0][0].x += 1.0f;
+            return;
+        }
+        const uint8_t *SA = sh + LDS_A32 + (g % 3) * A32_STAGE;
+        const uint8_t *SB = sh + LDS_WB + (g & 1) * B_STAGE;
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            f.a[i][0] = *reinterpret_cast<const float4 *>(SA + a_off[i][s][0]);
+            f.a[i][1] = *reinterpret_cast<const float4 *>(SA + a_off[i][s][1]);
+#pragma unroll
+            for (int p = 0; p < 3; ++p)
+                f.b[i][p] = *reinterpret_cast<const bf16x8_t *>(SB + p * B_PLANE + b_off[i][s]);
+        }
+    };
+
+    // Accumulators hold the TRANSPOSED tile, D[n][m] = sum_k Bt[n][k] A[m][k]
+    // (the weight fragment is the MFMA's A operand): a lane then owns 4
+    // consecutive output columns per register quad, stored as one float4.
+    f32x16_t acc_h[2][2], acc_l[2][2];       // [A row tile i][weight tile j]
+    auto zero_acc = [&]() {
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                acc_h[i][j] = (f32x16_t){};
+                acc_l[i][j] = (f32x16_t){};
+            }
+    };
+    auto mfma_step = [&](const Frag &f) {
+        bf16x8_t fa[2][3];
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            const float x[8] = {f.a[i][0].x, f.a[i][0].y, f.a[i][0].z, f.a[i][0].w,
+                                f.a[i][1].x, f.a[i][1].y, f.a[i][1].z, f.a[i][1].w};
+            u32x4_t h, mm, l;
+            if (DR_X6_ABL == 1) {
+                h = (u32x4_t){__float_as_uint(x[0]), __float_as_uint(x[1]), __float_as_uint(x[2]),
+                              __float_as_uint(x[3])};
+                mm = (u32x4_t){__float_as_uint(x[4]), __float_as_uint(x[5]), __float_as_uint(x[6]),
+                               __float_as_uint(x[7])};
+                l = h ^ mm;
+            } else {
+                split8(x, h, mm, l);
+            }
+            fa[i][0] = __builtin_bit_cast(bf16x8_t, h);
+            fa[i][1] = __builtin_bit_cast(bf16x8_t, mm);
+            fa[i][2] = __builtin_bit_cast(bf16x8_t, l);
+        }
+        if (DR_X6_PRIO) __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                const bf16x8_t *w = f.b[j];
+                acc_h[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w[0], fa[i][0],
+                                                                      acc_h[i][j], 0, 0, 0);
+                f32x16_t t = acc_l[i][j];
+                t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w[1], fa[i][0], t, 0, 0, 0);
+                t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w[0], fa[i][1], t, 0, 0, 0);
+                t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w[2], fa[i][0], t, 0, 0, 0);
+                t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w[0], fa[i][2], t, 0, 0, 0);
+                t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w[1], fa[i][1], t, 0, 0, 0);
+                acc_l[i][j] = t;
+            }
+        if (DR_X6_PRIO) __builtin_amdgcn_s_setprio(0);
+    };
+    // D[n][m] map: m = fr (the lane), n = 8 (r >> 2) + 4 fh + (r & 3): the
+    // register quad q holds columns n0 + 8q + 4fh .. +4 of row m -> float4.
+    auto epilogue = [&](int g) {
+        const int t = tile_of(g), b = net_of(t);
+        float *Cb = C + ((int64_t)b * m + (int64_t)(t - b * tiles_per_net) * XBM) * XN;
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                const f32x16_t v = acc_h[i][j] + acc_l[i][j];
+                float *c = Cb + (int64_t)(wm * 64 + i * 32 + fr) * XN + wn * 64 + j * 32 + 4 * fh;
+#pragma unroll
+                for (int q = 0; q < 4; ++q)
+                    *reinterpret_cast<float4 *>(c + 8 * q) =
+                        make_float4(v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]);
+            }
+    };
+
+    // Stage g's schedule (per wave): MFMAs of k16 step 0 while the step-1
+    // fragments are read; wait for stage g + 1's operands + barrier; issue
+    // the image of g + 2 and the A rows of g + 3 into stage g's (now free)
+    // buffers; read stage g + 1's step-0 fragments during step 1's MFMAs.
+    // VMEM ops per wave: 6 image + 2 A loads per stage, 16 stores per tile.
+    zero_acc();
+    issue_b(0);
+    issue_a(0);
+    issue_a(1);
+    issue_b(1);
+    issue_a(2);                                   // G >= 8
+    asm volatile("s_waitcnt vmcnt(10)\n\ts_barrier" ::: "memory");
+    Frag f0, f1;
+    read_frag(0, 0, f0);
+    for (int g = 0; g < G; ++g) {
+        read_frag(g, 1, f1);
+        mfma_step(f0);
+        // stage g + 1's image and A rows have landed; younger VMEM ops: the
+        // A rows of g + 2 (issued one stage ago) and the previous tile's
+        // 16 stores
+        const bool a2 = g + 2 < G, epi_prev = (g & 7) == 0 && g > 0;
+        __builtin_amdgcn_sched_barrier(0);
+        if (a2 && epi_prev)
+            asm volatile("s_waitcnt vmcnt(18) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        else if (epi_prev)
+            asm volatile("s_waitcnt vmcnt(16) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        else if (a2)
+            asm volatile("s_waitcnt vmcnt(2) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        else
+            asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        if (g + 2 < G && DR_X6_ABL != 3) issue_b(g + 2);
+        if (g + 3 < G && DR_X6_ABL != 3) issue_a(g + 3);
+        if (g + 1 < G) read_frag(g + 1, 0, f0);
+        __builtin_amdgcn_sched_barrier(0);
+        mfma_step(f1);
+        if ((g & 7) == 7) {
+            epilogue(g);
+            zero_acc();
+        }
+    }
+}
+
+int fail_g(int code, const std::string &msg) {
+    set_global_error(msg);
+    return code;
+}
+
+}  // namespace
+}  // namespace dr
+
+using namespace dr;
+
+extern "C" {
+
+size_t dr_gemm_x6_weights_bytes(int64_t batch) {
+    return batch < 1 ? 0 : (size_t)(batch * W_IMG);
+}
+
+int dr_gemm_x6_split_weights(int64_t batch, const float *w, int transpose, void *img,
+                             void *stream) {
+    if (batch < 1 || batch > 2 || !w || !img || (transpose != 0 && transpose != 1) ||
+        (((uintptr_t)img) & 15))
+        return fail_g(DR_ERR_INVALID, "dr_gemm_x6_split_weights: bad arguments");
+    const int threads = (int)batch * XKC * XN * 4;
+    hipLaunchKernelGGL(split_weights_kernel, dim3((threads + 255) / 256), dim3(256), 0,
+                       static_cast<hipStream_t>(stream), w, transpose, (int)batch,
+                       static_cast<uint8_t *>(img));
+    const hipError_t e = hipGetLastError();
+    return e == hipSuccess ? DR_OK
+                           : fail_g(DR_ERR_HIP, std::string("split_weights_kernel: ") +
+                                                    hipGetErrorString(e));
+}
+
+int dr_gemm_x6(int64_t batch, int64_t m, const float *a, const void *img, float *c,
+               void *stream) {
+    if (batch < 1 || batch > 2 || m < XBM || m % XBM || m > (int64_t(1) << 26) || !a ||
+        !img || !c || (((uintptr_t)a) & 15) || (((uintptr_t)img) & 15) ||
+        (((uintptr_t)c) & 15))
+        return fail_g(DR_ERR_INVALID,
+                      "dr_gemm_x6: bad arguments (m must be a positive multiple of 128, "
+                      "pointers 16-byte aligned)");
+    static int n_cu = 0;
+    if (n_cu == 0) {
+        int dev = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+            n_cu < 1)
+            n_cu = 256;
+    }
+    const int ntiles = (int)(batch * (m / XBM));
+    const int grid = ntiles < n_cu ? ntiles : n_cu;       // one 144-KB block per CU
+    hipLaunchKernelGGL(gemm_x6_kernel, dim3(grid), dim3(XTHREADS), 0,
+                       static_cast<hipStream_t>(stream), a, static_cast<const uint8_t *>(img),
+                       c, m, ntiles);
+    const hipError_t e = hipGetLastError();
+    return e == hipSuccess
+               ? DR_OK
+               : fail_g(DR_ERR_HIP, std::string("gemm_x6_kernel: ") + hipGetErrorString(e));
+}
+
+}  // extern "C"

@@ -39,7 +39,7 @@
 extern "C" {
 #endif
 
-#define DR_ABI_VERSION 9
+#define DR_ABI_VERSION 10
 
 enum dr_status {
     DR_OK = 0,
@@ -455,6 +455,29 @@ int dr_grad_finish_clip_adam_sched(const dr_grad_finish *f, int64_t n, float *pa
                                    float max_grad_norm, const float *sched,
                                    float *grad_norm_out, void *workspace,
                                    size_t workspace_bytes, void *stream);
+
+/* ---- fp32-accurate 256 x 256 layer GEMM on the bf16 matrix cores ---------
+   Replaces the torch fp32 Linear of SB3's MlpExtractor 256 -> 256 layer
+   (forward z = h W^T and the input gradient grad_h = grad_z W; reference
+   policy net_arch at /root/reference/train.py:36-43).  Operands are split
+   exactly into three bf16 planes and multiplied with six MFMA products per
+   element pair (csrc/gemm_x6.hip); the error against an f64 GEMM is below
+   the f32 MFMA GEMM's.  (ABI v10.) */
+
+/* Bytes of the pre-split weight image of `batch` (1 or 2) 256 x 256 layers. */
+size_t dr_gemm_x6_weights_bytes(int64_t batch);
+
+/* Split `batch` row-major 256 x 256 f32 weights w (consecutive) into the
+   image dr_gemm_x6 reads: transpose 0 for C = A W^T, 1 for C = A W.
+   img 16-byte aligned, dr_gemm_x6_weights_bytes(batch) bytes. */
+int dr_gemm_x6_split_weights(int64_t batch, const float *w, int transpose, void *img,
+                             void *stream);
+
+/* C[b] = A[b] . Bt[b]^T for b < batch: A (batch, m, 256) f32, C (batch, m,
+   256) f32, Bt given by img.  m a positive multiple of 128; a, img and c
+   16-byte aligned.  Deterministic. */
+int dr_gemm_x6(int64_t batch, int64_t m, const float *a, const void *img, float *c,
+               void *stream);
 
 #ifdef __cplusplus
 }

@@ -21,5 +21,6 @@ if [ $what = product ] || [ $what = all ]; then
   /opt/rocm/bin/hipcc -O1 -g -std=c++17 -fPIC --offload-arch=gfx950 -ffp-contract=off \
       -fno-fast-math -Iinclude -fno-omit-frame-pointer \
       -Xarch_host -fsanitize=address -Xarch_host -fsanitize=undefined \
-      -shared -o $OUT/libdronerl.so drone_rl_amd/csrc/env_kernels.hip drone_rl_amd/csrc/ppo_kernels.hip
+      -shared -o $OUT/libdronerl.so drone_rl_amd/csrc/env_kernels.hip drone_rl_amd/csrc/ppo_kernels.hip \
+      drone_rl_amd/csrc/gemm_x6.hip
 fi

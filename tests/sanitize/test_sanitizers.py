@@ -48,7 +48,7 @@ def test_oracle_under_asan_ubsan():
     if not os.path.isabs(asan) or not os.path.exists(asan):
         pytest.skip("gcc's libasan not available")
     target = os.path.join(OUT, "liboracle.so")
-    _build("oracle", target, glob.glob(os.path.join(ROOT, "oracle", "*.c")))
+    _build("oracle", target, glob.glob(os.path.join(ROOT, "oracle", "*.c")) + [BUILD])
     out = _run(asan, {"ORACLE_LIB": target}, ["tests/test_oracle.py"])
     assert "passed" in out
 
@@ -59,7 +59,7 @@ def test_product_host_code_under_asan_ubsan():
         pytest.skip("clang ASan runtime / hipcc not available")
     target = os.path.join(OUT, "libdronerl.so")
     srcs = glob.glob(os.path.join(ROOT, "drone_rl_amd", "csrc", "*")) + \
-        [os.path.join(ROOT, "include", "dronerl.h")]
+        [os.path.join(ROOT, "include", "dronerl.h"), BUILD]
     _build("product", target, srcs)
     out = _run(rt[-1], {"DRONERL_LIB": target}, ["tests/test_abi.py"])
     assert "passed" in out
