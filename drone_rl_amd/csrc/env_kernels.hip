@@ -99,6 +99,13 @@ __device__ unsigned long long g_stamps[16384 * 8];
 #endif
 constexpr int kEnvBlock = 64 * DR_ENV_WPB;
 
+// 1: the observation is formed once, after the auto-reset (the terminal
+// obs only when requested); 0: formed before the reset and again for the
+// reset rows
+#ifndef DR_OBS_ONCE
+#define DR_OBS_ONCE 1
+#endif
+
 #ifndef DR_NT_STORES
 #define DR_NT_STORES 1
 #endif
@@ -700,7 +707,9 @@ __global__ __launch_bounds__(kEnvBlock) void env_step_kernel(EnvView<S> v,
         st_out(at(io.rew, i), rf);
         st_out(at(io.done, i), (uint8_t)done);
     }
+#if !DR_OBS_ONCE
     make_obs<S, OD>(st, ob, tvel);
+#endif
 
     float ret = 0.f;
     int32_t len = 0;
@@ -712,6 +721,9 @@ __global__ __launch_bounds__(kEnvBlock) void env_step_kernel(EnvView<S> v,
         if (done && io.auto_reset && DR_ABLATE != 2) {
             // DummyVecEnv: keep the terminal obs, reset in the same step.
             if (io.term_obs) {
+#if DR_OBS_ONCE
+                make_obs<S, OD>(st, ob, tvel);
+#endif
 #pragma unroll
                 for (int k = 0; k < OD; ++k) io.term_obs[i * OD + k] = ob[k];
             }
@@ -729,9 +741,16 @@ __global__ __launch_bounds__(kEnvBlock) void env_step_kernel(EnvView<S> v,
                 for (int k = 0; k < 9; ++k) *at(v.mot + k * v.stride, i) = mp[k];
                 moving_target(cen, mp, 0, (float)v.dt, &st[F_TGT], tvel);
             }
+#if !DR_OBS_ONCE
             make_obs<S, OD>(st, ob, tvel);
+#endif
         }
     }
+#if DR_OBS_ONCE
+    // ONE observation pass over the post-reset state (the terminal obs is
+    // formed inside the reset branch only when the caller keeps it)
+    make_obs<S, OD>(st, ob, tvel);
+#endif
     if constexpr (MON) {
         if (done) {               // VecMonitor: report, then restart counters
             *at(io.ep_ret_out, i) = ret;

@@ -68,7 +68,6 @@ constexpr int XBK = 32;                 // k per LDS stage
 constexpr int XKC = XK / XBK;           // 8 stages
 constexpr int XWAVES = 8;
 constexpr int XTHREADS = 64 * XWAVES;
-constexpr int A_PLANE = XBM * 64;       // 8 KB: 128 rows x 32 bf16
 constexpr int B_PLANE = XN * 64;        // 16 KB: 256 rows x 32 bf16
 constexpr int B_STAGE = 3 * B_PLANE;    // 48 KB
 constexpr int64_t W_IMG = (int64_t)XKC * B_STAGE;  // 384 KB per net

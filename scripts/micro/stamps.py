@@ -59,6 +59,8 @@ for t in range(60):
         rel = (s[:, :6] - t0) * 10.0 / 1000.0   # us
         rs = (s[:, 6] >= s[:, 2]) & (s[:, 6] <= s[:, 3])   # reset this step
         rr = (s[rs] - t0) * 10.0 / 1000.0
+        if len(rr) == 0:
+            rr = np.full((1, 8), np.nan)
         res.append({"wave_start_p50_us": np.percentile(rel[:, 0], 50),
                     "wave_start_max_us": rel[:, 0].max(),
                     "first_data_p50_us": np.percentile(rel[:, 1] - rel[:, 0], 50),
