@@ -56,6 +56,17 @@ namespace {
 #ifndef DR_X6_ABL
 #define DR_X6_ABL 0
 #endif
+// DR_X6_STAMPS (diagnostic builds only): s_memtime at four points of every
+// stage for the waves of blocks 0-7, read back by dr_x6_diag_stamps
+// (scripts/micro/gemm_x6_stamps.py); no output depends on a stamp.
+#ifndef DR_X6_STAMPS
+#define DR_X6_STAMPS 0
+#endif
+// 1: the f32 A fragments of a k16 step are split into bf16 planes as soon as
+// they are read (during the previous step's MFMAs), not at the step's start
+#ifndef DR_X6_EARLY
+#define DR_X6_EARLY 0
+#endif
 // 1: raise the wave's issue priority around its MFMA cluster (A/B knob)
 #ifndef DR_X6_PRIO
 #define DR_X6_PRIO 0
@@ -66,7 +77,28 @@ constexpr int XN = 256;                 // output columns
 constexpr int XBM = 128;                // rows per block
 constexpr int XBK = 32;                 // k per LDS stage
 constexpr int XKC = XK / XBK;           // 8 stages
-constexpr int XWAVES = 8;
+// waves per block: 8 (2 x 4 waves of 64 x 64 outputs, 2 waves per SIMD) or
+// 4 (1 x 4 waves of 128 x 64 outputs, one wave per SIMD with 512 registers)
+#ifndef DR_X6_WAVES
+#define DR_X6_WAVES 8
+#endif
+#if DR_X6_WAVES == 8
+#define X6_NA 2      // A-row global_load_lds per wave per stage
+#define X6_NA_NST 18 // + the 16 float4 stores of a finished tile
+#define X6_NST 16
+#define X6_PRO 10    // prologue: younger than stage 0's loads (A1 + B1 + A2)
+#elif DR_X6_WAVES == 4
+#define X6_NA 4
+#define X6_NA_NST 36
+#define X6_NST 32
+#define X6_PRO 20
+#else
+#error "DR_X6_WAVES must be 4 or 8"
+#endif
+#define X6_S2(x) #x
+#define X6_S(x) X6_S2(x)
+constexpr int XWAVES = DR_X6_WAVES;
+constexpr int XMT = 16 / XWAVES;        // 32-row tiles per wave
 constexpr int XTHREADS = 64 * XWAVES;
 constexpr int B_PLANE = XN * 64;        // 16 KB: 256 rows x 32 bf16
 constexpr int B_STAGE = 3 * B_PLANE;    // 48 KB
@@ -129,6 +161,23 @@ __global__ __launch_bounds__(256) void split_weights_kernel(const float *__restr
 
 typedef __attribute__((address_space(3))) void lds_void;
 
+#if DR_X6_STAMPS
+constexpr int kStG = 64;   // stages recorded per wave
+__device__ unsigned long long g_x6_st[8 * XWAVES * kStG * 4];
+#define X6_STAMP(g, k)                                                                 \
+    do {                                                                               \
+        __builtin_amdgcn_sched_barrier(0);                                             \
+        const unsigned long long t__ = __builtin_amdgcn_s_memtime();                   \
+        if (blockIdx.x < 8 && (g) < kStG && (threadIdx.x & 63) == 0)                    \
+            g_x6_st[((blockIdx.x * XWAVES + (threadIdx.x >> 6)) * kStG + (g)) * 4 + (k)] = t__; \
+        __builtin_amdgcn_sched_barrier(0);                                             \
+    } while (0)
+#else
+#define X6_STAMP(g, k) \
+    do {               \
+    } while (0)
+#endif
+
 // LDS: weight image stages WB[2] (48 KB each, bf16 planes), A stages A32[3]
 // (16 KB each, f32 rows of 32 k: 128 B, 16-B chunk c of row r at c ^ ((r >>
 // 1) & 7), conflict-free for the fragment reads).  144 KB: one block per CU.
@@ -170,7 +219,7 @@ __global__ __launch_bounds__(XTHREADS) void gemm_x6_kernel(const float *__restri
     __shared__ __attribute__((aligned(16))) uint8_t sh[LDS_TOTAL];
     const int tid = threadIdx.x, lane = tid & 63;
     const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int wm = wid >> 2, wn = wid & 3;
+    const int wm = XWAVES == 8 ? wid >> 2 : 0, wn = wid & 3;
     const int tiles_per_net = (int)(m / XBM);
     const int nmine = (ntiles - (int)blockIdx.x + (int)gridDim.x - 1) / (int)gridDim.x;
     const int G = nmine * XKC;
@@ -205,23 +254,25 @@ __global__ __launch_bounds__(XTHREADS) void gemm_x6_kernel(const float *__restri
 
     // fragment offsets: tile row fr = lane & 31, k half fh = lane >> 5
     const int fr = lane & 31, fh = lane >> 5;
-    int a_off[2][2][2], b_off[2][2];
+    int a_off[XMT][2][2], b_off[2][2];
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
 #pragma unroll
-        for (int i = 0; i < 2; ++i) {
+        for (int i = 0; i < XMT; ++i) {
             // 8 consecutive k of A row r: chunks 4s + 2fh and 4s + 2fh + 1
             a_off[i][s][0] = swz32(wm * 64 + i * 32 + fr, 4 * s + 2 * fh);
             a_off[i][s][1] = swz32(wm * 64 + i * 32 + fr, 4 * s + 2 * fh + 1);
-            b_off[i][s] = swz(wn * 64 + i * 32 + fr, 2 * s + fh);
         }
+#pragma unroll
+        for (int j = 0; j < 2; ++j) b_off[j][s] = swz(wn * 64 + j * 32 + fr, 2 * s + fh);
     }
 
     // Raw fragments of one k16 step: the f32 A rows (split later) and the
     // three weight planes.
     struct Frag {
-        float4 a[2][2];
+        float4 a[XMT][2];
         bf16x8_t b[2][3];
+        bf16x8_t a3[XMT][3];   // the split A planes
     };
     auto read_frag = [&](int g, int s, Frag &f) {
         if (DR_X6_ABL == 2 && g > 0) {
@@ -231,32 +282,33 @@ __global__ __launch_bounds__(XTHREADS) void gemm_x6_kernel(const float *__restri
         const uint8_t *SA = sh + LDS_A32 + (g % 3) * A32_STAGE;
         const uint8_t *SB = sh + LDS_WB + (g & 1) * B_STAGE;
 #pragma unroll
-        for (int i = 0; i < 2; ++i) {
+        for (int i = 0; i < XMT; ++i) {
             f.a[i][0] = *reinterpret_cast<const float4 *>(SA + a_off[i][s][0]);
             f.a[i][1] = *reinterpret_cast<const float4 *>(SA + a_off[i][s][1]);
+        }
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
 #pragma unroll
             for (int p = 0; p < 3; ++p)
-                f.b[i][p] = *reinterpret_cast<const bf16x8_t *>(SB + p * B_PLANE + b_off[i][s]);
-        }
+                f.b[j][p] = *reinterpret_cast<const bf16x8_t *>(SB + p * B_PLANE + b_off[j][s]);
     };
 
     // Accumulators hold the TRANSPOSED tile, D[n][m] = sum_k Bt[n][k] A[m][k]
     // (the weight fragment is the MFMA's A operand): a lane then owns 4
     // consecutive output columns per register quad, stored as one float4.
-    f32x16_t acc_h[2][2], acc_l[2][2];       // [A row tile i][weight tile j]
+    f32x16_t acc_h[XMT][2], acc_l[XMT][2];   // [A row tile i][weight tile j]
     auto zero_acc = [&]() {
 #pragma unroll
-        for (int i = 0; i < 2; ++i)
+        for (int i = 0; i < XMT; ++i)
 #pragma unroll
             for (int j = 0; j < 2; ++j) {
                 acc_h[i][j] = (f32x16_t){};
                 acc_l[i][j] = (f32x16_t){};
             }
     };
-    auto mfma_step = [&](const Frag &f) {
-        bf16x8_t fa[2][3];
+    auto split_frag = [&](Frag &f) {
 #pragma unroll
-        for (int i = 0; i < 2; ++i) {
+        for (int i = 0; i < XMT; ++i) {
             const float x[8] = {f.a[i][0].x, f.a[i][0].y, f.a[i][0].z, f.a[i][0].w,
                                 f.a[i][1].x, f.a[i][1].y, f.a[i][1].z, f.a[i][1].w};
             u32x4_t h, mm, l;
@@ -269,13 +321,17 @@ __global__ __launch_bounds__(XTHREADS) void gemm_x6_kernel(const float *__restri
             } else {
                 split8(x, h, mm, l);
             }
-            fa[i][0] = __builtin_bit_cast(bf16x8_t, h);
-            fa[i][1] = __builtin_bit_cast(bf16x8_t, mm);
-            fa[i][2] = __builtin_bit_cast(bf16x8_t, l);
+            f.a3[i][0] = __builtin_bit_cast(bf16x8_t, h);
+            f.a3[i][1] = __builtin_bit_cast(bf16x8_t, mm);
+            f.a3[i][2] = __builtin_bit_cast(bf16x8_t, l);
         }
+    };
+    auto mfma_step = [&](Frag &f) {
+        if (!DR_X6_EARLY) split_frag(f);
+        const bf16x8_t(&fa)[XMT][3] = f.a3;
         if (DR_X6_PRIO) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
-        for (int i = 0; i < 2; ++i)
+        for (int i = 0; i < XMT; ++i)
 #pragma unroll
             for (int j = 0; j < 2; ++j) {
                 const bf16x8_t *w = f.b[j];
@@ -297,7 +353,7 @@ __global__ __launch_bounds__(XTHREADS) void gemm_x6_kernel(const float *__restri
         const int t = tile_of(g), b = net_of(t);
         float *Cb = C + ((int64_t)b * m + (int64_t)(t - b * tiles_per_net) * XBM) * XN;
 #pragma unroll
-        for (int i = 0; i < 2; ++i)
+        for (int i = 0; i < XMT; ++i)
 #pragma unroll
             for (int j = 0; j < 2; ++j) {
                 const f32x16_t v = acc_h[i][j] + acc_l[i][j];
@@ -320,30 +376,37 @@ __global__ __launch_bounds__(XTHREADS) void gemm_x6_kernel(const float *__restri
     issue_a(1);
     issue_b(1);
     issue_a(2);                                   // G >= 8
-    asm volatile("s_waitcnt vmcnt(10)\n\ts_barrier" ::: "memory");
+    asm volatile("s_waitcnt vmcnt(" X6_S(X6_PRO) ")\n\ts_barrier" ::: "memory");
     Frag f0, f1;
     read_frag(0, 0, f0);
+    if (DR_X6_EARLY) split_frag(f0);
     for (int g = 0; g < G; ++g) {
+        X6_STAMP(g, 0);
         read_frag(g, 1, f1);
         mfma_step(f0);
+        if (DR_X6_EARLY) split_frag(f1);
+        X6_STAMP(g, 1);
         // stage g + 1's image and A rows have landed; younger VMEM ops: the
         // A rows of g + 2 (issued one stage ago) and the previous tile's
         // 16 stores
         const bool a2 = g + 2 < G, epi_prev = (g & 7) == 0 && g > 0;
         __builtin_amdgcn_sched_barrier(0);
         if (a2 && epi_prev)
-            asm volatile("s_waitcnt vmcnt(18) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+            asm volatile("s_waitcnt vmcnt(" X6_S(X6_NA_NST) ") lgkmcnt(0)\n\ts_barrier" ::: "memory");
         else if (epi_prev)
-            asm volatile("s_waitcnt vmcnt(16) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+            asm volatile("s_waitcnt vmcnt(" X6_S(X6_NST) ") lgkmcnt(0)\n\ts_barrier" ::: "memory");
         else if (a2)
-            asm volatile("s_waitcnt vmcnt(2) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+            asm volatile("s_waitcnt vmcnt(" X6_S(X6_NA) ") lgkmcnt(0)\n\ts_barrier" ::: "memory");
         else
             asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        X6_STAMP(g, 2);
         if (g + 2 < G && DR_X6_ABL != 3) issue_b(g + 2);
         if (g + 3 < G && DR_X6_ABL != 3) issue_a(g + 3);
         if (g + 1 < G) read_frag(g + 1, 0, f0);
         __builtin_amdgcn_sched_barrier(0);
         mfma_step(f1);
+        if (DR_X6_EARLY && g + 1 < G) split_frag(f0);
+        X6_STAMP(g, 3);
         if ((g & 7) == 7) {
             epilogue(g);
             zero_acc();
@@ -408,5 +471,14 @@ int dr_gemm_x6(int64_t batch, int64_t m, const float *a, const void *img, float 
                ? DR_OK
                : fail_g(DR_ERR_HIP, std::string("gemm_x6_kernel: ") + hipGetErrorString(e));
 }
+
+#if DR_X6_STAMPS
+int dr_x6_diag_stamps(void *host_out, size_t bytes) {
+    if (bytes < sizeof(g_x6_st)) return DR_ERR_INVALID;
+    return hipMemcpyFromSymbol(host_out, HIP_SYMBOL(g_x6_st), sizeof(g_x6_st)) == hipSuccess
+               ? DR_OK
+               : DR_ERR_HIP;
+}
+#endif
 
 }  // extern "C"
