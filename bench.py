@@ -175,6 +175,7 @@ def time_ppo(args, rank, world, device):
     import torch
     import torch.distributed as dist
 
+    from drone_rl_amd.policy import x6_weights
     from drone_rl_amd.ppo import PPOConfig, PPOTrainer
     cfg = PPOConfig(num_envs=args.envs, n_steps=args.ppo_steps, batch_size=args.envs,
                     n_epochs=args.ppo_epochs, state_dtype=args.state_dtype, seed=0,
@@ -211,8 +212,12 @@ def time_ppo(args, rank, world, device):
                        "optimizer_steps_per_update": cfg.n_epochs * cfg.n_steps *
                        cfg.num_envs // cfg.batch_size,
                        "net_arch": list(cfg.net_arch), "mlp_dtype": "fp32",
-                       "gemm": ("hipBLASLt/rocBLAS, MI355X-tuned solutions (TunableOp lookup)"
-                                if tr.tuned_gemms else "hipBLASLt heuristic"),
+                       "gemm": ((("256x256 layer forward + input gradient: dr_gemm_x6 "
+                                  "(fp32-accurate: exact 3-plane bf16 split, 6 MFMA products, "
+                                  "f32 accumulate); weight gradient: ")
+                                 if x6_weights(tr.policy, cfg.batch_size) is not None else "") +
+                                ("hipBLASLt/rocBLAS, MI355X-tuned solutions (TunableOp lookup)"
+                                 if tr.tuned_gemms else "hipBLASLt heuristic")),
                        "grad_allreduce": ({"nccl": "rccl"}.get(dist.get_backend(),
                                                                dist.get_backend())
                                           + (" (2 buckets, the first overlapped with the "

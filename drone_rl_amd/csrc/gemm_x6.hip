@@ -144,6 +144,10 @@ __global__ __launch_bounds__(256) void split_weights_kernel(const float *__restr
                                                             uint8_t *__restrict__ img) {
     const int t = blockIdx.x * 256 + threadIdx.x;
     if (t >= batch * XKC * XN * 4) return;
+    if (transpose == 2) {      // both images: blockIdx.y 0 -> W^T form, 1 -> W form
+        transpose = (int)blockIdx.y;
+        img += (int64_t)blockIdx.y * batch * W_IMG;
+    }
     const int c = t & 3, n = (t >> 2) & (XN - 1), kc = (t >> 10) & (XKC - 1), b = t >> 13;
     const float *wb = w + (int64_t)b * XN * XK;
     const int k0 = kc * XBK + c * 8;
@@ -432,12 +436,13 @@ size_t dr_gemm_x6_weights_bytes(int64_t batch) {
 
 int dr_gemm_x6_split_weights(int64_t batch, const float *w, int transpose, void *img,
                              void *stream) {
-    if (batch < 1 || batch > 2 || !w || !img || (transpose != 0 && transpose != 1) ||
+    if (batch < 1 || batch > 2 || !w || !img || transpose < 0 || transpose > 2 ||
         (((uintptr_t)img) & 15))
         return fail_g(DR_ERR_INVALID, "dr_gemm_x6_split_weights: bad arguments");
     const int threads = (int)batch * XKC * XN * 4;
-    hipLaunchKernelGGL(split_weights_kernel, dim3((threads + 255) / 256), dim3(256), 0,
-                       static_cast<hipStream_t>(stream), w, transpose, (int)batch,
+    // transpose 2: both images in one launch (W^T form at img, W form after it)
+    hipLaunchKernelGGL(split_weights_kernel, dim3((threads + 255) / 256, transpose == 2 ? 2 : 1),
+                       dim3(256), 0, static_cast<hipStream_t>(stream), w, transpose, (int)batch,
                        static_cast<uint8_t *>(img));
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? DR_OK

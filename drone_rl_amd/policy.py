@@ -123,6 +123,11 @@ class ActorCritic:
             self.offsets[name] = (off, off + n, shape)
             off += n
         self.num_params = off
+        # the 256 x 256 layer's forward / input-gradient GEMMs on dr_gemm_x6
+        # (fp32-accurate bf16 MFMA) where it applies;
+        # DRONERL_GEMM_X6=0: the f32 library GEMMs
+        self.gemm_x6 = os.environ.get("DRONERL_GEMM_X6", "1") != "0"
+        self._x6 = None
         self.flat = torch.zeros(off, dtype=torch.float32, device=self.device)
         self.reset_parameters(seed, log_std_init)
         self.flat.requires_grad_(True)
@@ -201,6 +206,46 @@ class ActorCritic:
         with torch.no_grad():
             for name, _, _ in self.layout:
                 self.p(name).copy_(torch.as_tensor(sd[_sb3_name(name, len(self.net_arch))]))
+
+
+class X6Weights:
+    """Both MLPs' 256 x 256 layer weights pre-split for dr_gemm_x6
+    (DESIGN.md section 12): `fwd` for z = h W^T, `bwd` for grad_h = grad_z W.
+    refresh() re-splits the current weights (one launch, graph-capturable);
+    callers refresh whenever the weights may have changed."""
+
+    def __init__(self, pol: "ActorCritic"):
+        from . import _lib
+        nb = _lib.lib().dr_gemm_x6_weights_bytes(2)
+        self.pol = pol
+        self.img = torch.empty(2 * nb, dtype=torch.uint8, device=pol.device)
+        self.fwd, self.bwd = self.img[:nb], self.img[nb:]
+
+    def refresh(self):
+        from . import _lib
+        w = self.pol.p2(1, "w")
+        _lib.check(_lib.lib().dr_gemm_x6_split_weights(
+            2, w.data_ptr(), 2, self.img.data_ptr(),
+            torch.cuda.current_stream(w.device).cuda_stream))
+
+
+def x6_weights(pol: "ActorCritic", m: int):
+    """pol's X6Weights when dr_gemm_x6 covers its 256 x 256 layer at m rows
+    (net_arch (256, 256), m a positive multiple of 128, pol.gemm_x6), else
+    None (the library GEMMs run)."""
+    if (not pol.gemm_x6 or pol.net_arch != (256, 256) or m < 128 or m % 128 or
+            pol.device.type != "cuda"):
+        return None
+    if pol._x6 is None:
+        pol._x6 = X6Weights(pol)
+    return pol._x6
+
+
+def gemm_x6(a, img, out):
+    """out (2, m, 256) = a (2, m, 256) . Bt^T for the pre-split image img."""
+    from . import _lib
+    _lib.check(_lib.lib().dr_gemm_x6(2, a.shape[1], a.data_ptr(), img.data_ptr(), out.data_ptr(),
+                                     torch.cuda.current_stream(a.device).cuda_stream))
 
 
 def _sb3_name(name: str, depth: int) -> str:
@@ -351,7 +396,11 @@ class FusedTrainStep:
                 # all but the first layer's gradient is final from here on
                 on_ready(self.first_layer_end(), self.grad.numel())
             g = self._g2.view(-1)[:2 * M * n_in].view(2, M, n_in)
-            torch.bmm(gz, pol.p2(k, "w"), out=g)
+            xw = x6_weights(pol, M) if k == 1 else None
+            if xw is not None:
+                gemm_x6(gz, xw.bwd, g)       # images refreshed by hidden_forward
+            else:
+                torch.bmm(gz, pol.p2(k, "w"), out=g)
             if k == 1:
                 # first layer of both MLPs: tanh backward + weight/bias
                 # gradients fused, one launch
@@ -471,7 +520,12 @@ def hidden_forward(pol: ActorCritic, obs, acts, acts2=None, rows=None, top_preac
     top = len(pol.net_arch) - 1
     for k in range(1, len(pol.net_arch)):
         if top_preact and k == top and acts2 is not None:
-            torch.bmm(acts2[k - 1], pol.p2(k, "w").transpose(1, 2), out=acts2[k])
+            xw = x6_weights(pol, acts2[k - 1].shape[1]) if k == 1 else None
+            if xw is not None:
+                xw.refresh()                 # the weights may have changed since
+                gemm_x6(acts2[k - 1], xw.fwd, acts2[k])
+            else:
+                torch.bmm(acts2[k - 1], pol.p2(k, "w").transpose(1, 2), out=acts2[k])
             continue
         for pre in ("pi", "vf"):
             torch.addmm(pol.p(f"{pre}{k}.b"), acts[pre][k - 1], pol.p(f"{pre}{k}.w").t(),

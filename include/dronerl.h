@@ -468,8 +468,10 @@ int dr_grad_finish_clip_adam_sched(const dr_grad_finish *f, int64_t n, float *pa
 size_t dr_gemm_x6_weights_bytes(int64_t batch);
 
 /* Split `batch` row-major 256 x 256 f32 weights w (consecutive) into the
-   image dr_gemm_x6 reads: transpose 0 for C = A W^T, 1 for C = A W.
-   img 16-byte aligned, dr_gemm_x6_weights_bytes(batch) bytes. */
+   image dr_gemm_x6 reads: transpose 0 for C = A W^T, 1 for C = A W, 2 for
+   both in one launch (the transpose-0 image at img, the transpose-1 image
+   right after it).  img 16-byte aligned, dr_gemm_x6_weights_bytes(batch)
+   bytes (twice that for transpose 2). */
 int dr_gemm_x6_split_weights(int64_t batch, const float *w, int transpose, void *img,
                              void *stream);
 
