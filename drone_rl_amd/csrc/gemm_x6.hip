@@ -67,6 +67,12 @@ namespace {
 #ifndef DR_X6_EARLY
 #define DR_X6_EARLY 0
 #endif
+// 1 (A/B knob): one accumulator per tile; each k16 step's five small
+// products go into a zero-started temporary that is added to it (64 fewer
+// accumulator registers, 16 f32 adds per tile and step)
+#ifndef DR_X6_ACC1
+#define DR_X6_ACC1 0
+#endif
 // 1: raise the wave's issue priority around its MFMA cluster (A/B knob)
 #ifndef DR_X6_PRIO
 #define DR_X6_PRIO 0
@@ -341,13 +347,18 @@ __global__ __launch_bounds__(XTHREADS) void gemm_x6_kernel(const float *__restri
                 const bf16x8_t *w = f.b[j];
                 acc_h[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w[0], fa[i][0],
                                                                       acc_h[i][j], 0, 0, 0);
-                f32x16_t t = acc_l[i][j];
+                f32x16_t t = DR_X6_ACC1 ? (f32x16_t){} : acc_l[i][j];
                 t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w[1], fa[i][0], t, 0, 0, 0);
                 t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w[0], fa[i][1], t, 0, 0, 0);
                 t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w[2], fa[i][0], t, 0, 0, 0);
                 t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w[0], fa[i][2], t, 0, 0, 0);
                 t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w[1], fa[i][1], t, 0, 0, 0);
-                acc_l[i][j] = t;
+                if (DR_X6_ACC1) {
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) acc_h[i][j][r] = acc_h[i][j][r] + t[r];
+                } else {
+                    acc_l[i][j] = t;
+                }
             }
         if (DR_X6_PRIO) __builtin_amdgcn_s_setprio(0);
     };

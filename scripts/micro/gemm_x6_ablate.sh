@@ -8,22 +8,23 @@ cd "$(dirname "$0")/../.."
 B=scripts/micro/build
 declare -A V=(
   [base]=""
-  [prio]="-DDR_X6_PRIO=1"
+  [acc1]="-DDR_X6_ACC1=1"
+  [acc1_early]="-DDR_X6_ACC1=1 -DDR_X6_EARLY=1"
   [noslp]="-fno-slp-vectorize"
-  [prio_noslp]="-DDR_X6_PRIO=1 -fno-slp-vectorize"
 )
 if [ "$1" = build ]; then
   for v in "${!V[@]}"; do
     rm -rf $B/$v && mkdir -p $B/$v
     make -C drone_rl_amd/csrc OBJDIR=$PWD/$B/$v/obj OUT=$PWD/$B/$v/libdronerl.so \
          KFLAGS="${V[$v]}" -j8 > /dev/null 2>&1 || { echo "build $v failed"; exit 1; }
+    rm -rf $B/$v/obj
   done
   exit 0
 fi
 for rep in 1 2; do
-  for v in base prio noslp prio_noslp; do
+  for v in base acc1 acc1_early noslp; do
     echo "== $v"
     DRONERL_LIB=$PWD/$B/$v/libdronerl.so timeout -k 10 60 python scripts/micro/gemm_x6_bench.py \
-        | grep -E '"us_x6"' || exit 1
+        | grep -E '"us_x6"|"rel_err_x6"' || exit 1
   done
 done
