@@ -131,6 +131,7 @@ SIGNATURES = {
     "dr_gemm_x6_weights_bytes": (c_size_t, [c_int64]),
     "dr_gemm_x6_split_weights": (c_int, [c_int64, _P, c_int, _P, _P]),
     "dr_gemm_x6": (c_int, [c_int64, c_int64, _P, _P, _P, _P]),
+    "dr_gemm_x6_wgrad": (c_int, [c_int64, c_int64, c_int64, _P, _P, _P, _P]),
 }
 
 _lib = None

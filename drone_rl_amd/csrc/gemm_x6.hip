@@ -429,6 +429,160 @@ __global__ __launch_bounds__(XTHREADS) void gemm_x6_kernel(const float *__restri
     }
 }
 
+// ---------------------------------------------------------------------------
+// Weight gradient of the same layer, dW[b] = G[b]^T H[b] (G = grad_z, H = the
+// layer input, both (m, 256) f32 row-major), split over C row chunks: block
+// (b, n-half, chunk) writes the 128 x 256 partial ws[b][chunk][n][k] of its
+// (m / C)-row chunk; the chunk sum is left to the caller (the
+// trainer's deferred finish sums C = 64 chunks in a fixed order).  Both
+// operands are reduced over rows, so a fragment needs 8 consecutive ROWS of
+// one column: each lane gathers them with ds_read_b32 from the f32 stage
+// images (rows of 128 / 256 floats, consecutive lanes on consecutive columns:
+// conflict-free) and splits them into the three bf16 planes in registers.
+// Stages of 32 rows arrive by global_load_lds two stages ahead (three
+// buffers); 8 waves as 2 (n) x 4 (k) of 64 x 64, the same split hi/lo
+// accumulation as gemm_x6_kernel.
+constexpr int TN_BM = 32;                          // rows per stage
+constexpr int TN_G = TN_BM * 128 * 4;              // 16 KB: G stage (128 n)
+constexpr int TN_H = TN_BM * 256 * 4;              // 32 KB: H stage (256 k)
+constexpr int TN_STAGE = TN_G + TN_H;              // 48 KB
+constexpr int TN_LDS = 3 * TN_STAGE;               // 144 KB
+constexpr int TN_NG = TN_G / 1024 / XWAVES;        // 2 glds per wave per stage
+constexpr int TN_NH = TN_H / 1024 / XWAVES;        // 4
+#define TN_VM_YOUNG 6                              // TN_NG + TN_NH
+#define TN_VM_PRO 12
+
+__global__ __launch_bounds__(XTHREADS) void gemm_x6_wgrad_kernel(
+    const float *__restrict__ Gm, const float *__restrict__ Hm, float *__restrict__ ws,
+    int64_t m, int chunks) {
+    __shared__ __attribute__((aligned(16))) uint8_t sh[TN_LDS];
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wn = wid >> 2, wk = wid & 3;
+    const int chunk = (int)(blockIdx.x % chunks);
+    const int nh = (int)((blockIdx.x / chunks) & 1);
+    const int b = (int)(blockIdx.x / chunks / 2);
+    const int64_t rows = m / chunks;
+    const int G_ = (int)(rows / TN_BM);
+    const float *Gb = Gm + ((int64_t)b * m + (int64_t)chunk * rows) * 256 + nh * 128;
+    const float *Hb = Hm + ((int64_t)b * m + (int64_t)chunk * rows) * 256;
+
+    // stage g -> buffer g % 3; a G wave-instruction moves 2 rows x 512 B, an H
+    // one 1 row x 1 KB (lane-linear, no swizzle: the b32 reads below are
+    // conflict-free on plain rows)
+    auto issue = [&](int g) {
+        uint8_t *dst = sh + (g % 3) * TN_STAGE;
+        const int64_t r0 = (int64_t)g * TN_BM;
+#pragma unroll
+        for (int i = 0; i < TN_NG; ++i) {
+            const int ins = wid + XWAVES * i;                 // rows 2 ins, 2 ins + 1
+            const int row = 2 * ins + (lane >> 5);
+            glds16(Gb + (r0 + row) * 256 + (lane & 31) * 4, lds_addr(dst + ins * 1024));
+        }
+#pragma unroll
+        for (int i = 0; i < TN_NH; ++i) {
+            const int ins = wid + XWAVES * i;                 // row ins
+            glds16(Hb + (r0 + ins) * 256 + lane * 4, lds_addr(dst + TN_G + ins * 1024));
+        }
+    };
+
+    const int fr = lane & 31, fh = lane >> 5;
+    // fragment of k16 step s: rows 16 s + 8 fh + j (j = 0..7) of one column
+    int g_off[2][2], h_off[2][2];
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            g_off[i][s2] = (16 * s2 + 8 * fh) * 512 + (wn * 64 + i * 32 + fr) * 4;
+            h_off[i][s2] = TN_G + (16 * s2 + 8 * fh) * 1024 + (wk * 64 + i * 32 + fr) * 4;
+        }
+    struct RawFrag {
+        float g[2][8];
+        float h[2][8];
+    };
+    auto read_frag = [&](int g, int s2, RawFrag &f) {
+        const uint8_t *S = sh + (g % 3) * TN_STAGE;
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                f.g[i][j] = *reinterpret_cast<const float *>(S + g_off[i][s2] + j * 512);
+                f.h[i][j] = *reinterpret_cast<const float *>(S + h_off[i][s2] + j * 1024);
+            }
+    };
+    f32x16_t acc_h[2][2], acc_l[2][2];                    // [n tile i][k tile j]
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            acc_h[i][j] = (f32x16_t){};
+            acc_l[i][j] = (f32x16_t){};
+        }
+    auto mfma_step = [&](const RawFrag &f) {
+        bf16x8_t fg[2][3], fhp[2][3];
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            u32x4_t a0, a1, a2, c0, c1, c2;
+            split8(f.g[i], a0, a1, a2);
+            split8(f.h[i], c0, c1, c2);
+            fg[i][0] = __builtin_bit_cast(bf16x8_t, a0);
+            fg[i][1] = __builtin_bit_cast(bf16x8_t, a1);
+            fg[i][2] = __builtin_bit_cast(bf16x8_t, a2);
+            fhp[i][0] = __builtin_bit_cast(bf16x8_t, c0);
+            fhp[i][1] = __builtin_bit_cast(bf16x8_t, c1);
+            fhp[i][2] = __builtin_bit_cast(bf16x8_t, c2);
+        }
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                const bf16x8_t *a = fg[i], *c = fhp[j];
+                acc_h[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], c[0], acc_h[i][j],
+                                                                      0, 0, 0);
+                f32x16_t t = acc_l[i][j];
+                t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], c[1], t, 0, 0, 0);
+                t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], c[0], t, 0, 0, 0);
+                t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], c[2], t, 0, 0, 0);
+                t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[2], c[0], t, 0, 0, 0);
+                t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], c[1], t, 0, 0, 0);
+                acc_l[i][j] = t;
+            }
+    };
+
+    issue(0);
+    issue(1);
+    issue(2);                                      // G_ >= 3 (checked by the host)
+    asm volatile("s_waitcnt vmcnt(" X6_S(TN_VM_PRO) ")\n\ts_barrier" ::: "memory");
+    RawFrag f0, f1;
+    read_frag(0, 0, f0);
+    for (int g = 0; g < G_; ++g) {
+        read_frag(g, 1, f1);
+        mfma_step(f0);
+        // stage g + 1 has landed (the loads of g + 2 may be in flight), and
+        // every wave's reads of stage g are done
+        __builtin_amdgcn_sched_barrier(0);
+        if (g + 2 < G_)
+            asm volatile("s_waitcnt vmcnt(" X6_S(TN_VM_YOUNG) ") lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        else
+            asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        if (g + 3 < G_) issue(g + 3);
+        if (g + 1 < G_) read_frag(g + 1, 0, f0);
+        __builtin_amdgcn_sched_barrier(0);
+        mfma_step(f1);
+    }
+    // D[n][k]: column k = fr, row n = (r & 3) + 8 (r >> 2) + 4 fh
+    float *out = ws + ((int64_t)b * chunks + chunk) * 256 * 256 + (int64_t)(nh * 128) * 256;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const f32x16_t v = acc_h[i][j] + acc_l[i][j];
+            float *c = out + (int64_t)(wn * 64 + i * 32 + 4 * fh) * 256 + wk * 64 + j * 32 + fr;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) c[((r & 3) + 8 * (r >> 2)) * 256] = v[r];
+        }
+}
+
 int fail_g(int code, const std::string &msg) {
     set_global_error(msg);
     return code;
@@ -486,6 +640,23 @@ int dr_gemm_x6(int64_t batch, int64_t m, const float *a, const void *img, float 
     return e == hipSuccess
                ? DR_OK
                : fail_g(DR_ERR_HIP, std::string("gemm_x6_kernel: ") + hipGetErrorString(e));
+}
+
+int dr_gemm_x6_wgrad(int64_t batch, int64_t m, int64_t chunks, const float *g, const float *h,
+                     float *ws, void *stream) {
+    if (batch < 1 || batch > 2 || chunks < 1 || m < 1 || m % chunks ||
+        (m / chunks) % TN_BM || m / chunks < 3 * TN_BM || m > (int64_t(1) << 26) || !g || !h ||
+        !ws || (((uintptr_t)g) & 15) || (((uintptr_t)h) & 15) || (((uintptr_t)ws) & 15))
+        return fail_g(DR_ERR_INVALID,
+                      "dr_gemm_x6_wgrad: bad arguments (m / chunks a multiple of 32, >= 96; "
+                      "pointers 16-byte aligned)");
+    hipLaunchKernelGGL(gemm_x6_wgrad_kernel, dim3((unsigned)(batch * 2 * chunks)),
+                       dim3(XTHREADS), 0, static_cast<hipStream_t>(stream), g, h, ws, m,
+                       (int)chunks);
+    const hipError_t e = hipGetLastError();
+    return e == hipSuccess ? DR_OK
+                           : fail_g(DR_ERR_HIP, std::string("gemm_x6_wgrad_kernel: ") +
+                                                    hipGetErrorString(e));
 }
 
 #if DR_X6_STAMPS

@@ -331,8 +331,16 @@ class FusedTrainStep:
             torch.bmm(gz.transpose(1, 2), x, out=out)
             return
         ws = self._ws2[:2 * C * N * Kd].view(2 * C, N, Kd)
-        torch.bmm(gz.reshape(2 * C, M // C, N).transpose(1, 2), x.reshape(2 * C, M // C, Kd),
-                  out=ws)
+        rows = M // C
+        if (x6_weights(self.pol, M) is not None and N == 256 and Kd == 256 and rows % 32 == 0
+                and rows >= 96):
+            from . import _lib
+            _lib.check(_lib.lib().dr_gemm_x6_wgrad(
+                2, M, C, gz.data_ptr(), x.data_ptr(), ws.data_ptr(),
+                torch.cuda.current_stream(gz.device).cuda_stream))
+        else:
+            torch.bmm(gz.reshape(2 * C, rows, N).transpose(1, 2), x.reshape(2 * C, rows, Kd),
+                      out=ws)
         if not defer:
             torch.sum(ws.view(2, C, N, Kd), dim=1, out=out)
 

@@ -80,3 +80,31 @@ def test_gemm_x6_one_net_and_bad_arguments():
     s = torch.cuda.current_stream().cuda_stream
     assert L.dr_gemm_x6(2, 100, ptr(A), ptr(W), ptr(C), s) == _lib.DR_ERR_INVALID
     assert L.dr_gemm_x6(3, 128, ptr(A), ptr(W), ptr(C), s) == _lib.DR_ERR_INVALID
+
+
+@pytest.mark.parametrize("m,chunks", [(65536, 64), (3072, 4)])
+def test_gemm_x6_wgrad_as_accurate_as_fp32(m, chunks):
+    """The weight-gradient form: ws[b][c] = G[b, chunk c]^T H[b, chunk c]
+    (torch's split-K bmm layout), against f64, relative to sum|g h|."""
+    L = _lib.lib()
+    g = torch.Generator().manual_seed(m)
+    G = (torch.randn(2, m, 256, generator=g) * 1e-3).cuda()
+    H = torch.tanh(torch.randn(2, m, 256, generator=g)).cuda()
+    ws = torch.empty(2, chunks, 256, 256, device="cuda")
+    s = torch.cuda.current_stream().cuda_stream
+    check(L.dr_gemm_x6_wgrad(2, m, chunks, ptr(G), ptr(H), ptr(ws), s))
+    rows = m // chunks
+    for c in (0, chunks - 1):
+        Gc, Hc = G[:, c * rows:(c + 1) * rows], H[:, c * rows:(c + 1) * rows]
+        ref = torch.bmm(Gc.transpose(1, 2).double(), Hc.double())
+        den = torch.bmm(Gc.transpose(1, 2).abs().double(), Hc.abs().double())
+        r32 = torch.bmm(Gc.transpose(1, 2), Hc)
+        e6 = ((ws[:, c].double() - ref).abs() / den).max().item()
+        e32 = ((r32.double() - ref).abs() / den).max().item()
+        assert e6 <= e32, (c, e6, e32)
+        assert e6 < 4e-7
+    ws2 = torch.empty_like(ws)
+    check(L.dr_gemm_x6_wgrad(2, m, chunks, ptr(G), ptr(H), ptr(ws2), s))
+    assert torch.equal(ws, ws2)
+    assert L.dr_gemm_x6_wgrad(2, m, 3 * chunks + 1, ptr(G), ptr(H), ptr(ws), s) == \
+        _lib.DR_ERR_INVALID
