@@ -8,9 +8,9 @@ cd "$(dirname "$0")/../.."
 B=scripts/micro/build
 declare -A V=(
   [base]=""
-  [acc1]="-DDR_X6_ACC1=1"
-  [acc1_early]="-DDR_X6_ACC1=1 -DDR_X6_EARLY=1"
-  [noslp]="-fno-slp-vectorize"
+  [stagger]="-DDR_X6_STAGGER=1"
+  [prio2]="-DDR_X6_PRIO=2"
+  [stagger_prio2]="-DDR_X6_STAGGER=1 -DDR_X6_PRIO=2"
 )
 if [ "$1" = build ]; then
   for v in "${!V[@]}"; do
@@ -22,7 +22,7 @@ if [ "$1" = build ]; then
   exit 0
 fi
 for rep in 1 2; do
-  for v in base acc1 acc1_early noslp; do
+  for v in base stagger prio2 stagger_prio2; do
     echo "== $v"
     DRONERL_LIB=$PWD/$B/$v/libdronerl.so timeout -k 10 60 python scripts/micro/gemm_x6_bench.py \
         | grep -E '"us_x6"|"rel_err_x6"' || exit 1
