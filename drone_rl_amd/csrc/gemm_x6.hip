@@ -41,6 +41,8 @@
 // Reference: the MLP layers of SB3's ActorCriticPolicy (MlpExtractor,
 // net_arch [256, 256], /root/reference/train.py:36-43) -- torch fp32 Linear.
 
+#include <cstdlib>
+
 #include "common.h"
 
 #pragma clang fp contract(off)
@@ -238,7 +240,7 @@ __device__ inline int swz32(int row, int chunk) {
 __global__ __launch_bounds__(XTHREADS) void gemm_x6_kernel(const float *__restrict__ A,
                                                            const uint8_t *__restrict__ img,
                                                            float *__restrict__ C, int64_t m,
-                                                           int ntiles) {
+                                                           int ntiles, int nt) {
     __shared__ __attribute__((aligned(16))) uint8_t sh[LDS_TOTAL];
     const int tid = threadIdx.x, lane = tid & 63;
     const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -387,9 +389,13 @@ __global__ __launch_bounds__(XTHREADS) void gemm_x6_kernel(const float *__restri
                 const f32x16_t v = acc_h[i][j] + acc_l[i][j];
                 float *c = Cb + (int64_t)(wm * 64 + i * 32 + fr) * XN + wn * 64 + j * 32 + 4 * fh;
 #pragma unroll
-                for (int q = 0; q < 4; ++q)
-                    *reinterpret_cast<float4 *>(c + 8 * q) =
-                        make_float4(v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]);
+                for (int q = 0; q < 4; ++q) {
+                    const float4 o = make_float4(v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]);
+                    if (nt)
+                        store_nt(reinterpret_cast<float4 *>(c + 8 * q), o);
+                    else
+                        *reinterpret_cast<float4 *>(c + 8 * q) = o;
+                }
             }
     };
 
@@ -655,9 +661,16 @@ int dr_gemm_x6(int64_t batch, int64_t m, const float *a, const void *img, float 
     }
     const int ntiles = (int)(batch * (m / XBM));
     const int grid = ntiles < n_cu ? ntiles : n_cu;       // one 144-KB block per CU
+    // DRONERL_X6_NT=1 (A/B knob, read once): nontemporal output stores --
+    // measured 4.76 vs 5.74 updates/s: the next GEMM reads these rows back
+    // from the Infinity Cache when they are stored plainly
+    static const int nt = [] {
+        const char *e = getenv("DRONERL_X6_NT");
+        return e && e[0] == '1' ? 1 : 0;
+    }();
     hipLaunchKernelGGL(gemm_x6_kernel, dim3(grid), dim3(XTHREADS), 0,
                        static_cast<hipStream_t>(stream), a, static_cast<const uint8_t *>(img),
-                       c, m, ntiles);
+                       c, m, ntiles, nt);
     const hipError_t e = hipGetLastError();
     return e == hipSuccess
                ? DR_OK

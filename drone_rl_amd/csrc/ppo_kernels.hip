@@ -834,12 +834,14 @@ __device__ inline float tanh_fast(float x) {
 
 __device__ inline float4 ld4(const float *p) { return *reinterpret_cast<const float4 *>(p); }
 
-// Activation and grad_z rows (64 MB per net per minibatch) are written with
-// nontemporal stores: linear_tanh 23.9 -> 21.6 us, heads+loss 68.8 -> 66.2 us,
-// and the first-layer backward that reads them back 31.8 -> 30.3 us
-// (rocprofv3 over 2 PPO updates).  0 restores plain stores for A/B builds.
+// Activation and grad_z rows (64 MB per net per minibatch): 1 = nontemporal
+// stores.  With the library GEMMs (round 1) they measured faster
+// (linear_tanh 23.9 -> 21.6 us, heads+loss 68.8 -> 66.2 us, the first-layer
+// backward 31.8 -> 30.3 us); with the dr_gemm_x6 GEMMs reading these rows
+// back, plain stores leave them in the Infinity Cache for those GEMMs:
+// 6.000 -> 6.033 / 5.999 -> 6.056 updates/s (bench.py, same box), so 0.
 #ifndef DR_PPO_NT
-#define DR_PPO_NT 1
+#define DR_PPO_NT 0
 #endif
 __device__ inline void st4(float *p, float4 x) {
     if (DR_PPO_NT) store_nt(reinterpret_cast<float4 *>(p), x);
