@@ -379,8 +379,28 @@ class DroneGymEnv:
     ep_num = property(lambda self: int(self._b.get_host("ep_num")[0]))
     eps = property(lambda self: float(self._b.get_host("eps")[0]))
 
-    def render(self, mode="human", close=False):
-        raise NotImplementedError("rendering is out of scope (SURVEY.md 2 #11)")
+    # ---- recording (drone.py:189-248; test.py:9-21) -------------------------
+    def _recorder(self):
+        if getattr(self, "_rec", None) is None:
+            from .render import DroneRecorder
+            self._rec = DroneRecorder()
+        return self._rec
+
+    def start_record(self, filename="drone_run.mp4", dpi=200, fps=20, bitrate=-1):
+        """Start a GIF (PillowWriter) of the frames render() draws."""
+        self._recorder().start_record(filename, dpi=dpi, fps=fps, bitrate=bitrate)
+
+    def stop_record(self):
+        """Finish and save the recording."""
+        self._recorder().stop_record()
+
+    def render(self, ax=None):
+        """Draw the drone (motors, arms, centre) and the target in 3-D from
+        the device state; grabs a frame when recording.  Returns the (4, 3)
+        motor positions drawn."""
+        return self._recorder().render(self.pos, self.euler, self.target, self.arm_length, ax)
 
     def close(self):
+        if getattr(self, "_rec", None) is not None:
+            self._rec.close()
         self._b.close()
