@@ -458,6 +458,165 @@ __global__ __launch_bounds__(XTHREADS) void gemm_x6_kernel(const float *__restri
 }
 
 // ---------------------------------------------------------------------------
+// Half-width variant: 256-thread blocks own 128 rows x 128 columns (one
+// column half of the output), 80 KB of LDS, so TWO blocks share a CU and the
+// two waves on each SIMD come from different blocks: no common barrier keeps
+// them in lockstep (in the 512-thread kernel a SIMD's two waves reach their
+// VALU / LDS phases together, stamps in DESIGN.md section 12).  Both operand
+// rings are two stages deep (A and the image of stage g + 2 issued after
+// stage g's barrier); the A rows of a row tile are read by both column-half
+// blocks (the second read mostly from L2 / the Infinity Cache).
+constexpr int HX_WAVES = 4;
+constexpr int HX_THREADS = 64 * HX_WAVES;
+constexpr int HX_BPLANE = 128 * 64;                  // 8 KB
+constexpr int HX_BSTAGE = 3 * HX_BPLANE;             // 24 KB
+constexpr int HX_LDS_A = 2 * HX_BSTAGE;              // A32 ring after the image ring
+constexpr int HX_LDS = 2 * HX_BSTAGE + 2 * A32_STAGE; // 80 KB
+#define HX_NLOAD 10                                  // 6 image + 4 A per wave per stage
+#define HX_NST 16                                    // float4 stores per lane per tile
+
+__global__ __launch_bounds__(HX_THREADS) __attribute__((amdgpu_waves_per_eu(2, 2)))
+void gemm_x6_half_kernel(const float *__restrict__ A, const uint8_t *__restrict__ img,
+                         float *__restrict__ C, int64_t m, int ntiles) {
+    __shared__ __attribute__((aligned(16))) uint8_t sh[HX_LDS];
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wm = wid >> 1, wn = wid & 1;
+    const int tiles_per_net = (int)(m / XBM);
+    const int nmine = (ntiles - (int)blockIdx.x + (int)gridDim.x - 1) / (int)gridDim.x;
+    const int G = nmine * XKC;
+    // tile t: column half t & 1 of row tile t >> 1 (global over both nets)
+    auto tile_of = [&](int g) { return (int)blockIdx.x + (g >> 3) * (int)gridDim.x; };
+    auto issue = [&](int g) {
+        const int t = tile_of(g), h = t & 1, rt = t >> 1, b = rt / tiles_per_net;
+        const uint8_t *srcb = img + (int64_t)b * W_IMG + (g & 7) * B_STAGE + h * HX_BPLANE;
+        uint8_t *dstb = sh + (g & 1) * HX_BSTAGE;
+#pragma unroll
+        for (int i = 0; i < HX_BSTAGE / 1024 / HX_WAVES; ++i) {
+            const int ins = wid + HX_WAVES * i, p = ins >> 3;
+            glds16(srcb + p * B_PLANE + (ins & 7) * 1024 + lane * 16,
+                   lds_addr(dstb + ins * 1024));
+        }
+        const float *srca = A + ((int64_t)b * m + (int64_t)(rt - b * tiles_per_net) * XBM) * XK +
+                            (g & 7) * XBK;
+        uint8_t *dsta = sh + HX_LDS_A + (g & 1) * A32_STAGE;
+#pragma unroll
+        for (int i = 0; i < A32_STAGE / 1024 / HX_WAVES; ++i) {
+            const int ins = wid + HX_WAVES * i;
+            const int row = ins * 8 + (lane >> 3);
+            const int chunk = (lane & 7) ^ ((row >> 1) & 7);
+            glds16(srca + (int64_t)row * XK + chunk * 4, lds_addr(dsta + ins * 1024));
+        }
+    };
+    const int fr = lane & 31, fh = lane >> 5;
+    int a_off[2][2][2], b_off[2][2];
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) {
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            a_off[i][s2][0] = swz32(wm * 64 + i * 32 + fr, 4 * s2 + 2 * fh);
+            a_off[i][s2][1] = swz32(wm * 64 + i * 32 + fr, 4 * s2 + 2 * fh + 1);
+            b_off[i][s2] = swz(wn * 64 + i * 32 + fr, 2 * s2 + fh);
+        }
+    }
+    struct Frag {
+        float4 a[2][2];
+        bf16x8_t b[2][3];
+    };
+    auto read_frag = [&](int g, int s2, Frag &f) {
+        const uint8_t *SA = sh + HX_LDS_A + (g & 1) * A32_STAGE;
+        const uint8_t *SB = sh + (g & 1) * HX_BSTAGE;
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            f.a[i][0] = *reinterpret_cast<const float4 *>(SA + a_off[i][s2][0]);
+            f.a[i][1] = *reinterpret_cast<const float4 *>(SA + a_off[i][s2][1]);
+#pragma unroll
+            for (int p = 0; p < 3; ++p)
+                f.b[i][p] = *reinterpret_cast<const bf16x8_t *>(SB + p * HX_BPLANE + b_off[i][s2]);
+        }
+    };
+    f32x16_t acc_h[2][2], acc_l[2][2];
+    auto zero_acc = [&]() {
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                acc_h[i][j] = (f32x16_t){};
+                acc_l[i][j] = (f32x16_t){};
+            }
+    };
+    auto mfma_step = [&](const Frag &f) {
+        bf16x8_t fa[2][3];
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            const float x[8] = {f.a[i][0].x, f.a[i][0].y, f.a[i][0].z, f.a[i][0].w,
+                                f.a[i][1].x, f.a[i][1].y, f.a[i][1].z, f.a[i][1].w};
+            u32x4_t h, mm, l;
+            split8(x, h, mm, l);
+            fa[i][0] = __builtin_bit_cast(bf16x8_t, h);
+            fa[i][1] = __builtin_bit_cast(bf16x8_t, mm);
+            fa[i][2] = __builtin_bit_cast(bf16x8_t, l);
+        }
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                const bf16x8_t *w = f.b[j];
+                acc_h[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w[0], fa[i][0],
+                                                                      acc_h[i][j], 0, 0, 0);
+                f32x16_t t = acc_l[i][j];
+                t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w[1], fa[i][0], t, 0, 0, 0);
+                t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w[0], fa[i][1], t, 0, 0, 0);
+                t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w[2], fa[i][0], t, 0, 0, 0);
+                t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w[0], fa[i][2], t, 0, 0, 0);
+                t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w[1], fa[i][1], t, 0, 0, 0);
+                acc_l[i][j] = t;
+            }
+    };
+    auto epilogue = [&](int g) {
+        const int t = tile_of(g), h = t & 1, rt = t >> 1, b = rt / tiles_per_net;
+        float *Cb = C + ((int64_t)b * m + (int64_t)(rt - b * tiles_per_net) * XBM) * XN + h * 128;
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                const f32x16_t v = acc_h[i][j] + acc_l[i][j];
+                float *c = Cb + (int64_t)(wm * 64 + i * 32 + fr) * XN + wn * 64 + j * 32 + 4 * fh;
+#pragma unroll
+                for (int q = 0; q < 4; ++q)
+                    *reinterpret_cast<float4 *>(c + 8 * q) =
+                        make_float4(v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]);
+            }
+    };
+
+    zero_acc();
+    issue(0);
+    issue(1);                                     // G >= 8
+    asm volatile("s_waitcnt vmcnt(" X6_S(HX_NLOAD) ")\n\ts_barrier" ::: "memory");
+    Frag f0, f1;
+    read_frag(0, 0, f0);
+    for (int g = 0; g < G; ++g) {
+        read_frag(g, 1, f1);
+        mfma_step(f0);
+        // stage g + 1 has landed (issued a stage ago; younger: the previous
+        // tile's stores) and every wave's reads of stage g are done
+        __builtin_amdgcn_sched_barrier(0);
+        if ((g & 7) == 0 && g > 0)
+            asm volatile("s_waitcnt vmcnt(" X6_S(HX_NST) ") lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        else
+            asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        if (g + 2 < G) issue(g + 2);
+        if (g + 1 < G) read_frag(g + 1, 0, f0);
+        __builtin_amdgcn_sched_barrier(0);
+        mfma_step(f1);
+        if ((g & 7) == 7) {
+            epilogue(g);
+            zero_acc();
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
 // Weight gradient of the same layer, dW[b] = G[b]^T H[b] (G = grad_z, H = the
 // layer input, both (m, 256) f32 row-major), split over C row chunks: block
 // (b, n-half, chunk) writes the 128 x 256 partial ws[b][chunk][n][k] of its
@@ -658,6 +817,22 @@ int dr_gemm_x6(int64_t batch, int64_t m, const float *a, const void *img, float 
             hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
             n_cu < 1)
             n_cu = 256;
+    }
+    // DRONERL_X6_HALF=1: the half-width kernel (two 80-KB blocks per CU)
+    static const int half = [] {
+        const char *e = getenv("DRONERL_X6_HALF");
+        return e && e[0] == '1' ? 1 : 0;
+    }();
+    if (half) {
+        const int nt2 = (int)(batch * (m / XBM) * 2);
+        const int grid2 = nt2 < 2 * n_cu ? nt2 : 2 * n_cu;
+        hipLaunchKernelGGL(gemm_x6_half_kernel, dim3(grid2), dim3(HX_THREADS), 0,
+                           static_cast<hipStream_t>(stream), a,
+                           static_cast<const uint8_t *>(img), c, m, nt2);
+        const hipError_t e2 = hipGetLastError();
+        return e2 == hipSuccess ? DR_OK
+                                : fail_g(DR_ERR_HIP, std::string("gemm_x6_half_kernel: ") +
+                                                         hipGetErrorString(e2));
     }
     const int ntiles = (int)(batch * (m / XBM));
     const int grid = ntiles < n_cu ? ntiles : n_cu;       // one 144-KB block per CU
