@@ -874,6 +874,11 @@ struct LayerPair {
 #ifndef DR_LT_SCALAR
 #define DR_LT_SCALAR 1
 #endif
+// rows per wave and iteration of linear_tanh_kernel (A/B knob: 1 | 2; 2
+// measured 38.1 vs 37.6-37.8 us per call, scripts/micro/ppo_prof.sh)
+#ifndef DR_LT_RPI
+#define DR_LT_RPI 1
+#endif
 // blocks per net of linear_tanh_kernel (A/B knob)
 #ifndef DR_LT_MAXB
 #define DR_LT_MAXB 1024
@@ -911,7 +916,55 @@ __global__ __launch_bounds__(kBlock) void linear_tanh_kernel(int64_t m, int n,
             for (int k = 0; k < K; ++k) wr[q][k] = flat[q * K + k];
         }
     }
-#if DR_LT_SCALAR
+#if DR_LT_SCALAR && DR_LT_RPI == 2
+    // two rows per iteration (r, r + stride): two independent FMA / tanh
+    // chains per wave and two stores in flight; the next pair's inputs are
+    // scalar-loaded before this pair's arithmetic
+    const int64_t stride = (int64_t)gridDim.x * 4;
+    int64_t r = (int64_t)blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(wid);
+    auto xrow = [&](int64_t q) -> int64_t { return rows ? (int64_t)rows[q] : q; };
+    float xn[2][K];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+        const int64_t ru = r + u * stride;
+        if (ru < m) {
+            const float *xr = x + xrow(ru) * K;
+#pragma unroll
+            for (int k = 0; k < K; ++k) xn[u][k] = xr[k];
+        }
+    }
+    for (; r < m; r += 2 * stride) {
+        float xv[2][K];
+#pragma unroll
+        for (int u = 0; u < 2; ++u)
+#pragma unroll
+            for (int k = 0; k < K; ++k) xv[u][k] = xn[u][k];
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            const int64_t rn = r + (2 + u) * stride;
+            if (rn < m) {
+                const float *xr = x + xrow(rn) * K;
+#pragma unroll
+                for (int k = 0; k < K; ++k) xn[u][k] = xr[k];
+            }
+        }
+        float acc[2][4] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+        for (int k = 0; k < K; ++k)
+#pragma unroll
+            for (int u = 0; u < 2; ++u)
+#pragma unroll
+                for (int q = 0; q < 4; ++q) acc[u][q] = fmaf(xv[u][k], wr[q][k], acc[u][q]);
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            const int64_t ru = r + u * stride;
+            if (act && ru < m)
+                st4(h + ru * n + c0,
+                    make_float4(tanh_fast(acc[u][0] + bb[0]), tanh_fast(acc[u][1] + bb[1]),
+                                tanh_fast(acc[u][2] + bb[2]), tanh_fast(acc[u][3] + bb[3])));
+        }
+    }
+#elif DR_LT_SCALAR
     // rows are wave-strided; row r is wave-uniform, so its K inputs are
     // scalar loads straight into SGPRs (no per-lane load + K readlanes), the
     // next row's issued before this row's arithmetic
