@@ -8,4 +8,4 @@ cd "$(dirname "$0")/.."
 mkdir -p gpurun_out
 EPS=${1:-4.8}; STEPS=${2:-2.1e9}; SEED=${3:-0}
 timeout -k 10 900 python -u -m drone_rl_amd.train --initial-eps $EPS --total-steps $STEPS \
-  --log-every 10 --seed $SEED --checkpoint /tmp/c3_eps$EPS.pt > gpurun_out/c3_eps${EPS}_s$SEED.jsonl 2> gpurun_out/c3_eps${EPS}_s$SEED.err
+  --log-every 10 --seed $SEED --checkpoint /tmp/c3_eps${EPS}_s$SEED.pt > gpurun_out/c3_eps${EPS}_s$SEED.jsonl 2> gpurun_out/c3_eps${EPS}_s$SEED.err

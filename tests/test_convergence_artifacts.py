@@ -6,7 +6,7 @@ committed artefacts (CPU only; every log is a builder run):
   tests/golden/c1_anchor.json          oracle/sb3_c1.py, 3 seeds, 2e6 steps
   profiles/r01_ppo_c3_converge.jsonl   GPU PPO, 65,536 envs, 2x256 (train.py), eps 0
   profiles/r02_ppo_c3_eps*.jsonl       the same at eps 0.5 / 1 / 2 / 4.8 (c3_matched.sh),
-                                       and at eps 0 on the x6 GEMMs (r02_ppo_c3_eps0_x6_s0)
+                                       and at eps 0 on the x6 GEMMs (r02_ppo_c3_eps0_x6_s0..2)
   profiles/r01_ppo_c1_gpu.jsonl        GPU PPO with SB3 defaults on 1 env
 """
 import json
@@ -39,7 +39,8 @@ def _anchor_at(a, eps):
 
 # configs[2] GPU runs at a fixed curriculum level (every env starts at eps;
 # the per-env 2000-episode bump never fires in these runs), scripts/c3_matched.sh
-C3_AT_EPS = {0.0: ["r01_ppo_c3_converge.jsonl", "r02_ppo_c3_eps0_x6_s0.jsonl"],
+C3_AT_EPS = {0.0: ["r01_ppo_c3_converge.jsonl", "r02_ppo_c3_eps0_x6_s0.jsonl",
+                   "r02_ppo_c3_eps0_x6_s1.jsonl", "r02_ppo_c3_eps0_x6_s2.jsonl"],
              0.5: ["r02_ppo_c3_eps0.5_s0.jsonl"],
              1.0: ["r02_ppo_c3_eps1.0_s0.jsonl"],
              2.0: ["r02_ppo_c3_eps2.0_s0.jsonl"],
