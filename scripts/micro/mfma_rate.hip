@@ -11,8 +11,12 @@ __global__ __launch_bounds__(512) void k(float *out, int iters, float seed) {
     for (int i = 0; i < 2; ++i)
         for (int p = 0; p < 3; ++p)
             for (int e = 0; e < 8; ++e) {
-                a[i][p][e] = (__bf16)(seed * (threadIdx.x + 7 * e + 3 * p + i) * 0.001f);
-                b[i][p][e] = (__bf16)(seed * (threadIdx.x * 3 + 5 * e + p - i) * 0.0013f);
+                // hashed (random-looking) operands: toggling bits set the power
+                unsigned hsh = (threadIdx.x * 2654435761u) ^ ((e * 8 + p * 2 + i) * 40503u) ^
+                               (unsigned)(seed * 977.f);
+                hsh ^= hsh >> 13; hsh *= 0x5bd1e995u; hsh ^= hsh >> 15;
+                a[i][p][e] = (__bf16)(((hsh & 0xffff) / 32768.f - 1.f));
+                b[i][p][e] = (__bf16)((((hsh >> 16) & 0xffff) / 32768.f - 1.f) * 0.06f);
             }
     f32x16_t h[2][2] = {}, l[2][2] = {};
     for (int it = 0; it < iters; ++it) {
