@@ -20,7 +20,11 @@ The JSON line also carries
                 the fixture-pinned numpy port (oracle/cpu_baseline.py),
                 run BEFORE the GPU is touched;
   ppo           PPO updates/s for configs[2] (65,536 envs, 2x256 tanh MLP,
-                GAE lambda 0.95), when --ppo-updates > 0.
+                GAE lambda 0.95), when --ppo-updates > 0;
+  rollout_kernel  the same envs and action stream through the K-step
+                rollout kernel (dr_rollout: K steps per launch, state in
+                registers, every step's outputs written), separately
+                reported; `value` stays on the single-step kernel.
 """
 import argparse
 import json
@@ -59,6 +63,8 @@ def parse():
     ap.add_argument("--ppo-steps", type=int, default=32, help="rollout length T")
     ap.add_argument("--extra", action="store_true",
                     help="also time the f32-state mode and the 4M-env size")
+    ap.add_argument("--rollout-k", type=int, default=32,
+                    help="steps per launch of the K-step rollout kernel line (0 = skip)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"))
     return ap.parse_args()
 
@@ -167,6 +173,55 @@ def time_env(args, dtype_name, n_envs, rank, world, device, steps, warmup, varia
     b.close()
     del graph
     return elapsed, gpu_ms, ep
+
+
+def time_rollout(args, n_envs, device, k, reps, gen):
+    """The K-step rollout kernel (dr_rollout; dr_rollout_random when gen):
+    `reps` launches of k steps each over the same 65,536 envs, captured in
+    one hipGraph; returns the per-launch GPU time (HIP events on the launch
+    stream) in seconds.  Reported beside the headline, never as `value`
+    (the headline stays on the single-step kernel PPO uses)."""
+    import torch
+
+    from drone_rl_amd import DroneBatch, random_actions
+    dtype = torch.float64 if args.state_dtype == "f64" else torch.float32
+    b = DroneBatch(n_envs, "gym", dtype=dtype, device=device, seed=2025, auto_reset=True)
+    b.reset()
+    obs = torch.empty(k, n_envs, b.obs_dim, device=device)
+    rew = torch.empty(k, n_envs, device=device)
+    done = torch.empty(k, n_envs, dtype=torch.uint8, device=device)
+    acts = torch.empty(reps, k, n_envs, 4, device=device)
+    for r in range(reps):
+        for t in range(k):
+            random_actions(n_envs, seed=7, step=r * k + t, out=acts[r, t])
+
+    def launch(r):
+        if gen:
+            b.rollout(k, None, seed=7, step0=r * k, obs_out=obs, rew_out=rew, done_out=done)
+        else:
+            b.rollout(k, acts[r], obs_out=obs, rew_out=rew, done_out=done)
+    for r in range(2):
+        launch(r)
+    stream = torch.cuda.current_stream(device)
+    s = torch.cuda.Stream(device)
+    s.wait_stream(stream)
+    with torch.cuda.stream(s):
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=s):
+            for r in range(reps):
+                launch(r)
+    stream.wait_stream(s)
+    g.replay()
+    torch.cuda.synchronize(device)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(stream)
+    g.replay()
+    e1.record(stream)
+    torch.cuda.synchronize(device)
+    per_launch = e0.elapsed_time(e1) / 1e3 / reps
+    b.close()
+    del g
+    return per_launch
 
 
 def time_ppo(args, rank, world, device):
@@ -317,6 +372,25 @@ def main():
                                          "peak": HBM_PEAK_GBS, "unit": "GB/s",
                                          "frac": round(ach4 / HBM_PEAK_GBS, 4),
                                          "traffic": tr4}}
+    if world == 1 and args.rollout_k > 0:
+        # SURVEY 7 "hard parts" (a): the K-step random-policy rollout kernel,
+        # same envs and action stream, every step's obs / rew / done written
+        # (bitwise the K single steps; tests/test_rollout_gpu.py)
+        k, sb = args.rollout_k, (8 if args.state_dtype == "f64" else 4)
+        state_b = (15 * sb + 4) + (12 * sb + 4)   # state in + out once per launch
+        ro = {"kernel": "env_rollout_kernel", "k": k, "envs": N, "launches": 10}
+        for gen in (False, True):
+            pl = time_rollout(args, N, device, k, 10, gen)
+            bpe = (65 if gen else 81) + state_b / k
+            ach = N * k * bpe / pl / 1e9
+            ro["random_policy_in_kernel" if gen else "actions_from_hbm"] = {
+                "env_steps_per_s": round(N * k / pl, 1),
+                "avg_launch_us": round(pl * 1e6, 3), "us_per_step": round(pl * 1e6 / k, 3),
+                "bytes_per_env_step": round(bpe, 2),
+                "roofline": {"bound": "valu (f64 issue; DESIGN.md 6)", "achieved": round(ach, 1),
+                             "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                             "frac": round(ach / HBM_PEAK_GBS, 4)}}
+        out["rollout_kernel"] = ro
     if cpu is not None:
         out["cpu_baseline"] = cpu
     if args.ppo_updates > 0:

@@ -90,9 +90,6 @@ __device__ unsigned long long g_stamps[16384 * 8];
 #ifndef DR_HOIST_RESET
 #define DR_HOIST_RESET 0
 #endif
-// 1: per-step outputs and state are written with nontemporal stores.  They
-// stream to HBM while the kernel runs instead of sitting dirty in L2 until
-// the end-of-kernel writeback (4-9 % faster from 65,536 to 4M envs).
 // waves per workgroup of env_step_kernel (A/B builds: 1, 2, 4)
 #ifndef DR_ENV_WPB
 #define DR_ENV_WPB 4
@@ -106,6 +103,9 @@ constexpr int kEnvBlock = 64 * DR_ENV_WPB;
 #define DR_OBS_ONCE 1
 #endif
 
+// 1: per-step outputs and state are written with nontemporal stores.  They
+// stream to HBM while the kernel runs instead of sitting dirty in L2 until
+// the end-of-kernel writeback (4-9 % faster from 65,536 to 4M envs).
 #ifndef DR_NT_STORES
 #define DR_NT_STORES 1
 #endif
@@ -434,22 +434,32 @@ __device__ inline void make_obs(const S st[F_N], float ob[OD],
 // One physics step on registers.  Returns the reward, sets `crash` (z<0 or
 // |p|>50).  VAR selects the two places the variants differ (W row 3 and the
 // reward form / bonus radius).
-template <typename S, int VAR>
-__device__ inline S physics_step(S st[F_N], float4 act, S dt, bool &crash) {
+// The action's motor mixes (drone.py:106, 113-117): total thrust and the
+// three torques' f32 sums, before any state is involved.
+struct MotorMix {
+    float thr, phi, theta, psi;
+};
+__device__ inline MotorMix motor_mix(float4 act) {
     const float a0 = act.x, a1 = act.y, a2 = act.z, a3 = act.w;
+    return MotorMix{((a0 + a1) + a2) + a3, ((a0 + a1) - a2) - a3,
+                    ((-a0 + a1) + a2) - a3, ((a0 - a1) + a2) - a3};
+}
+
+template <typename S, int VAR>
+__device__ inline S physics_step_mixed(S st[F_N], MotorMix mx, S dt, bool &crash) {
 #if DR_ABLATE == 6
     // diagnostic: no physics (loads / stores / reset / obs as built)
 #pragma unroll
-    for (int k = 0; k < 12; ++k) st[k] += (S)a0 * (S)1e-300;
+    for (int k = 0; k < 12; ++k) st[k] += (S)mx.thr * (S)1e-300;
     crash = st[F_POS + 2] < (S)0;
-    return (S)a1;
+    return (S)mx.phi;
 #endif
     // thrust / torques (drone.py:106, 113-117): f32 sums, f64 factor product,
     // the yaw torque stays f32.
-    const float thr = ((a0 + a1) + a2) + a3;
-    const S tau_phi = (S)kFactor * (S)(((a0 + a1) - a2) - a3);
-    const S tau_theta = (S)kFactor * (S)(((-a0 + a1) + a2) - a3);
-    const float tau_psi = kKyaw32 * (((a0 - a1) + a2) - a3);
+    const float thr = mx.thr;
+    const S tau_phi = (S)kFactor * (S)mx.phi;
+    const S tau_theta = (S)kFactor * (S)mx.theta;
+    const float tau_psi = kKyaw32 * mx.psi;
 
     // One sincos per angle: a shared range reduction yields exactly the
     // separate sin() and cos() results at half the instructions.
@@ -525,6 +535,11 @@ __device__ inline S physics_step(S st[F_N], float4 act, S dt, bool &crash) {
     const S pn2 = (px * px + py * py) + pz * pz;
     crash = (pz < (S)0) || (pn2 > (S)2500);
     return r;
+}
+
+template <typename S, int VAR>
+__device__ inline S physics_step(S st[F_N], float4 act, S dt, bool &crash) {
+    return physics_step_mixed<S, VAR>(st, motor_mix(act), dt, crash);
 }
 
 // Per-wave variant: each wave stages its own 64 rows (3,840 B) and writes
@@ -786,6 +801,207 @@ __global__ __launch_bounds__(kEnvBlock) void env_step_kernel(EnvView<S> v,
     store_obs_block<OD>(reinterpret_cast<float *>(sh4), ob, io.obs, base, v.n);
 #endif
     DR_STAMP(5);
+}
+
+// ----------------------------------------------------------------------------
+// K-step rollout: K successive steps of the same batch in ONE launch, the
+// state held in registers between steps.  Equivalent, output for output and
+// bit for bit, to K env_step_kernel launches (dr_step with no terminal obs,
+// no VecMonitor) on actions[t] -- or, GEN, on the random policy's actions
+// generated in-kernel with random_actions_kernel's exact Philox draw for
+// step step0 + t.  This is the random-policy rollout loop (a = sample();
+// obs, r, done = env.step(a), K times; drone.py:81-159 per step, the
+// DummyVecEnv auto-reset in between) with the per-step state round trip
+// through HBM and the per-launch gap removed: per env-step it moves the
+// outputs (obs 4*OD + rew 4 + done 1 B) and the action (16 B, none when
+// GEN), plus the state once per launch.
+//
+// Every step's outputs are stored as they are formed (rew / done per lane,
+// obs through the per-wave LDS staging), so the stores of step t drain
+// while step t+1 computes; the next step's action load is issued one step
+// ahead.  The fields a reset changes outside the 12 dynamic ones (target,
+// motion; ep_num / eps are written by the reset itself) are written back
+// at the end only for lanes that reset during the launch.
+// ----------------------------------------------------------------------------
+struct RolloutIO {
+    const float *actions;   // (K, n, 4); unused when GEN
+    float *act_out;         // GEN: optional (K, n, 4) copy of the drawn actions
+    float *obs;             // (K, n, OD)
+    float *rew;             // (K, n)
+    uint8_t *done;          // (K, n)
+    int32_t k;
+    uint32_t a_k0, a_k1;    // action Philox key
+    uint64_t a_step0;
+    float a_lo, a_span;
+    int auto_reset;
+};
+
+template <typename S, int VAR, int RPW, bool GEN>
+__global__ __launch_bounds__(kEnvBlock) void env_rollout_kernel(EnvView<S> v, RolloutIO io,
+                                                                FieldPtrs<S> fp) {
+    constexpr int OD = VAR == DR_VARIANT_GYM ? 15 : (VAR == DR_VARIANT_MOVING ? 18 : 12);
+    constexpr bool GYMLIKE = VAR != DR_VARIANT_VECTORIZED;
+    __shared__ float4 sh4[kEnvBlock * OD / 4];
+    const int64_t n_ = v.n;
+    const int64_t base = (int64_t)blockIdx.x * (DR_ENV_WPB * RPW);
+    const int lane_ = threadIdx.x & 63;
+    const int64_t i_own = lane_ < RPW ? base + (threadIdx.x >> 6) * RPW + lane_ : n_;
+    const bool live = i_own < n_;
+    const int64_t i = live ? i_own : n_ - 1;
+    const uint64_t gid = (uint64_t)(v.env_id_offset + i);
+
+    S st[F_N];
+#pragma unroll
+    for (int k = F_EUL; k < F_N - 3; ++k) st[k] = *at(fp.p[k], i);
+#pragma unroll
+    for (int k = 0; k < F_EUL; ++k) st[k] = *at(fp.p[k], i);
+    S cen[3];
+    float mp[9], tvel[3];
+    if constexpr (VAR == DR_VARIANT_GYM) {
+#pragma unroll
+        for (int k = F_TGT; k < F_N; ++k) st[k] = *at(fp.p[k], i);
+    } else if constexpr (VAR == DR_VARIANT_MOVING) {
+#pragma unroll
+        for (int k = 0; k < 3; ++k) cen[k] = *at(fp.p[F_TGT + k], i);
+#pragma unroll
+        for (int k = 0; k < 9; ++k) mp[k] = *at(v.mot + k * v.stride, i);
+    } else {
+        st[F_TGT + 0] = (S)0;
+        st[F_TGT + 1] = (S)0;
+        st[F_TGT + 2] = (S)10.0;
+    }
+    int32_t step = *at(fp.step, i);
+    int32_t ep_num = 0;
+    double eps = 0.0;
+    if constexpr (GYMLIKE) {
+        ep_num = *at(fp.ep_num, i);
+        eps = *at(fp.eps, i);
+    }
+    bool reset_any = false;
+    float ob[OD];
+
+    // one step on action `act`: the body of env_step_kernel on registers
+    // The Philox keys (reset draws; GEN: actions) are re-declared opaque
+    // once per step, so the compiler cannot hoist the 10-round key
+    // schedules out of the loop: hoisted, their 40 words spilled to VGPR
+    // lanes, and every round paid a v_readlane plus a hazard s_nop.
+    EnvView<S> vk = v;
+    auto step_one = [&](const MotorMix mx, const int t) {
+        asm volatile("" : "+s"(vk.seed_lo), "+s"(vk.seed_hi));
+        if constexpr (VAR == DR_VARIANT_MOVING)
+            moving_target(cen, mp, step + 1, (float)v.dt, &st[F_TGT], tvel);
+        bool crash;
+        const S r = physics_step_mixed<S, VAR>(st, mx, v.dt, crash);
+        step += 1;
+        const bool done = live && (crash || (step >= v.max_steps));
+        const int64_t row = (int64_t)t * n_;
+        if (live) {
+            st_out(at(io.rew + row, i), (float)r);
+            st_out(at(io.done + row, i), (uint8_t)done);
+        }
+        if constexpr (GYMLIKE) {
+            if (done && io.auto_reset) {
+                step = 0;
+                reset_any = true;
+                if constexpr (VAR == DR_VARIANT_GYM) {
+                    gym_reset_regs(vk, i, 0, st, ep_num, eps);
+                } else {
+                    moving_reset_regs(vk, i, 0, st, cen, mp, ep_num, eps);
+                    moving_target(cen, mp, 0, (float)v.dt, &st[F_TGT], tvel);
+                }
+                // the curriculum counters gym/moving_reset_regs just wrote
+                // (drone.py:61, 68-70), carried on in registers
+                ep_num += 1;
+                if (ep_num % 2000 == 0) eps += 0.1;
+            }
+        }
+        make_obs<S, OD>(st, ob, tvel);
+        if (!live) {
+#pragma unroll
+            for (int k = 0; k < OD; ++k) ob[k] = 0.f;
+        }
+        // (plain stores for these outputs measured the same: 60.2 / 62.2 us
+        // per 32-step launch at 65,536 envs)
+        store_obs_wave<OD, RPW>(reinterpret_cast<float *>(sh4), ob, io.obs + row * OD, n_);
+    };
+
+    if constexpr (GEN) {
+        for (int t = 0; t < io.k; ++t) {
+            const uint64_t s = io.a_step0 + (uint64_t)t;
+            uint32_t ak0 = io.a_k0, ak1 = io.a_k1;
+            asm volatile("" : "+s"(ak0), "+s"(ak1));
+            const u32x4 r = philox4x32_10(
+                u32x4{(uint32_t)s, (uint32_t)(s >> 32), (uint32_t)gid,
+                      TAG_ACTION ^ (uint32_t)(gid >> 32)},
+                ak0, ak1);
+            const float4 act = make_float4(io.a_lo + io.a_span * u01_f32(r.x),
+                                           io.a_lo + io.a_span * u01_f32(r.y),
+                                           io.a_lo + io.a_span * u01_f32(r.z),
+                                           io.a_lo + io.a_span * u01_f32(r.w));
+            if (io.act_out && live)
+                st_out(at(reinterpret_cast<float4 *>(io.act_out) + (int64_t)t * n_, i), act);
+            step_one(motor_mix(act), t);
+        }
+    } else {
+        // The next step's action is loaded one step ahead, into the same
+        // registers, right after this step's motor mixes are formed from
+        // them (their only use), by an asm load the compiler does not
+        // track: its own waitcnt pass, at a loop back edge, waits vmcnt(0)
+        // for any load in flight -- draining every store of the step as
+        // well (vmcnt counts both, in issue order).  The wait before the
+        // next step's mixes is instead vmcnt(2): younger than the load are
+        // at least that step's rew and done stores whenever the wave has a
+        // live lane (a wave with none stores nothing and its lanes' results
+        // are discarded).  The first action is an ordinary load.
+        typedef float f4v __attribute__((ext_vector_type(4)));
+        const float4 *const acts = reinterpret_cast<const float4 *>(io.actions);
+        const float4 a_first = *at(acts, i);
+        f4v act = {a_first.x, a_first.y, a_first.z, a_first.w};
+        // every preheader load landed before the loop: otherwise the
+        // compiler places the waits for them at their first uses inside
+        // the loop (ep_num / eps in the reset branch, a state component in
+        // the physics), where they run every step as vmcnt(0)
+        asm volatile("" ::"v"(ep_num), "v"(eps), "v"(act), "v"(step));
+#pragma unroll
+        for (int k = 0; k < F_N; ++k) asm volatile("" ::"v"(st[k]));
+        if constexpr (VAR == DR_VARIANT_MOVING) {
+#pragma unroll
+            for (int k = 0; k < 3; ++k) asm volatile("" ::"v"(cen[k]));
+#pragma unroll
+            for (int k = 0; k < 9; ++k) asm volatile("" ::"v"(mp[k]));
+        }
+        for (int t = 0; t < io.k; ++t) {
+            if (t > 0) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+            const MotorMix mx = motor_mix(make_float4(act.x, act.y, act.z, act.w));
+            asm volatile("" ::"v"(mx.thr), "v"(mx.phi), "v"(mx.theta), "v"(mx.psi));
+            __builtin_amdgcn_sched_barrier(0);
+            if (t + 1 < io.k) {
+                const float4 *pa = at(acts + (int64_t)(t + 1) * n_, i);
+                asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(act) : "v"(pa) : "memory");
+            }
+            __builtin_amdgcn_sched_barrier(0);
+            step_one(mx, t);
+        }
+        // a wave with no live lane never waited for its loads: none may
+        // still be writing registers the code below reuses
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    if (live) {
+#pragma unroll
+        for (int k = 0; k < 12; ++k) st_out(at(fp.p[k], i), st[k]);
+        st_out(at(fp.step, i), step);
+        if (reset_any) {
+            if constexpr (VAR == DR_VARIANT_GYM) {
+#pragma unroll
+                for (int k = F_TGT; k < F_N; ++k) *at(fp.p[k], i) = st[k];
+            } else if constexpr (VAR == DR_VARIANT_MOVING) {
+#pragma unroll
+                for (int k = 0; k < 3; ++k) *at(fp.p[F_TGT + k], i) = cen[k];
+#pragma unroll
+                for (int k = 0; k < 9; ++k) *at(v.mot + k * v.stride, i) = mp[k];
+            }
+        }
+    }
 }
 
 // ----------------------------------------------------------------------------
@@ -1326,6 +1542,44 @@ int dispatch_step(dr_handle *h, const StepIO &io, hipStream_t st) {
                : launch_step<float, DR_VARIANT_VECTORIZED, MON>(h, io, st);
 }
 
+template <typename S, int VAR, bool GEN>
+int launch_rollout(dr_handle *h, const RolloutIO &io, hipStream_t st) {
+    EnvView<S> v = view_of<S>(h);
+    FieldPtrs<S> fp;
+    for (int k = 0; k < F_N; ++k) fp.p[k] = v.field(k);
+    fp.step = v.step;
+    fp.ep_num = v.ep_num;
+    fp.eps = v.eps;
+    // rows per wave: 64 unless DRONERL_ROLLOUT_RPW=32 (A/B)
+    int rpw = 64;
+    if (const char *r = std::getenv("DRONERL_ROLLOUT_RPW")) rpw = std::atoi(r) == 32 ? 32 : 64;
+    if (rpw == 32)
+        hipLaunchKernelGGL((env_rollout_kernel<S, VAR, 32, GEN>),
+                           dim3(grid_for(h->n, DR_ENV_WPB * 32)), dim3(kEnvBlock), 0, st, v, io,
+                           fp);
+    else
+        hipLaunchKernelGGL((env_rollout_kernel<S, VAR, 64, GEN>),
+                           dim3(grid_for(h->n, DR_ENV_WPB * 64)), dim3(kEnvBlock), 0, st, v, io,
+                           fp);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess)
+        return fail(h, DR_ERR_HIP, std::string("env_rollout_kernel: ") + hipGetErrorString(e));
+    return DR_OK;
+}
+
+template <bool GEN>
+int dispatch_rollout(dr_handle *h, const RolloutIO &io, hipStream_t st) {
+    const bool f64 = h->cfg.state_dtype == DR_STATE_F64;
+    if (h->cfg.variant == DR_VARIANT_GYM)
+        return f64 ? launch_rollout<double, DR_VARIANT_GYM, GEN>(h, io, st)
+                   : launch_rollout<float, DR_VARIANT_GYM, GEN>(h, io, st);
+    if (h->cfg.variant == DR_VARIANT_MOVING)
+        return f64 ? launch_rollout<double, DR_VARIANT_MOVING, GEN>(h, io, st)
+                   : launch_rollout<float, DR_VARIANT_MOVING, GEN>(h, io, st);
+    return f64 ? launch_rollout<double, DR_VARIANT_VECTORIZED, GEN>(h, io, st)
+               : launch_rollout<float, DR_VARIANT_VECTORIZED, GEN>(h, io, st);
+}
+
 int check_rng(dr_handle *h) {
     if (h->cfg.rng_mode == DR_RNG_HOST_UNIFORMS && h->host_u == nullptr &&
         h->cfg.variant != DR_VARIANT_VECTORIZED)
@@ -1500,6 +1754,56 @@ int dr_step_monitored(dr_handle *h, const float *actions, float *obs_out,
                       float *ep_return_out, int32_t *ep_length_out, void *stream) {
     return step_common(h, actions, obs_out, rew_out, done_out, terminal_obs_out,
                        ep_return_out, ep_length_out, true, stream);
+}
+
+static int rollout_common(dr_handle *h, int32_t k, RolloutIO io, bool gen, void *stream) {
+    if (!h) return fail(nullptr, DR_ERR_INVALID, "dr_rollout: null handle");
+    if (k < 0) return fail(h, DR_ERR_INVALID, "dr_rollout: k < 0");
+    if (!io.obs || !io.rew || !io.done)
+        return fail(h, DR_ERR_INVALID, "dr_rollout: obs/rew/done must be non-null");
+    if (!gen && !io.actions) return fail(h, DR_ERR_INVALID, "dr_rollout: actions is null");
+    if ((((uintptr_t)io.actions) & 15) || (((uintptr_t)io.act_out) & 15))
+        return fail(h, DR_ERR_INVALID, "dr_rollout: actions must be 16-byte aligned");
+    // per-step output offsets t * n are formed in 64 bits, the per-env
+    // offset in 32 (as dr_step); K * n rows must still fit one allocation
+    if ((int64_t)k * h->n > ((int64_t)1 << 31))
+        return fail(h, DR_ERR_INVALID, "dr_rollout: k * num_envs above 2^31");
+    if (h->cfg.variant != DR_VARIANT_VECTORIZED && h->cfg.auto_reset &&
+        h->cfg.rng_mode != DR_RNG_PHILOX)
+        return fail(h, DR_ERR_UNSUPPORTED,
+                    "dr_rollout: host-supplied reset uniforms change per step; use dr_step");
+    if (k == 0) return DR_OK;
+    io.k = k;
+    io.auto_reset = h->cfg.auto_reset;
+    DeviceGuard g(h->cfg.device);
+    return gen ? dispatch_rollout<true>(h, io, as_stream(stream))
+               : dispatch_rollout<false>(h, io, as_stream(stream));
+}
+
+int dr_rollout(dr_handle *h, int32_t k, const float *actions, float *obs_out, float *rew_out,
+               uint8_t *done_out, void *stream) {
+    RolloutIO io{};
+    io.actions = actions;
+    io.obs = obs_out;
+    io.rew = rew_out;
+    io.done = done_out;
+    return rollout_common(h, k, io, false, stream);
+}
+
+int dr_rollout_random(dr_handle *h, int32_t k, uint64_t action_seed, int64_t action_step0,
+                      float lo, float hi, float *actions_out, float *obs_out, float *rew_out,
+                      uint8_t *done_out, void *stream) {
+    RolloutIO io{};
+    io.act_out = actions_out;
+    io.obs = obs_out;
+    io.rew = rew_out;
+    io.done = done_out;
+    io.a_k0 = (uint32_t)action_seed;
+    io.a_k1 = (uint32_t)(action_seed >> 32);
+    io.a_step0 = (uint64_t)action_step0;
+    io.a_lo = lo;
+    io.a_span = hi - lo;
+    return rollout_common(h, k, io, true, stream);
 }
 
 int dr_get_state(dr_handle *h, int field, void *out, void *stream) {

@@ -151,6 +151,42 @@ class DroneBatch:
                                  ptr(self.term_obs), s), self.handle)
         return obs, rew, done
 
+    def rollout(self, k: int, actions: torch.Tensor | None = None, *, seed: int = 0,
+                step0: int = 0, lo: float = 0.0, hi: float = MOTOR_MAX,
+                actions_out: torch.Tensor | None = None,
+                obs_out=None, rew_out=None, done_out=None):
+        """k steps in one launch (dr_rollout): outputs identical to k calls of
+        step().  `actions` (k,N,4) f32 on the device, or None for the
+        in-kernel random policy (step t draws random_actions(N, seed, step0+t,
+        env_id_offset, lo, hi); `actions_out` (k,N,4) receives them if given).
+        Returns (obs (k,N,obs_dim), rew (k,N), done (k,N)); no terminal obs or
+        VecMonitor counters (use step() for those)."""
+        k = int(k)
+        n, od, dev = self.num_envs, self.obs_dim, self.device
+        obs = torch.empty(k, n, od, dtype=torch.float32, device=dev) if obs_out is None else obs_out
+        rew = torch.empty(k, n, dtype=torch.float32, device=dev) if rew_out is None else rew_out
+        done = torch.empty(k, n, dtype=torch.uint8, device=dev) if done_out is None else done_out
+        self._check_out(obs, (k, n, od), torch.float32)
+        self._check_out(rew, (k, n), torch.float32)
+        self._check_out(done, (k, n), torch.uint8)
+        s = _stream(dev)
+        if actions is None:
+            if actions_out is not None:
+                self._check_out(actions_out, (k, n, 4), torch.float32)
+            check(self.L.dr_rollout_random(self.handle, k, seed & (2**64 - 1), step0, lo, hi,
+                                           ptr(actions_out), ptr(obs), ptr(rew), ptr(done), s),
+                  self.handle)
+        else:
+            a = actions
+            if a.dtype != torch.float32 or a.device != dev or not a.is_contiguous() \
+                    or a.data_ptr() % 16:
+                a = a.to(device=dev, dtype=torch.float32).contiguous()
+            if a.shape != (k, n, 4):
+                raise ValueError(f"actions must be ({k}, {n}, 4), got {tuple(a.shape)}")
+            check(self.L.dr_rollout(self.handle, k, ptr(a), ptr(obs), ptr(rew), ptr(done), s),
+                  self.handle)
+        return obs, rew, done
+
     # -- host-buffer I/O (the drop-in surfaces) ------------------------------
     def _host_buffers(self):
         """Pinned host buffers the kernels read / write directly (zero-copy

@@ -39,7 +39,7 @@
 extern "C" {
 #endif
 
-#define DR_ABI_VERSION 10
+#define DR_ABI_VERSION 11
 
 enum dr_status {
     DR_OK = 0,
@@ -189,6 +189,30 @@ int dr_set_seed(dr_handle *h, uint64_t seed);
    reference; it generates the benchmark's action stream. */
 int dr_random_actions(int64_t n, uint64_t seed, int64_t env_id_offset,
                       int64_t step, float lo, float hi, float *out,
+                      void *stream);
+
+/* K successive steps in ONE launch, the state held in registers between
+   steps: outputs identical, bit for bit, to k calls of
+   dr_step(h, actions + t*N*4, obs_out + t*N*obs_dim, rew_out + t*N,
+   done_out + t*N, NULL) for t = 0..k-1 (auto-reset per the handle; no
+   terminal obs, no VecMonitor counters).  The random-policy rollout loop
+   `a = action_space.sample(); env.step(a)` over DroneEnv.step
+   (drone.py:81-159) k times, without the per-step state round trip
+   through HBM or the per-launch gap.
+     actions   (k,N,4) f32, 16-byte aligned
+     obs_out   (k,N,obs_dim) f32; rew_out (k,N) f32; done_out (k,N) u8
+   k * N <= 2^31.  DR_RNG_HOST_UNIFORMS handles with auto-reset are
+   DR_ERR_UNSUPPORTED (their reset draws are supplied per step). */
+int dr_rollout(dr_handle *h, int32_t k, const float *actions, float *obs_out,
+               float *rew_out, uint8_t *done_out, void *stream);
+
+/* dr_rollout on the synthetic random policy drawn in-kernel: step t's
+   actions are exactly dr_random_actions(N, action_seed, env_id_offset of
+   the handle, action_step0 + t, lo, hi).  actions_out nullable: (k,N,4) f32
+   copy of the drawn actions. */
+int dr_rollout_random(dr_handle *h, int32_t k, uint64_t action_seed,
+                      int64_t action_step0, float lo, float hi, float *actions_out,
+                      float *obs_out, float *rew_out, uint8_t *done_out,
                       void *stream);
 
 const char *dr_last_error(const dr_handle *h);

@@ -1,0 +1,30 @@
+#!/bin/bash
+# PMC passes over scripts/micro/rollout_bench.py at 65,536 envs, K = 32
+# (one counter group per run): VALU instruction count and issue occupancy
+# of env_rollout_kernel.
+cd "$(dirname "$0")/../.."
+OUT=$PWD/gpurun_out/pmc_rollout
+mkdir -p "$OUT"
+export TMPDIR=/tmp
+i=0
+for grp in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU GRBM_GUI_ACTIVE GRBM_COUNT" \
+           "SQ_INSTS_SALU SQ_INSTS_VMEM_WR SQ_INSTS_VMEM_RD SQ_INSTS_LDS SQ_INSTS_BRANCH SQ_ACTIVE_INST_SCA FETCH_SIZE"; do
+  i=$((i+1))
+  timeout -s KILL 90 rocprofv3 --pmc $grp --output-format csv -d "$OUT/p$i" -o run \
+      -- python3 "$PWD/scripts/micro/rollout_bench.py" --envs 65536 --ks 32 --reps 5 "$@" > "$OUT/p$i.log" 2>&1
+  rc=$?; echo "pass $i rc=$rc"
+  if [ $rc -ne 0 ]; then tail -5 "$OUT/p$i.log"; exit $rc; fi
+done
+python3 - "$OUT" <<'PY'
+import csv, glob, sys, collections
+out = sys.argv[1]
+for tag in ("64, false>", "64, true>"):   # actions from HBM / in-kernel random policy
+    acc = collections.defaultdict(list)
+    for f in glob.glob(out + "/p*/run_counter_collection.csv"):
+        for r in csv.DictReader(open(f)):
+            if "env_rollout_kernel<double, 0, " + tag in r["Kernel_Name"]:
+                acc[r["Counter_Name"]].append(float(r["Counter_Value"]))
+    print("GEN" if "true" in tag else "READ")
+    for k, v in sorted(acc.items()):
+        print(f"  {k:28s} {sum(v)/len(v):.6g}  (n={len(v)})")
+PY

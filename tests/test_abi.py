@@ -41,7 +41,7 @@ def test_library_exports_every_declared_symbol():
 def test_library_loads_and_validates_without_gpu():
     from drone_rl_amd import _lib
     L = _lib.lib()
-    assert L.dr_abi_version() == _lib.ABI_VERSION == 10
+    assert L.dr_abi_version() == _lib.ABI_VERSION == 11
     # argument validation happens before any HIP call
     cfg = _lib.dr_config(num_envs=0)
     h = ctypes.c_void_p()
@@ -49,6 +49,9 @@ def test_library_loads_and_validates_without_gpu():
     assert rc == _lib.DR_ERR_INVALID
     assert "num_envs" in _lib.last_error()
     assert L.dr_step(None, None, None, None, None, None, None) == _lib.DR_ERR_INVALID
+    assert L.dr_rollout(None, 4, None, None, None, None, None) == _lib.DR_ERR_INVALID
+    assert L.dr_rollout_random(None, 4, 7, 0, 0.0, 1.0, None, None, None, None,
+                               None) == _lib.DR_ERR_INVALID
     assert L.dr_gae(0, 0, None, None, None, None, None, 0.99, 0.95, None, None,
                     None) == _lib.DR_ERR_INVALID
     with pytest.raises(_lib.DroneRLError):
