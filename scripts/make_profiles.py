@@ -6,6 +6,7 @@
   profiles/traffic.json                 HBM bytes per env_step launch, read
                                         by bench.py for roofline.traffic
   profiles/<round>_bench[_extra].json   the bench.py JSON lines of the session
+  profiles/<round>_pmc_rollout.json     the K-step rollout kernel's PMC summary
 Usage: python scripts/make_profiles.py r01
 """
 import json
@@ -46,5 +47,8 @@ for tag, key, n in (("n65536", "f64_65536", 65536), ("n4m", "f64_4194304", 41943
                         "algorithmic_bytes_per_launch": 305 * n,
                         "source": f"profiles/{rnd}_pmc_{tag}.json (FETCH_SIZE x2 gfx950 "
                                   "correction + WRITE_SIZE, KiB -> B)"}
+rs = os.path.join(src, "pmc_rollout", "summary.json")     # scripts/micro/rollout_pmc.sh
+if os.path.exists(rs):
+    shutil.copy(rs, os.path.join(out, f"{rnd}_pmc_rollout.json"))
 json.dump(traffic, open(tpath, "w"), indent=1, sort_keys=True)
 print(json.dumps(traffic, indent=1))

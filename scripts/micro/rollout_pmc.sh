@@ -16,15 +16,29 @@ for grp in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY 
   if [ $rc -ne 0 ]; then tail -5 "$OUT/p$i.log"; exit $rc; fi
 done
 python3 - "$OUT" <<'PY'
-import csv, glob, sys, collections
+import csv, glob, json, sys, collections
 out = sys.argv[1]
+res = {"workload": "scripts/micro/rollout_bench.py --envs 65536 --ks 32 --reps 5 (f64 gym, "
+                   "one action set), rocprofv3 --pmc, two passes (scripts/micro/rollout_pmc.sh)"}
 for tag in ("64, false>", "64, true>"):   # actions from HBM / in-kernel random policy
     acc = collections.defaultdict(list)
     for f in glob.glob(out + "/p*/run_counter_collection.csv"):
         for r in csv.DictReader(open(f)):
             if "env_rollout_kernel<double, 0, " + tag in r["Kernel_Name"]:
                 acc[r["Counter_Name"]].append(float(r["Counter_Value"]))
-    print("GEN" if "true" in tag else "READ")
-    for k, v in sorted(acc.items()):
-        print(f"  {k:28s} {sum(v)/len(v):.6g}  (n={len(v)})")
+    m = {k: sum(v) / len(v) for k, v in acc.items()}
+    w, K = m["SQ_WAVES"], 32
+    res["random_policy_in_kernel" if "true" in tag else "actions_from_hbm"] = {
+        "counters_per_launch": {k: round(v, 1) for k, v in sorted(m.items())},
+        "valu_insts_per_wave_step": round(m["SQ_INSTS_VALU"] / w / K, 1),
+        "salu_insts_per_wave_step": round(m["SQ_INSTS_SALU"] / w / K, 1),
+        "valu_active_frac_of_wave_cycles": round(m["SQ_ACTIVE_INST_VALU"] / m["SQ_WAVE_CYCLES"], 3),
+        "any_active_frac": round(m["SQ_ACTIVE_INST_ANY"] / m["SQ_WAVE_CYCLES"], 3),
+        "wait_any_frac": round(m["SQ_WAIT_ANY"] / m["SQ_WAVE_CYCLES"], 3),
+        "wait_inst_any_frac": round(m["SQ_WAIT_INST_ANY"] / m["SQ_WAVE_CYCLES"], 3),
+        "quad_cycles_per_valu_inst": round(m["SQ_ACTIVE_INST_VALU"] / m["SQ_INSTS_VALU"], 3),
+        "fetch_bytes_x2": round(m["FETCH_SIZE"] * 1024 * 2)}
+json.dump(res, open(out + "/summary.json", "w"), indent=1)
+print(json.dumps({k: {kk: vv for kk, vv in v.items() if kk != "counters_per_launch"}
+                  for k, v in res.items() if k != "workload"}, indent=1))
 PY

@@ -37,5 +37,6 @@ fi
 if [ "$WHAT" = pmc ]; then
   step pmc_n65536 400 bash scripts/pmc.sh n65536 --steps 50 --ppo-updates 0
   step pmc_n4m 400 bash scripts/pmc.sh n4m --envs 4194304 --steps 20 --warmup 5 --ppo-updates 0
+  step pmc_rollout 300 bash scripts/micro/rollout_pmc.sh
 fi
 echo "== done"
