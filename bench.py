@@ -267,12 +267,13 @@ def time_ppo(args, rank, world, device):
                        "optimizer_steps_per_update": cfg.n_epochs * cfg.n_steps *
                        cfg.num_envs // cfg.batch_size,
                        "net_arch": list(cfg.net_arch), "mlp_dtype": "fp32",
-                       "gemm": ((("256x256 layer forward + input gradient: dr_gemm_x6 "
-                                  "(fp32-accurate: exact 3-plane bf16 split, 6 MFMA products, "
-                                  "f32 accumulate); weight gradient: ")
-                                 if x6_weights(tr.policy, cfg.batch_size) is not None else "") +
-                                ("hipBLASLt/rocBLAS, MI355X-tuned solutions (TunableOp lookup)"
-                                 if tr.tuned_gemms else "hipBLASLt heuristic")),
+                       "gemm": (("256x256 layer forward, input gradient and weight gradient: "
+                                 "dr_gemm_x6 / dr_gemm_x6_wgrad (fp32-accurate: exact 3-plane "
+                                 "bf16 split, 6 MFMA products, f32 accumulate)"
+                                 if x6_weights(tr.policy, cfg.batch_size) is not None else
+                                 "256x256 layer: " + ("hipBLASLt/rocBLAS, MI355X-tuned solutions "
+                                                      "(TunableOp lookup)" if tr.tuned_gemms
+                                                      else "hipBLASLt heuristic"))),
                        "grad_allreduce": ({"nccl": "rccl"}.get(dist.get_backend(),
                                                                dist.get_backend())
                                           + (" (2 buckets, the first overlapped with the "
