@@ -56,6 +56,10 @@ def _fields(b):
     ("gym", torch.float64, 1000, 25),
     ("moving", torch.float64, 5003, 30),
     ("vectorized", torch.float64, 777, None),
+    # the large-batch launch forms of the step kernel (32 rows per wave,
+    # nontemporal loads) against the rollout kernel's 64 rows per wave
+    ("gym", torch.float64, 1 << 20, None),
+    ("moving", torch.float64, 1 << 20, None),
 ])
 def test_rollout_is_bitwise_k_steps(variant, dtype, n, max_steps):
     from drone_rl_amd import random_actions
