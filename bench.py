@@ -175,7 +175,7 @@ def time_env(args, dtype_name, n_envs, rank, world, device, steps, warmup, varia
     return elapsed, gpu_ms, ep
 
 
-def time_rollout(args, n_envs, device, k, reps, gen):
+def time_rollout(args, n_envs, device, k, reps, gen, variant="gym"):
     """The K-step rollout kernel (dr_rollout; dr_rollout_random when gen):
     `reps` launches of k steps each over the same 65,536 envs, captured in
     one hipGraph; returns the per-launch GPU time (HIP events on the launch
@@ -185,15 +185,17 @@ def time_rollout(args, n_envs, device, k, reps, gen):
 
     from drone_rl_amd import DroneBatch, random_actions
     dtype = torch.float64 if args.state_dtype == "f64" else torch.float32
-    b = DroneBatch(n_envs, "gym", dtype=dtype, device=device, seed=2025, auto_reset=True)
+    b = DroneBatch(n_envs, variant, dtype=dtype, device=device, seed=2025, auto_reset=True)
     b.reset()
     obs = torch.empty(k, n_envs, b.obs_dim, device=device)
     rew = torch.empty(k, n_envs, device=device)
     done = torch.empty(k, n_envs, dtype=torch.uint8, device=device)
-    acts = torch.empty(reps, k, n_envs, 4, device=device)
-    for r in range(reps):
-        for t in range(k):
-            random_actions(n_envs, seed=7, step=r * k + t, out=acts[r, t])
+    acts = None
+    if not gen:
+        acts = torch.empty(reps, k, n_envs, 4, device=device)
+        for r in range(reps):
+            for t in range(k):
+                random_actions(n_envs, seed=7, step=r * k + t, out=acts[r, t])
 
     def launch(r):
         if gen:
@@ -419,6 +421,13 @@ def main():
                 "env_steps_per_s": round(n * k / el, 1),
                 "avg_launch_us": round(pl * 1e6, 3),
                 "achieved_GBs": round(n * BYTES_PER_ENV_STEP_MOVING[dn] / pl / 1e9, 1)}
+        # the K-step rollout kernel (in-kernel random policy, K = 32) at the
+        # configs[4] sizes: per-GPU slice and whole 1M
+        for n in (1 << 17, 1 << 20):
+            pl = time_rollout(args, n, device, 32, 4, True, variant="moving")
+            ex[f"rollout_moving_f64_{n}"] = {"env_steps_per_s": round(n * 32 / pl, 1),
+                                             "avg_launch_us": round(pl * 1e6, 3),
+                                             "us_per_step": round(pl * 1e6 / 32, 3)}
         if saved is None:
             os.environ.pop("DRONERL_STEP_KERNEL", None)
         else:
