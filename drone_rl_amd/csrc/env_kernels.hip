@@ -886,8 +886,27 @@ __global__ __launch_bounds__(kEnvBlock) void env_rollout_kernel(EnvView<S> v, Ro
     // schedules out of the loop: hoisted, their 40 words spilled to VGPR
     // lanes, and every round paid a v_readlane plus a hazard s_nop.
     EnvView<S> vk = v;
+    // Gym variant: the Philox block of a lane's NEXT reset (episode
+    // ep_num + 1: pos x, y and target x, y) is drawn ahead, for every lane
+    // whose draw is used up, at the first step of each group of
+    // kResetAhead steps -- a wave-wide pass once per group instead of the
+    // reset branch's Philox, which a wave runs at almost every step (≈86 % of
+    // waves hold a resetting env at each step under the random policy).  A
+    // lane resetting twice within one group draws in the branch as before;
+    // the draws are the same Philox words either way.
+    constexpr int kResetAhead = 8;
+    u32x4 nd{};
+    bool nd_ok = false;
     auto step_one = [&](const MotorMix mx, const int t) {
         asm volatile("" : "+s"(vk.seed_lo), "+s"(vk.seed_hi));
+        if constexpr (VAR == DR_VARIANT_GYM) {
+            if (t % kResetAhead == 0 && !nd_ok) {
+                nd = philox4x32_10(u32x4{(uint32_t)(ep_num + 1), (uint32_t)gid,
+                                         (uint32_t)(gid >> 32), TAG_RESET},
+                                   vk.seed_lo, vk.seed_hi);
+                nd_ok = true;
+            }
+        }
         if constexpr (VAR == DR_VARIANT_MOVING)
             moving_target(cen, mp, step + 1, (float)v.dt, &st[F_TGT], tvel);
         bool crash;
@@ -904,7 +923,8 @@ __global__ __launch_bounds__(kEnvBlock) void env_rollout_kernel(EnvView<S> v, Ro
                 step = 0;
                 reset_any = true;
                 if constexpr (VAR == DR_VARIANT_GYM) {
-                    gym_reset_regs(vk, i, 0, st, ep_num, eps);
+                    gym_reset_regs(vk, i, 0, st, ep_num, eps, nd_ok ? &nd : nullptr);
+                    nd_ok = false;
                 } else {
                     moving_reset_regs(vk, i, 0, st, cen, mp, ep_num, eps);
                     moving_target(cen, mp, 0, (float)v.dt, &st[F_TGT], tvel);
