@@ -65,7 +65,38 @@ int main(void) {
     if (episodes < n) return 9;     /* random policy: ~3 episodes / 100 steps */
     /* error path: a misaligned action pointer is rejected, not dereferenced */
     if (dr_step(h, act + 1, obs, rew, done, NULL, s) != DR_ERR_INVALID) return 10;
+    /* the same 100 steps as 4 launches of the K-step rollout (random policy
+       drawn in the kernel): the last step's obs and every ep_num bitwise */
+    dr_handle *h2 = NULL;
+    {
+        dr_handle *hsave = h;
+        h = NULL;
+        CK(dr_create(&cfg, &h2));
+        h = hsave;
+    }
+    const int K = 25;
+    float *obs_k, *rew_k;
+    uint8_t *done_k;
+    if (hipMalloc((void **)&obs_k, (size_t)K * n * 60) ||
+        hipMalloc((void **)&rew_k, (size_t)K * n * 4) || hipMalloc((void **)&done_k, (size_t)K * n))
+        return 11;
+    CK(dr_reset(h2, obs, s));
+    for (int c = 0; c < 100 / K; ++c)
+        CK(dr_rollout_random(h2, K, 7, (int64_t)c * K, 0.0f, 7.3575f, NULL, obs_k, rew_k,
+                             done_k, s));
+    CK(dr_get_state(h2, DR_FIELD_EP_NUM, ep, s));
+    if (hipStreamSynchronize(s)) return 12;
+    float *ho2 = malloc(n * 60);
+    int32_t *he2 = malloc(n * 4);
+    if (hipMemcpy(ho2, obs_k + (size_t)(K - 1) * n * 15, n * 60, hipMemcpyDeviceToHost) ||
+        hipMemcpy(he2, ep, n * 4, hipMemcpyDeviceToHost))
+        return 13;
+    for (int64_t i = 0; i < n * 15; ++i)
+        if (ho2[i] != ho[i] && !(isnan(ho2[i]) && isnan(ho[i]))) return 14;
+    for (int64_t i = 0; i < n; ++i)
+        if (he2[i] != he[i]) return 15;
+    CK(dr_destroy(h2));
     CK(dr_destroy(h));
-    printf("c abi ok: %ld episodes finished\n", episodes);
+    printf("c abi ok: %ld episodes finished; dr_rollout_random == dr_step\n", episodes);
     return 0;
 }
