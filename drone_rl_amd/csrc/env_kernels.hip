@@ -106,6 +106,11 @@ constexpr int kEnvBlock = 64 * DR_ENV_WPB;
 // 1: per-step outputs and state are written with nontemporal stores.  They
 // stream to HBM while the kernel runs instead of sitting dirty in L2 until
 // the end-of-kernel writeback (4-9 % faster from 65,536 to 4M envs).
+// 1: the step kernel's loads are all waited for before its first store
+// (see env_step_kernel); 0 (A/B only): the compiler's own wait placement
+#ifndef DR_LOADS_LANDED
+#define DR_LOADS_LANDED 1
+#endif
 #ifndef DR_NT_STORES
 #define DR_NT_STORES 1
 #endif
@@ -718,6 +723,19 @@ __global__ __launch_bounds__(kEnvBlock) void env_step_kernel(EnvView<S> v,
     step += 1;                                             // (155)
     const bool done = live && (crash || (step >= v.max_steps));   // (156-157)
     const float rf = (float)r;                             // SB3 f32 buffer
+#if DR_LOADS_LANDED
+    // Every value loaded up front has landed before the first store is
+    // issued (they were issued first and the physics took longer than
+    // their latency, so this waits for nothing).  Without it the compiler
+    // places the waits for the late-used ones (ep_num / eps in the reset
+    // branch, the VecMonitor counters, the step counter) at their uses,
+    // after the rew / done (and terminal obs) stores: vmcnt(0) there drains
+    // those stores as well -- vmcnt counts both, in issue order -- once
+    // in the reset branch and again where it rejoins, for every wave.
+    asm volatile("" ::"v"(step), "v"(ep_old), "v"(eps_old), "v"(ret0), "v"(len0));
+#pragma unroll
+    for (int k = 0; k < F_N; ++k) asm volatile("" ::"v"(st[k]));
+#endif
     if (live) {
         st_out(at(io.rew, i), rf);
         st_out(at(io.done, i), (uint8_t)done);
