@@ -915,6 +915,11 @@ __global__ __launch_bounds__(kEnvBlock) void env_rollout_kernel(EnvView<S> v, Ro
     constexpr int kResetAhead = 8;
     u32x4 nd{};
     bool nd_ok = false;
+    // the step limit in a VGPR: under the kernel's SGPR pressure the
+    // compiler otherwise re-reads it from the kernel arguments at every
+    // step (a scalar load and its wait on the critical path)
+    int32_t max_steps;
+    asm volatile("v_mov_b32 %0, %1" : "=v"(max_steps) : "s"(v.max_steps));
     auto step_one = [&](const MotorMix mx, const int t) {
         asm volatile("" : "+s"(vk.seed_lo), "+s"(vk.seed_hi));
         if constexpr (VAR == DR_VARIANT_GYM) {
@@ -930,7 +935,7 @@ __global__ __launch_bounds__(kEnvBlock) void env_rollout_kernel(EnvView<S> v, Ro
         bool crash;
         const S r = physics_step_mixed<S, VAR>(st, mx, v.dt, crash);
         step += 1;
-        const bool done = live && (crash || (step >= v.max_steps));
+        const bool done = live && (crash || (step >= max_steps));
         const int64_t row = (int64_t)t * n_;
         if (live) {
             st_out(at(io.rew + row, i), (float)r);
