@@ -836,8 +836,8 @@ __global__ __launch_bounds__(kEnvBlock) void env_step_kernel(EnvView<S> v,
 //
 // Every step's outputs are stored as they are formed (rew / done per lane,
 // obs through the per-wave LDS staging), so the stores of step t drain
-// while step t+1 computes; the next step's action load is issued one step
-// ahead.  The fields a reset changes outside the 12 dynamic ones (target,
+// while step t+1 computes; actions are loaded two steps ahead.  The fields
+// a reset changes outside the 12 dynamic ones (target,
 // motion; ep_num / eps are written by the reset itself) are written back
 // at the end only for lanes that reset during the launch.
 // ----------------------------------------------------------------------------
@@ -898,7 +898,6 @@ __global__ __launch_bounds__(kEnvBlock) void env_rollout_kernel(EnvView<S> v, Ro
     bool reset_any = false;
     float ob[OD];
 
-    // one step on action `act`: the body of env_step_kernel on registers
     // The Philox keys (reset draws; GEN: actions) are re-declared opaque
     // once per step, so the compiler cannot hoist the 10-round key
     // schedules out of the loop: hoisted, their 40 words spilled to VGPR
@@ -920,6 +919,8 @@ __global__ __launch_bounds__(kEnvBlock) void env_rollout_kernel(EnvView<S> v, Ro
     // step (a scalar load and its wait on the critical path)
     int32_t max_steps;
     asm volatile("v_mov_b32 %0, %1" : "=v"(max_steps) : "s"(v.max_steps));
+    // one step from the action's motor mixes: the body of env_step_kernel
+    // on registers
     auto step_one = [&](const MotorMix mx, const int t) {
         asm volatile("" : "+s"(vk.seed_lo), "+s"(vk.seed_hi));
         if constexpr (VAR == DR_VARIANT_GYM) {
