@@ -202,14 +202,14 @@ int dr_random_actions(int64_t n, uint64_t seed, int64_t env_id_offset,
      actions   (k,N,4) f32, 16-byte aligned
      obs_out   (k,N,obs_dim) f32; rew_out (k,N) f32; done_out (k,N) u8
    k * N <= 2^31.  DR_RNG_HOST_UNIFORMS handles with auto-reset are
-   DR_ERR_UNSUPPORTED (their reset draws are supplied per step). */
+   DR_ERR_UNSUPPORTED (their reset draws are supplied per step).  (ABI v11.) */
 int dr_rollout(dr_handle *h, int32_t k, const float *actions, float *obs_out,
                float *rew_out, uint8_t *done_out, void *stream);
 
 /* dr_rollout on the synthetic random policy drawn in-kernel: step t's
    actions are exactly dr_random_actions(N, action_seed, env_id_offset of
    the handle, action_step0 + t, lo, hi).  actions_out nullable: (k,N,4) f32
-   copy of the drawn actions. */
+   copy of the drawn actions.  (ABI v11.) */
 int dr_rollout_random(dr_handle *h, int32_t k, uint64_t action_seed,
                       int64_t action_step0, float lo, float hi, float *actions_out,
                       float *obs_out, float *rew_out, uint8_t *done_out,
