@@ -175,7 +175,7 @@ def time_env(args, dtype_name, n_envs, rank, world, device, steps, warmup, varia
     return elapsed, gpu_ms, ep
 
 
-def time_rollout(args, n_envs, device, k, reps, gen, variant="gym"):
+def time_rollout(args, n_envs, device, k, reps, gen, variant="gym", state_dtype=None):
     """The K-step rollout kernel (dr_rollout; dr_rollout_random when gen):
     `reps` launches of k steps each over the same 65,536 envs, captured in
     one hipGraph; returns the per-launch GPU time (HIP events on the launch
@@ -184,7 +184,7 @@ def time_rollout(args, n_envs, device, k, reps, gen, variant="gym"):
     import torch
 
     from drone_rl_amd import DroneBatch, random_actions
-    dtype = torch.float64 if args.state_dtype == "f64" else torch.float32
+    dtype = torch.float64 if (state_dtype or args.state_dtype) == "f64" else torch.float32
     b = DroneBatch(n_envs, variant, dtype=dtype, device=device, seed=2025, auto_reset=True)
     b.reset()
     obs = torch.empty(k, n_envs, b.obs_dim, device=device)
@@ -423,6 +423,11 @@ def main():
                 "achieved_GBs": round(n * BYTES_PER_ENV_STEP_MOVING[dn] / pl / 1e9, 1)}
         # the K-step rollout kernel (in-kernel random policy, K = 32) at the
         # configs[4] sizes: per-GPU slice and whole 1M
+        for gen in (False, True):         # f32 state through the rollout kernel
+            pl = time_rollout(args, N, device, 32, 10, gen, state_dtype="f32")
+            ex["rollout_f32_%d_%s" % (N, "random_policy_in_kernel" if gen else "actions_from_hbm")] = {
+                "env_steps_per_s": round(N * 32 / pl, 1), "avg_launch_us": round(pl * 1e6, 3),
+                "us_per_step": round(pl * 1e6 / 32, 3)}
         for n in (1 << 17, 1 << 20):
             pl = time_rollout(args, n, device, 32, 4, True, variant="moving")
             ex[f"rollout_moving_f64_{n}"] = {"env_steps_per_s": round(n * 32 / pl, 1),
