@@ -283,7 +283,8 @@ struct StepIO {
 // first 5 are the gym variant's, so eps = 0 reproduces it exactly).
 template <int NU, typename S>
 __device__ inline void reset_uniforms(const EnvView<S> &v, int64_t i,
-                                      int32_t ep_new, int mode, double u[NU]) {
+                                      int32_t ep_new, int mode, double u[NU],
+                                      const u32x4 *pre = nullptr) {
     if (mode == 1) {
 #pragma unroll
         for (int k = 0; k < NU; ++k) u[k] = v.host_u[i * NU + k];
@@ -297,10 +298,11 @@ __device__ inline void reset_uniforms(const EnvView<S> &v, int64_t i,
     const uint64_t gid = (uint64_t)(v.env_id_offset + i);
 #pragma unroll
     for (int b = 0; b < (NU + 3) / 4; ++b) {
-        const u32x4 r = philox4x32_10(
-            u32x4{(uint32_t)ep_new, (uint32_t)gid, (uint32_t)(gid >> 32),
-                  TAG_RESET | (uint32_t)b},
-            v.seed_lo, v.seed_hi);
+        // pre: the blocks already drawn for this (episode, env)
+        const u32x4 r = pre ? pre[b]
+                            : philox4x32_10(u32x4{(uint32_t)ep_new, (uint32_t)gid,
+                                                  (uint32_t)(gid >> 32), TAG_RESET | (uint32_t)b},
+                                            v.seed_lo, v.seed_hi);
         const uint32_t w[4] = {r.x, r.y, r.z, r.w};
 #pragma unroll
         for (int k = 0; k < 4; ++k)
@@ -394,10 +396,11 @@ __device__ inline void moving_target(const S c[3], const float mp[9], int32_t s,
 template <typename S>
 __device__ inline void moving_reset_regs(const EnvView<S> &v, int64_t i, int mode,
                                          S st[F_N], S c[3], float mp[9],
-                                         int32_t ep_old, double eps) {
+                                         int32_t ep_old, double eps,
+                                         const u32x4 *pre4 = nullptr) {
     const int32_t ep_new = ep_old + 1;
     double u[14];
-    reset_uniforms<14>(v, i, ep_new, mode, u);
+    reset_uniforms<14>(v, i, ep_new, mode, u, pre4);
     if (!DR_PREFETCH_EPS) eps = v.eps[i];
     if (ep_new % 2000 == 0) {
         eps += 0.1;
@@ -903,8 +906,8 @@ __global__ __launch_bounds__(kEnvBlock) void env_rollout_kernel(EnvView<S> v, Ro
     // schedules out of the loop: hoisted, their 40 words spilled to VGPR
     // lanes, and every round paid a v_readlane plus a hazard s_nop.
     EnvView<S> vk = v;
-    // Gym variant: the Philox block of a lane's NEXT reset (episode
-    // ep_num + 1: pos x, y and target x, y) is drawn ahead, for every lane
+    // The Philox blocks of a lane's NEXT reset (episode ep_num + 1; gym:
+    // block 0 = pos x, y and target x, y; moving: all four) are drawn ahead, for every lane
     // whose draw is used up, at the first step of each group of
     // kResetAhead steps -- a wave-wide pass once per group instead of the
     // reset branch's Philox, which a wave runs at almost every step (≈86 % of
@@ -912,7 +915,8 @@ __global__ __launch_bounds__(kEnvBlock) void env_rollout_kernel(EnvView<S> v, Ro
     // lane resetting twice within one group draws in the branch as before;
     // the draws are the same Philox words either way.
     constexpr int kResetAhead = 8;
-    u32x4 nd{};
+    constexpr int NB = VAR == DR_VARIANT_MOVING ? 4 : 1;   // Philox blocks per reset
+    u32x4 nd[NB] = {};
     bool nd_ok = false;
     // the step limit in a VGPR: under the kernel's SGPR pressure the
     // compiler otherwise re-reads it from the kernel arguments at every
@@ -923,11 +927,13 @@ __global__ __launch_bounds__(kEnvBlock) void env_rollout_kernel(EnvView<S> v, Ro
     // on registers
     auto step_one = [&](const MotorMix mx, const int t) {
         asm volatile("" : "+s"(vk.seed_lo), "+s"(vk.seed_hi));
-        if constexpr (VAR == DR_VARIANT_GYM) {
+        if constexpr (GYMLIKE) {
             if (t % kResetAhead == 0 && !nd_ok) {
-                nd = philox4x32_10(u32x4{(uint32_t)(ep_num + 1), (uint32_t)gid,
-                                         (uint32_t)(gid >> 32), TAG_RESET},
-                                   vk.seed_lo, vk.seed_hi);
+#pragma unroll
+                for (int b = 0; b < NB; ++b)
+                    nd[b] = philox4x32_10(u32x4{(uint32_t)(ep_num + 1), (uint32_t)gid,
+                                                (uint32_t)(gid >> 32), TAG_RESET | (uint32_t)b},
+                                          vk.seed_lo, vk.seed_hi);
                 nd_ok = true;
             }
         }
@@ -947,10 +953,11 @@ __global__ __launch_bounds__(kEnvBlock) void env_rollout_kernel(EnvView<S> v, Ro
                 step = 0;
                 reset_any = true;
                 if constexpr (VAR == DR_VARIANT_GYM) {
-                    gym_reset_regs(vk, i, 0, st, ep_num, eps, nd_ok ? &nd : nullptr);
+                    gym_reset_regs(vk, i, 0, st, ep_num, eps, nd_ok ? &nd[0] : nullptr);
                     nd_ok = false;
                 } else {
-                    moving_reset_regs(vk, i, 0, st, cen, mp, ep_num, eps);
+                    moving_reset_regs(vk, i, 0, st, cen, mp, ep_num, eps, nd_ok ? nd : nullptr);
+                    nd_ok = false;
                     moving_target(cen, mp, 0, (float)v.dt, &st[F_TGT], tvel);
                 }
                 // the curriculum counters gym/moving_reset_regs just wrote
