@@ -41,9 +41,12 @@ def _anchor_at(a, eps):
 # the per-env 2000-episode bump never fires in these runs), scripts/c3_matched.sh
 C3_AT_EPS = {0.0: ["r01_ppo_c3_converge.jsonl", "r02_ppo_c3_eps0_x6_s0.jsonl",
                    "r02_ppo_c3_eps0_x6_s1.jsonl", "r02_ppo_c3_eps0_x6_s2.jsonl"],
-             0.5: ["r02_ppo_c3_eps0.5_s0.jsonl"],
-             1.0: ["r02_ppo_c3_eps1.0_s0.jsonl"],
-             2.0: ["r02_ppo_c3_eps2.0_s0.jsonl"],
+             0.5: ["r02_ppo_c3_eps0.5_s0.jsonl", "r02_ppo_c3_eps0.5_s1.jsonl",
+                   "r02_ppo_c3_eps0.5_s2.jsonl"],
+             1.0: ["r02_ppo_c3_eps1.0_s0.jsonl", "r02_ppo_c3_eps1.0_s1.jsonl",
+                   "r02_ppo_c3_eps1.0_s2.jsonl"],
+             2.0: ["r02_ppo_c3_eps2.0_s0.jsonl", "r02_ppo_c3_eps2.0_s1.jsonl",
+                   "r02_ppo_c3_eps2.0_s2.jsonl"],
              4.8: ["r02_ppo_c3_eps4.8_s0.jsonl", "r02_ppo_c3_eps4.8_s1.jsonl"]}
 
 
