@@ -47,7 +47,8 @@ C3_AT_EPS = {0.0: ["r01_ppo_c3_converge.jsonl", "r02_ppo_c3_eps0_x6_s0.jsonl",
                    "r02_ppo_c3_eps1.0_s2.jsonl"],
              2.0: ["r02_ppo_c3_eps2.0_s0.jsonl", "r02_ppo_c3_eps2.0_s1.jsonl",
                    "r02_ppo_c3_eps2.0_s2.jsonl"],
-             4.8: ["r02_ppo_c3_eps4.8_s0.jsonl", "r02_ppo_c3_eps4.8_s1.jsonl"]}
+             4.8: ["r02_ppo_c3_eps4.8_s0.jsonl", "r02_ppo_c3_eps4.8_s1.jsonl",
+                   "r02_ppo_c3_eps4.8_s2.jsonl"]}
 
 
 def test_c3_at_matched_curriculum_level_beats_the_c1_anchor():
