@@ -90,3 +90,17 @@ def test_c1_on_gpu_tracks_the_cpu_restatement():
         cpu = [min(s["history"], key=lambda h: abs(h["timesteps"] - ts))["ep_rew_mean"]
                for s in a["seeds"]]
         assert min(cpu) - 0.15 <= gpu[g] <= max(cpu) + 0.15, (ts, gpu[g], cpu)
+
+
+def test_moving_curriculum_at_configs4_per_gpu_size():
+    """configs[4]'s per-GPU slice (131,072 moving-target envs, 2x256, the
+    staged schedule 350:0.05 ... 750:0.4; profiles/r02_ppo_moving_131072.jsonl):
+    at eps 0 the trainer learns to hover (the variant is the gym env there),
+    and once the target moves the episodes stay long (the drone keeps flying
+    and following) while the 5 cm bonus gets rarer."""
+    rows = [r for r in _jsonl("r02_ppo_moving_131072.jsonl") if "update" in r]
+    at = {r["update"]: r for r in rows}
+    assert at[330]["ep_rew_mean"] > 100 and at[330]["ep_len_mean"] > 150
+    moving = [r for r in rows if r["update"] >= 450]
+    assert len(moving) >= 30
+    assert min(r["ep_len_mean"] for r in moving) > 150
