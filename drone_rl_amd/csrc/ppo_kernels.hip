@@ -1113,6 +1113,11 @@ constexpr int kHeadTile = DR_HEAD_TILE;
 #ifndef DR_HEAD_DIAG
 #define DR_HEAD_DIAG 0
 #endif
+// A/B knob: 1 = the next tile's activation rows are loaded while this
+// tile computes (software pipelining, +16 VGPRs per wave)
+#ifndef DR_HEAD_PF
+#define DR_HEAD_PF 0
+#endif
 
 // policy waves: accumulate u[0], u[2..7] (loss terms), u[9..12] (d b_act),
 // and per lane d b_pi (4 columns) and d W_act (4 x 4)
@@ -1127,13 +1132,30 @@ __device__ inline void head_policy_wave(const HeadArgs &a, const RowLossConst &c
     for (int j = 0; j < 4; ++j) wa[j] = act ? ld4(a.w_act + j * hd + c0) : z4;
     const float4 zb = (act && a.zb_pi) ? ld4(a.zb_pi + c0) : z4;
     const float ba[4] = {a.b_act[0], a.b_act[1], a.b_act[2], a.b_act[3]};
+#if DR_HEAD_PF
+    float4 hn[kHeadTile];
+    auto load_h = [&](int64_t tile, float4 *dst) {
+        const int64_t r0 = tile * kHeadTile;
+        const int nr = (int)min((int64_t)kHeadTile, a.m - r0);
+#pragma unroll
+        for (int i = 0; i < kHeadTile; ++i)
+            dst[i] = (act && i < nr) ? ld4(a.h_pi + (r0 + i) * hd + c0) : z4;
+    };
+    if (tile0 * kHeadTile < a.m) load_h(tile0, hn);
+#endif
     for (int64_t tile = tile0; tile * kHeadTile < a.m; tile += tstride) {
         const int64_t r0 = tile * kHeadTile;
         const int nr = (int)min((int64_t)kHeadTile, a.m - r0);
         float4 h[kHeadTile];
+#if DR_HEAD_PF
+#pragma unroll
+        for (int i = 0; i < kHeadTile; ++i) h[i] = hn[i];
+        if ((tile + tstride) * kHeadTile < a.m) load_h(tile + tstride, hn);
+#else
 #pragma unroll
         for (int i = 0; i < kHeadTile; ++i)
             h[i] = (act && i < nr) ? ld4(a.h_pi + (r0 + i) * hd + c0) : z4;
+#endif
         // this lane's row (lane < nr): its loss inputs, loaded while the dots run
         const bool own = lane < nr;
         const int64_t rr = r0 + (own ? lane : 0);
@@ -1207,13 +1229,30 @@ __device__ inline void head_value_wave(const HeadArgs &a, const RowLossConst &c,
     const float4 zb = (act && a.zb_vf) ? ld4(a.zb_vf + c0) : z4;
     const float bv = a.b_val[0];
     const float wvq[4] = {wv.x, wv.y, wv.z, wv.w};
+#if DR_HEAD_PF
+    float4 hn[kHeadTile];
+    auto load_h = [&](int64_t tile, float4 *dst) {
+        const int64_t r0 = tile * kHeadTile;
+        const int nr = (int)min((int64_t)kHeadTile, a.m - r0);
+#pragma unroll
+        for (int i = 0; i < kHeadTile; ++i)
+            dst[i] = (act && i < nr) ? ld4(a.h_vf + (r0 + i) * hd + c0) : z4;
+    };
+    if (tile0 * kHeadTile < a.m) load_h(tile0, hn);
+#endif
     for (int64_t tile = tile0; tile * kHeadTile < a.m; tile += tstride) {
         const int64_t r0 = tile * kHeadTile;
         const int nr = (int)min((int64_t)kHeadTile, a.m - r0);
         float4 h[kHeadTile];
+#if DR_HEAD_PF
+#pragma unroll
+        for (int i = 0; i < kHeadTile; ++i) h[i] = hn[i];
+        if ((tile + tstride) * kHeadTile < a.m) load_h(tile + tstride, hn);
+#else
 #pragma unroll
         for (int i = 0; i < kHeadTile; ++i)
             h[i] = (act && i < nr) ? ld4(a.h_vf + (r0 + i) * hd + c0) : z4;
+#endif
         const bool own = lane < nr;
         const int64_t rr = r0 + (own ? lane : 0);
         const int64_t ro = a.rows ? (int64_t)a.rows[rr] : rr;

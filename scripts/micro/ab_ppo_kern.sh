@@ -12,7 +12,7 @@ if [ "$1" = build ]; then
     /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -ffp-contract=off \
       -fno-fast-math -Iinclude $flags -c $C/ppo_kernels.hip -o $B/ppo_$name.o &&
     /opt/rocm/bin/hipcc -shared -fPIC --offload-arch=gfx950 -o $B/lib_$name.so \
-      $C/build/env_kernels.o $B/ppo_$name.o || exit 1
+      $C/build/env_kernels.o $C/build/gemm_x6.o $B/ppo_$name.o || exit 1
     rm -f $B/ppo_$name.o
   done
   exit 0
