@@ -3,28 +3,38 @@
 Workload (N=1 GPU): 65,536 DroneGymEnv-equivalent envs per GPU, synthetic
 random policy (actions i.i.d. U[0, 7.3575)^4 f32 from Philox, pre-generated
 and resident in HBM before the timed region), DummyVecEnv auto-reset inside
-the step, f64 state (the reference's precision).  One "step" = one
-dr_step over the whole batch.  The K timed steps are captured in one
-hipGraph and replayed (launch-bound loop), bracketed by barrier +
-synchronize on both sides; the max over ranks is taken.
+the step, f64 state (the reference's precision), every step's obs / reward /
+done written to HBM.  One "step" = one env step of the whole batch.  The
+headline runs the steps through the K-step rollout kernel (dr_rollout: up to
+32 steps per launch, the state in registers between steps; its outputs are
+bitwise those of K single dr_step launches, tests/test_rollout_gpu.py); the
+launches are captured in one hipGraph and replayed, bracketed by barrier +
+synchronize on both sides; the max over ranks is taken.  `--headline step`
+times one dr_step launch per step instead (the kernel PPO's rollout uses;
+always reported as `single_step`).
 
 Multi-GPU: one process per GPU (torchrun), independent env shards (global
 env ids rank*N+i), no data-path collective -> "scaling": "weak".
 
 The JSON line also carries
-  roofline      dominant kernel (env_step_kernel): algorithmic bytes per
-                launch (N x 305 B in f64 mode, 197 B in f32) over
-                its average per-launch GPU time from HIP events on the
+  roofline      the headline kernel: algorithmic bytes per launch (per env-
+                step 81 B of actions / obs / reward / done, plus the f64 state
+                read and written once per launch: 224 B / K)
+                over its average per-launch GPU time from HIP events on the
                 launch stream across the timed region;
+  single_step   the same envs through one dr_step launch per step (305 B per
+                env-step in f64), with its own roofline block;
   cpu_baseline  rank 0, N=1: the SubprocVecEnv-equivalent process pool over
                 the fixture-pinned numpy port (oracle/cpu_baseline.py),
                 run BEFORE the GPU is touched;
   ppo           PPO updates/s for configs[2] (65,536 envs, 2x256 tanh MLP,
-                GAE lambda 0.95), when --ppo-updates > 0;
-  rollout_kernel  the same envs and action stream through the K-step
-                rollout kernel (dr_rollout: K steps per launch, state in
-                registers, every step's outputs written), separately
-                reported; `value` stays on the single-step kernel.
+                GAE lambda 0.95), when --ppo-updates > 0, with a roofline
+                block: FLOP per update over the update time
+                against the f32 matrix peak, and every kernel of one
+                optimizer step timed by HIP events (MFMA fraction of the
+                256x256 GEMMs, HBM fraction of the memory-bound kernels);
+  rollout_kernel  K = 32 rollout-kernel launches with actions from HBM and
+                with the random policy drawn in the kernel.
 """
 import argparse
 import json
@@ -39,6 +49,9 @@ BYTES_PER_ENV_STEP = {"f64": 305, "f32": 197}
 # moving-target variant: + 9 f32 motion params read, + 3 f32 obs written
 BYTES_PER_ENV_STEP_MOVING = {"f64": 353, "f32": 245}
 HBM_PEAK_GBS = 8000.0      # MI355X HBM3E spec (MI355X_MICROARCH.md)
+# SQ_ACTIVE_INST_VALU / SQ_WAVE_CYCLES of the K = 32 rollout kernel at 65,536
+# envs (profiles/r02_pmc_rollout.json): one wave per SIMD, latency-bound
+PMC_ROLLOUT_VALU_ACTIVE = {"actions_from_hbm": 0.481, "random_policy_in_kernel": 0.502}
 
 
 def parse():
@@ -66,6 +79,11 @@ def parse():
     ap.add_argument("--rollout-k", type=int, default=32,
                     help="steps per launch of the K-step rollout kernel line (0 = skip)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"))
+    ap.add_argument("--headline", choices=["rollout", "step"], default="rollout",
+                    help="kernel of the headline value: the K-step rollout kernel or one "
+                         "dr_step launch per step")
+    ap.add_argument("--headline-k", type=int, default=32,
+                    help="max steps per rollout-kernel launch in the headline")
     return ap.parse_args()
 
 
@@ -175,6 +193,73 @@ def time_env(args, dtype_name, n_envs, rank, world, device, steps, warmup, varia
     return elapsed, gpu_ms, ep
 
 
+def time_headline(args, n_envs, rank, world, device, steps, warmup, kmax):
+    """The headline: `warmup` untimed then `steps` timed env steps of the
+    batch through dr_rollout, in launches of at most kmax steps (actions
+    pre-generated in HBM, outputs of every step written).  The timed launches
+    are one captured hipGraph (replayed once untimed first: its first launch
+    uploads it; the env simply runs those steps again on the same actions).
+    Returns (wall seconds, GPU ms over the timed launches, launches, mean ep_num)."""
+    import torch
+    import torch.distributed as dist
+
+    from drone_rl_amd import DroneBatch, random_actions
+    dtype = torch.float64 if args.state_dtype == "f64" else torch.float32
+    b = DroneBatch(n_envs, "gym", dtype=dtype, device=device, seed=2025,
+                   env_id_offset=rank * n_envs, auto_reset=True)
+    b.reset()
+    total = warmup + steps
+    acts = torch.empty(total, n_envs, 4, dtype=torch.float32, device=device)
+    for t in range(total):
+        random_actions(n_envs, seed=7, step=t, env_id_offset=rank * n_envs, out=acts[t])
+    k0 = min(kmax, max(steps, warmup, 1))
+    obs = torch.empty(k0, n_envs, b.obs_dim, device=device)
+    rew = torch.empty(k0, n_envs, device=device)
+    done = torch.empty(k0, n_envs, dtype=torch.uint8, device=device)
+
+    def run(t0, t1):
+        n = 0
+        while t0 < t1:
+            k = min(k0, t1 - t0)
+            b.rollout(k, acts[t0:t0 + k], obs_out=obs[:k], rew_out=rew[:k], done_out=done[:k])
+            t0 += k
+            n += 1
+        return n
+    run(0, warmup)
+    stream = torch.cuda.current_stream(device)
+    cs = torch.cuda.Stream(device)
+    cs.wait_stream(stream)
+    with torch.cuda.stream(cs):
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=cs):
+            launches = run(warmup, total)
+    stream.wait_stream(cs)
+    g.replay()
+    torch.cuda.synchronize(device)
+    ev0 = torch.cuda.Event(enable_timing=True)
+    ev1 = torch.cuda.Event(enable_timing=True)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(device)
+    t0 = time.perf_counter()
+    ev0.record(stream)
+    g.replay()
+    ev1.record(stream)
+    torch.cuda.synchronize(device)
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    gpu_ms = ev0.elapsed_time(ev1)
+    if world > 1:
+        t = torch.tensor([elapsed, gpu_ms], dtype=torch.float64, device=device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed, gpu_ms = float(t[0]), float(t[1])
+    ep = b.get("ep_num").float().mean().item()
+    b.close()
+    del g
+    return elapsed, gpu_ms, launches, ep
+
+
 def time_rollout(args, n_envs, device, k, reps, gen, variant="gym", state_dtype=None):
     """The K-step rollout kernel (dr_rollout; dr_rollout_random when gen):
     `reps` launches of k steps each over the same 65,536 envs, captured in
@@ -226,7 +311,108 @@ def time_rollout(args, n_envs, device, k, reps, gen, variant="gym", state_dtype=
     return per_launch
 
 
-def time_ppo(args, rank, world, device):
+# PPO algorithmic work: forward FLOP per sample of the 2x256
+# actor-critic (both MLPs' GEMMs and heads), training = 3 x forward per
+# sample and epoch (forward, input gradient, weight gradient)
+PPO_FWD_FLOP = 280064
+F32_MATRIX_PEAK_TFLOPS = 157.3     # MI355X f32 MFMA = f32 vector peak (spec)
+BF16_DENSE_PEAK_TFLOPS = 2500.0    # MI355X bf16 MFMA, dense (spec)
+
+
+def ppo_kernel_times(tr, reps=10):
+    """Every kernel of one configs[2] optimizer step (one 65,536-row
+    minibatch: gather, the fused forward / loss / backward, the deferred
+    finish + clip+Adam), enqueued eagerly `reps` times behind a spin kernel
+    that keeps the GPU busy while the host enqueues, with a HIP event on the
+    stream after each kernel: per-launch GPU time (kernel + its share of the
+    inter-kernel gap), averaged.  Runs after the timed region (it applies
+    `reps` more optimizer steps)."""
+    import torch
+
+    from drone_rl_amd import ppo_kernels as K
+    cfg = tr.cfg
+    T, N, M = cfg.n_steps, cfg.num_envs, cfg.batch_size
+    obs_flat = tr.obs[:T].reshape(T * N, -1)
+    act_flat = tr.actions.reshape(T * N, 4)
+    idx = tr.perm(seed=99, counter=0)[:M]
+    stream = torch.cuda.current_stream(tr.device)
+    sched = tr.opt.schedule(tr.opt.t + 1, 1).to(tr.device)
+    marks = []
+
+    def mark(name):
+        e = torch.cuda.Event(enable_timing=True)
+        e.record(stream)
+        marks.append((name, e))
+    torch.cuda.synchronize(tr.device)
+    torch.cuda._sleep(int(60e6))          # ~30 ms of spin: the host runs ahead
+    tr.fused.mark = mark
+    try:
+        mark("start")
+        for _ in range(reps):
+            K.gather_minibatch(idx, obs_flat, act_flat, tr.aux, tr.mb_obs, tr.mb_act,
+                               tr.mb_aux, adv_part=tr.head.adv_part)
+            mark("gather_minibatch")
+            grad, _ = tr.fused.step(tr.mb_obs, tr.mb_act, tr.mb_aux, tr.head, adv_ready=True,
+                                    defer_finish=True)
+            tr.opt.step_finish_sched(grad, tr.fused.finish, sched)
+            mark("grad_finish_clip_adam")
+    finally:
+        tr.fused.mark = None
+    torch.cuda.synchronize(tr.device)
+    acc = {}
+    for (_, e0), (name, e1) in zip(marks[:-1], marks[1:]):
+        acc[name] = acc.get(name, 0.0) + e0.elapsed_time(e1) * 1e3 / reps
+    return acc, (marks[-1][1], marks[0][1])
+
+
+def ppo_roofline(cfg, s_per_update, ktimes):
+    """The ppo block's roofline: the whole update's fp32-equivalent FLOP
+    rate against the f32 matrix peak, the 256x256 layer's x6 GEMMs against
+    the bf16 MFMA peak (6 bf16 products per fp32 product), and the
+    memory-bound kernels against HBM (algorithmic bytes per 65,536-row
+    minibatch)."""
+    M, NT, E = cfg.batch_size, cfg.num_envs * cfg.n_steps, cfg.n_epochs
+    flop_update = NT * PPO_FWD_FLOP * (1 + 3 * E)
+    gemm_flop = 2 * 2 * M * 256 * 256            # both nets, one fp32 GEMM
+    rows = {"gather_minibatch": 2 * (15 + 4 + 3) * 4,
+            "linear_tanh": 15 * 4 + 2 * 256 * 4,
+            "ppo_head": 2 * 1024 + 2 * 1024 + 44,
+            "first_layer_bwd": 2 * 2 * 1024 + 60}
+    kern = {}
+    for name, us in ktimes.items():
+        e = {"us": round(us, 2)}
+        if name.startswith("gemm_x6"):
+            tf32 = gemm_flop / (us * 1e-6) / 1e12
+            e.update({"bound": "mfma", "fp32_equiv_tflops": round(tf32, 1),
+                      "bf16_mfma_tflops": round(6 * tf32, 1),
+                      "frac": round(6 * tf32 / BF16_DENSE_PEAK_TFLOPS, 4)})
+        elif name in rows:
+            gbs = rows[name] * M / (us * 1e-6) / 1e9
+            e.update({"bound": "hbm", "bytes": rows[name] * M, "achieved_GBs": round(gbs, 1),
+                      "frac": round(gbs / HBM_PEAK_GBS, 4)})
+        kern[name] = e
+    ach = flop_update / s_per_update / 1e12
+    x6 = kern.get("gemm_x6_fwd")
+    out = {"bound": "mfma", "unit": "TFLOP/s",
+           "flop_per_update": flop_update,
+           "achieved": round(ach, 2), "peak": F32_MATRIX_PEAK_TFLOPS,
+           "frac": round(ach / F32_MATRIX_PEAK_TFLOPS, 4),
+           "basis": "fp32-equivalent FLOP per update (rollout forward 280,064 FLOP/sample + "
+                    "3 x forward per sample and epoch, SURVEY.md 8d) / s_per_update, against "
+                    "the f32 matrix peak",
+           "kernels_per_minibatch": kern,
+           "kernel_timing": "HIP events after each kernel of one optimizer step, eager, "
+                            "GPU kept busy ahead of the host; includes each launch's gap"}
+    if x6 is not None:
+        out["dominant_kernel"] = {"kernel": "gemm_x6_kernel (forward)", "bound": "mfma",
+                                  "achieved": x6["bf16_mfma_tflops"],
+                                  "peak": BF16_DENSE_PEAK_TFLOPS, "unit": "TFLOP/s",
+                                  "frac": x6["frac"]}
+    return out
+
+
+def time_ppo(args, rank, world, device, force_dp=False, dp_graph=False, profile=True,
+             updates=None):
     """configs[2]/[3]: 65,536 envs per GPU + PPO (2x256 tanh MLP, GAE 0.95),
     one PPO iteration = T-step rollout + GAE + n_epochs x minibatches."""
     import torch
@@ -236,17 +422,18 @@ def time_ppo(args, rank, world, device):
     from drone_rl_amd.ppo import PPOConfig, PPOTrainer
     cfg = PPOConfig(num_envs=args.envs, n_steps=args.ppo_steps, batch_size=args.envs,
                     n_epochs=args.ppo_epochs, state_dtype=args.state_dtype, seed=0,
-                    grad_buckets=args.grad_buckets)
+                    grad_buckets=args.grad_buckets, force_dp_path=force_dp, dp_graph=dp_graph)
     tr = PPOTrainer(cfg, device=device, rank=rank, world_size=world)
     # warm-up: the eager iteration, then the one that captures the rollout
-    # graph (replayed by every timed iteration)
+    # and training graphs (replayed by every timed iteration)
     tr.learn_step()
     tr.learn_step()
     torch.cuda.synchronize(device)
     if world > 1:
         dist.barrier()
+    K = args.ppo_updates if updates is None else updates
     t0 = time.perf_counter()
-    for _ in range(args.ppo_updates):
+    for _ in range(K):
         st = tr.learn_step()
     torch.cuda.synchronize(device)
     if world > 1:
@@ -259,31 +446,39 @@ def time_ppo(args, rank, world, device):
     es = tr.episode_stats()
     stats = dict(zip(("loss", "policy_loss", "value_loss", "entropy_loss", "clip_fraction",
                       "approx_kl"), [round(x, 5) for x in st.tolist()[:6]]))
+    path = ("data-parallel step (deferred finish -> " +
+            ("RCCL" if world > 1 or tr.dp_collective else "no") + " all-reduce -> clip+Adam)"
+            if tr.dp_step else "single-GPU fused step (deferred finish + clip+Adam)"
+            if tr._train_fast() else "per-kernel finishes")
+    res = {"updates_per_s": round(K / el, 4),
+           "env_steps_per_s": round(K * cfg.n_steps * cfg.num_envs * world / el, 1),
+           "s_per_update": round(el / K, 4),
+           "train_path": path, "train_graph": tr._train_graphable(),
+           "config": {"envs_per_gpu": cfg.num_envs, "n_steps": cfg.n_steps,
+                      "minibatch": cfg.batch_size, "n_epochs": cfg.n_epochs,
+                      "optimizer_steps_per_update": cfg.n_epochs * cfg.n_steps *
+                      cfg.num_envs // cfg.batch_size,
+                      "net_arch": list(cfg.net_arch), "mlp_dtype": "fp32",
+                      "gemm": (("256x256 layer forward, input gradient and weight gradient: "
+                                "dr_gemm_x6 / dr_gemm_x6_wgrad (fp32-accurate: exact 3-plane "
+                                "bf16 split, 6 MFMA products, f32 accumulate)"
+                                if x6_weights(tr.policy, cfg.batch_size) is not None else
+                                "256x256 layer: " + ("hipBLASLt/rocBLAS, MI355X-tuned solutions "
+                                                     "(TunableOp lookup)" if tr.tuned_gemms
+                                                     else "hipBLASLt heuristic"))),
+                      "grad_allreduce": ({"nccl": "rccl"}.get(dist.get_backend(),
+                                                              dist.get_backend())
+                                         + (" (2 buckets, the first overlapped with the "
+                                            "first-layer backward)" if cfg.grad_buckets == 2
+                                            else " (1 all-reduce of the flat gradient per "
+                                                 "optimizer step)"))
+                      if world > 1 or tr.dp_collective else "none"},
+           "last_update_stats": stats, "episodes": es}
+    if profile and world == 1 and tr._train_fast() and not tr.dp_step:
+        kt, _ = ppo_kernel_times(tr)
+        res["roofline"] = ppo_roofline(cfg, el / K, kt)
     tr.close()
-    K = args.ppo_updates
-    return {"updates_per_s": round(K / el, 4),
-            "env_steps_per_s": round(K * cfg.n_steps * cfg.num_envs * world / el, 1),
-            "s_per_update": round(el / K, 4),
-            "config": {"envs_per_gpu": cfg.num_envs, "n_steps": cfg.n_steps,
-                       "minibatch": cfg.batch_size, "n_epochs": cfg.n_epochs,
-                       "optimizer_steps_per_update": cfg.n_epochs * cfg.n_steps *
-                       cfg.num_envs // cfg.batch_size,
-                       "net_arch": list(cfg.net_arch), "mlp_dtype": "fp32",
-                       "gemm": (("256x256 layer forward, input gradient and weight gradient: "
-                                 "dr_gemm_x6 / dr_gemm_x6_wgrad (fp32-accurate: exact 3-plane "
-                                 "bf16 split, 6 MFMA products, f32 accumulate)"
-                                 if x6_weights(tr.policy, cfg.batch_size) is not None else
-                                 "256x256 layer: " + ("hipBLASLt/rocBLAS, MI355X-tuned solutions "
-                                                      "(TunableOp lookup)" if tr.tuned_gemms
-                                                      else "hipBLASLt heuristic"))),
-                       "grad_allreduce": ({"nccl": "rccl"}.get(dist.get_backend(),
-                                                               dist.get_backend())
-                                          + (" (2 buckets, the first overlapped with the "
-                                             "first-layer backward)" if cfg.grad_buckets == 2
-                                             else " (1 all-reduce of the flat gradient per "
-                                                  "optimizer step)")) if world > 1
-                       else "none"},
-            "last_update_stats": stats, "episodes": es}
+    return res
 
 
 def main():
@@ -311,21 +506,54 @@ def main():
         else:
             dist.init_process_group(backend)
 
-    elapsed, gpu_ms, ep = time_env(args, args.state_dtype, args.envs, rank, world, device,
-                                   args.steps, args.warmup)
     K, N = args.steps, args.envs
-    value = N * world * K / elapsed
-    per_launch_s = gpu_ms / 1e3 / K
-    bpe = BYTES_PER_ENV_STEP[args.state_dtype]
-    achieved = N * bpe / per_launch_s / 1e9
-    traffic = None
+    sb = 8 if args.state_dtype == "f64" else 4
+    state_b = (15 * sb + 4) + (12 * sb + 4)      # rollout kernel: state in + out per launch
+    tj = {}
     try:
         tj = json.load(open(args.traffic_json))
-        key = f"{args.state_dtype}_{N}"
-        if key in tj:
-            traffic = tj[key]["hbm_bytes_per_launch"]
-    except (OSError, ValueError, KeyError):
+    except (OSError, ValueError):
         pass
+
+    def step_block(elapsed, gpu_ms, steps, n):
+        pl = gpu_ms / 1e3 / steps
+        bpe = BYTES_PER_ENV_STEP[args.state_dtype]
+        ach = n * bpe / pl / 1e9
+        tr = tj.get(f"{args.state_dtype}_{n}", {}).get("hbm_bytes_per_launch")
+        return {"env_steps_per_s": round(n * world * steps / elapsed, 1),
+                "ms_per_step": round(elapsed / steps * 1e3, 6),
+                "roofline": {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
+                             "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4),
+                             "traffic": tr,
+                             "traffic_GBs": round(tr / pl / 1e9, 1) if tr else None,
+                             "kernel": "env_step_kernel", "bytes_per_env_step": bpe,
+                             "avg_launch_us": round(pl * 1e6, 3)}}
+
+    el_s, gm_s, ep_s = time_env(args, args.state_dtype, N, rank, world, device, K, args.warmup)
+    single = step_block(el_s, gm_s, K, N)
+    if args.headline == "rollout":
+        elapsed, gpu_ms, launches, ep = time_headline(args, N, rank, world, device, K,
+                                                      args.warmup, args.headline_k)
+        per_launch_s = gpu_ms / 1e3 / launches
+        bpe = 81 + state_b * launches / K
+        achieved = N * K * bpe / (gpu_ms / 1e3) / 1e9
+        kh = -(-K // launches)
+        tr = tj.get(f"rollout_{args.state_dtype}_{N}_k{kh}", {}).get("hbm_bytes_per_launch")
+        roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+                "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": tr,
+                "traffic_GBs": round(tr / per_launch_s / 1e9, 1) if tr else None,
+                "kernel": "env_rollout_kernel", "steps_per_launch": kh, "launches": launches,
+                "bytes_per_env_step": round(bpe, 2),
+                "bytes_basis": "per env-step 16 action + 60 obs + 4 reward + 1 done; per "
+                               "launch and env the f64 state read (124 B) and written (100 B) "
+                               "once",
+                "avg_launch_us": round(per_launch_s * 1e6, 3),
+                "limiter": "latency at one wave per SIMD (VALU active 0.48 of wave cycles, "
+                           "profiles/r02_pmc_rollout.json)"}
+    else:
+        elapsed, gpu_ms, ep = el_s, gm_s, ep_s
+        roof = single["roofline"]
+    value = N * world * K / elapsed
     out = {
         "metric": "env-steps/s (whole node) + PPO updates/s, 65 536 envs/GPU, 2x256 MLP",
         "value": round(value, 1),
@@ -338,20 +566,19 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": args.state_dtype,
-        "data": "synthetic (random policy U[0,7.3575)^4 f32 actions, Philox; "
-                "reset draws Philox)",
+        "data": "synthetic (random policy U[0,7.3575)^4 f32 actions, Philox, pre-generated in "
+                "HBM; reset draws Philox)",
         "config": {"workload": "configs[1]: 65,536 batched DroneGymEnv envs per GPU, "
-                               "random policy, dynamics-kernel throughput (auto-reset in step)",
+                               "random policy, dynamics-kernel throughput (auto-reset in step, "
+                               "every step's obs / reward / done written)",
                    "envs_per_gpu": N, "global_envs": N * world,
-                   "state_dtype": args.state_dtype, "hipgraph": not args.no_graph,
+                   "state_dtype": args.state_dtype, "hipgraph": True,
+                   "kernel": ("dr_rollout (K-step rollout kernel, <= %d steps per launch)"
+                              % args.headline_k if args.headline == "rollout"
+                              else "dr_step (one launch per step)"),
                    "parallelism": f"dp{world} (independent env shards)"},
-        "roofline": {"bound": "hbm", "achieved": round(achieved, 1),
-                     "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                     "traffic_GBs": (round(traffic / per_launch_s / 1e9, 1)
-                                     if traffic else None),
-                     "kernel": "env_step_kernel", "bytes_per_env_step": bpe,
-                     "avg_launch_us": round(per_launch_s * 1e6, 3)},
+        "roofline": roof,
+        "single_step": single,
         "mean_ep_num": round(ep, 2),
     }
     if world == 1 and not args.no_companion:
@@ -361,7 +588,7 @@ def main():
         n4, k4 = 1 << 22, 200
         el4, gm4, _ = time_env(args, args.state_dtype, n4, 0, 1, device, k4, 20)
         pl4 = gm4 / 1e3 / k4
-        ach4 = n4 * bpe / pl4 / 1e9
+        ach4 = n4 * BYTES_PER_ENV_STEP[args.state_dtype] / pl4 / 1e9
         tr4 = None
         try:
             tr4 = json.load(open(args.traffic_json))[f"{args.state_dtype}_{n4}"][
@@ -390,9 +617,11 @@ def main():
                 "env_steps_per_s": round(N * k / pl, 1),
                 "avg_launch_us": round(pl * 1e6, 3), "us_per_step": round(pl * 1e6 / k, 3),
                 "bytes_per_env_step": round(bpe, 2),
-                "roofline": {"bound": "valu (f64 issue; DESIGN.md 6)", "achieved": round(ach, 1),
+                "roofline": {"bound": "hbm", "achieved": round(ach, 1),
                              "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                             "frac": round(ach / HBM_PEAK_GBS, 4)}}
+                             "frac": round(ach / HBM_PEAK_GBS, 4)},
+                "valu_active_frac_of_wave_cycles": PMC_ROLLOUT_VALU_ACTIVE[
+                    "random_policy_in_kernel" if gen else "actions_from_hbm"]}
         out["rollout_kernel"] = ro
     if cpu is not None:
         out["cpu_baseline"] = cpu
@@ -400,6 +629,28 @@ def main():
         out["ppo"] = time_ppo(args, rank, world, device)
     if args.extra and world == 1:
         ex = {}
+        # the data-parallel optimizer step (PPOTrainer at world > 1: deferred
+        # finish -> gradient all-reduce -> clip+Adam) timed on one GPU: with
+        # no process group (all-reduce skipped), then on a one-rank RCCL
+        # group with the all-reduce captured in the training graph
+        if args.ppo_updates > 0:
+            ex["ppo_dp_path_world1"] = time_ppo(args, 0, 1, device, force_dp=True,
+                                                profile=False)
+            try:
+                import socket
+                sk = socket.socket()
+                sk.bind(("127.0.0.1", 0))
+                port = sk.getsockname()[1]
+                sk.close()
+                dist.init_process_group("nccl", rank=0, world_size=1, device_id=device,
+                                        init_method=f"tcp://127.0.0.1:{port}")
+                ex["ppo_dp_path_world1_rccl_graph"] = time_ppo(
+                    args, 0, 1, device, force_dp=True, dp_graph=True, profile=False)
+            except Exception as e:      # report, keep the rest of the line
+                ex["ppo_dp_path_world1_rccl_graph"] = {"error": repr(e)[:300]}
+            finally:
+                if dist.is_initialized():
+                    dist.destroy_process_group()
         saved = os.environ.get("DRONERL_STEP_KERNEL")
         for kern in ("quad", "lane"):
             os.environ["DRONERL_STEP_KERNEL"] = kern

@@ -1662,14 +1662,16 @@ inline int loss_head_blocks(int64_t m) {
 // ---------------------------------------------------------------------------
 // clip_grad_norm_ + Adam over one flat fp32 buffer.
 // ---------------------------------------------------------------------------
+// `scale` multiplies every entry first (1 / world for a summed data-parallel
+// gradient; x * 1 is x bitwise, so the single-GPU path is unchanged).
 __global__ __launch_bounds__(kBlock) void sumsq_kernel(int64_t n,
                                                        const float *__restrict__ g,
-                                                       float *__restrict__ part) {
+                                                       float *__restrict__ part, float scale) {
     __shared__ float sh[4];
     float acc = 0.f;
     for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n;
          i += (int64_t)gridDim.x * kBlock) {
-        const float x = g[i];
+        const float x = g[i] * scale;
         acc += x * x;
     }
     float x[1] = {acc};
@@ -1753,7 +1755,7 @@ __global__ __launch_bounds__(kBlock) void clip_adam_kernel(
     float *__restrict__ m, float *__restrict__ v, const float *__restrict__ part,
     int nb, float max_norm, float w1, float beta2, float one_m_b2,
     float step_size, float bc2_sqrt, const float *__restrict__ sched, float eps,
-    float *norm_out) {
+    float *norm_out, float gscale) {
     // sched (device): this step's (step_size, sqrt(bias_correction2)), written
     // by the host from dr_adam_schedule ahead of a graph replay
     if (sched) {
@@ -1777,7 +1779,7 @@ __global__ __launch_bounds__(kBlock) void clip_adam_kernel(
     if (blockIdx.x == 0 && threadIdx.x == 0 && norm_out) *norm_out = total;
     for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n;
          i += (int64_t)gridDim.x * kBlock) {
-        const float gi = g[i] * c;
+        const float gi = (g[i] * gscale) * c;   // gscale: sumsq_kernel's scale
         g[i] = gi;
         float mi = m[i];
         mi = mi + w1 * (gi - mi);                    // exp_avg.lerp_(g, 1-b1)
@@ -2036,7 +2038,7 @@ static int launch_adam(int64_t n, float *params, float *grads, float *exp_avg,
                        float *exp_avg_sq, double lr, double beta1, double beta2, double eps,
                        float max_grad_norm, int64_t step, float *grad_norm_out,
                        const float *sq_part, int nsq, hipStream_t st, const char *who,
-                       const float *sched = nullptr) {
+                       const float *sched = nullptr, float gscale = 1.0f) {
     // torch.optim.Adam scalars, formed in double as torch does on the host.
     const double b1 = beta1, b2 = beta2;
     float ss[2] = {0.f, 1.f};
@@ -2044,7 +2046,7 @@ static int launch_adam(int64_t n, float *params, float *grads, float *exp_avg,
     hipLaunchKernelGGL(clip_adam_kernel, dim3(nblocks_stream(n)), dim3(kBlock), 0, st, n,
                        params, grads, exp_avg, exp_avg_sq, sq_part, nsq, max_grad_norm,
                        (float)(1.0 - b1), (float)b2, (float)(1.0 - b2), ss[0], ss[1], sched,
-                       (float)eps, grad_norm_out);
+                       (float)eps, grad_norm_out, gscale);
     return check_launch(who);
 }
 
@@ -2072,7 +2074,7 @@ int dr_clip_adam(int64_t n, float *params, float *grads, float *exp_avg, float *
     const int nb = nblocks_stream(n);
     float *part = static_cast<float *>(workspace);
     hipStream_t st = as_stream(stream);
-    hipLaunchKernelGGL(sumsq_kernel, dim3(nb), dim3(kBlock), 0, st, n, grads, part);
+    hipLaunchKernelGGL(sumsq_kernel, dim3(nb), dim3(kBlock), 0, st, n, grads, part, 1.0f);
     int rc = check_launch("dr_clip_adam norm");
     if (rc) return rc;
     return launch_adam(n, params, grads, exp_avg, exp_avg_sq, lr, beta1, beta2, eps,
@@ -2085,30 +2087,28 @@ size_t dr_grad_finish_workspace_bytes(const dr_grad_finish *f) {
     return align_up(sizeof(float) * (size_t)(bh + bf + bc > 0 ? bh + bf + bc : 1));
 }
 
-static int grad_finish_adam_impl(const dr_grad_finish *f, int64_t n, float *params,
-                                 float *grads, float *exp_avg, float *exp_avg_sq, double lr,
-                                 double beta1, double beta2, double eps, float max_grad_norm,
-                                 int64_t step, const float *sched, float *grad_norm_out,
-                                 void *workspace, size_t workspace_bytes, void *stream) {
-    if (!f || n < 1 || !params || !grads || !exp_avg || !exp_avg_sq || (step < 1 && !sched))
-        return fail0(DR_ERR_INVALID, "dr_grad_finish_clip_adam: bad arguments");
+// Validates f and launches grad_finish_kernel (every deferred partial into
+// the flat gradient, the norm partials into workspace); *nsq = its blocks.
+static int launch_grad_finish(const dr_grad_finish *f, void *workspace, size_t workspace_bytes,
+                              hipStream_t st, int *nsq) {
+    if (!f) return fail0(DR_ERR_INVALID, "dr_grad_finish: null descriptor");
     if (f->head_workspace && (f->head_m < 1 || f->head_hd < 4 || f->head_hd > 256 ||
                               !f->log_std || !f->g_w_act || !f->g_b_act || !f->g_w_val ||
                               !f->g_b_val || !f->g_b_pi || !f->g_b_vf || !f->g_log_std ||
                               !f->stats))
-        return fail0(DR_ERR_INVALID, "dr_grad_finish_clip_adam: bad head arguments");
+        return fail0(DR_ERR_INVALID, "dr_grad_finish: bad head arguments");
     if (f->first_workspace && (f->first_m < 1 || f->first_n < 4 || f->first_n > 256 ||
                                f->first_k < 1 || !f->g_w0 || !f->g_b0 || !f->g_w1 || !f->g_b1))
-        return fail0(DR_ERR_INVALID, "dr_grad_finish_clip_adam: bad first-layer arguments");
+        return fail0(DR_ERR_INVALID, "dr_grad_finish: bad first-layer arguments");
     if (f->chunks && (f->chunk_groups < 1 || f->chunk_count < 1 || f->chunk_size < 1 ||
                       !f->chunk_dst))
-        return fail0(DR_ERR_INVALID, "dr_grad_finish_clip_adam: bad chunk arguments");
+        return fail0(DR_ERR_INVALID, "dr_grad_finish: bad chunk arguments");
     if (!workspace || workspace_bytes < dr_grad_finish_workspace_bytes(f))
-        return fail0(DR_ERR_INVALID, "dr_grad_finish_clip_adam: workspace too small");
+        return fail0(DR_ERR_INVALID, "dr_grad_finish: workspace too small");
     FinishArgs a{};
     finish_blocks(f, a.bh, a.bf, a.bc);
     if (a.bh + a.bf + a.bc < 1)
-        return fail0(DR_ERR_INVALID, "dr_grad_finish_clip_adam: nothing to finish");
+        return fail0(DR_ERR_INVALID, "dr_grad_finish: nothing to finish");
     if (f->head_workspace) {
         const int64_t m = f->head_m, hd = f->head_hd;
         const int nb = loss_head_blocks(m);
@@ -2150,16 +2150,54 @@ static int grad_finish_adam_impl(const dr_grad_finish *f, int64_t n, float *para
         a.chunks = f->chunks;
         a.c_dst = f->chunk_dst;
     }
-    float *part = static_cast<float *>(workspace);
-    a.sq_part = part;
-    const int nb = a.bh + a.bf + a.bc;
+    a.sq_part = static_cast<float *>(workspace);
+    *nsq = a.bh + a.bf + a.bc;
+    hipLaunchKernelGGL(grad_finish_kernel, dim3(*nsq), dim3(kBlock), 0, st, a);
+    return check_launch("dr_grad_finish");
+}
+
+static int grad_finish_adam_impl(const dr_grad_finish *f, int64_t n, float *params,
+                                 float *grads, float *exp_avg, float *exp_avg_sq, double lr,
+                                 double beta1, double beta2, double eps, float max_grad_norm,
+                                 int64_t step, const float *sched, float *grad_norm_out,
+                                 void *workspace, size_t workspace_bytes, void *stream) {
+    if (!f || n < 1 || !params || !grads || !exp_avg || !exp_avg_sq || (step < 1 && !sched))
+        return fail0(DR_ERR_INVALID, "dr_grad_finish_clip_adam: bad arguments");
     hipStream_t st = as_stream(stream);
-    hipLaunchKernelGGL(grad_finish_kernel, dim3(nb), dim3(kBlock), 0, st, a);
-    int rc = check_launch("dr_grad_finish_clip_adam finish");
+    int nb = 0;
+    const int rc = launch_grad_finish(f, workspace, workspace_bytes, st, &nb);
     if (rc) return rc;
     return launch_adam(n, params, grads, exp_avg, exp_avg_sq, lr, beta1, beta2, eps,
-                       max_grad_norm, step, grad_norm_out, part, nb, st,
-                       "dr_grad_finish_clip_adam", sched);
+                       max_grad_norm, step, grad_norm_out, static_cast<const float *>(workspace),
+                       nb, st, "dr_grad_finish_clip_adam", sched);
+}
+
+int dr_grad_finish_run(const dr_grad_finish *f, void *workspace, size_t workspace_bytes,
+                   void *stream) {
+    int nb = 0;
+    return launch_grad_finish(f, workspace, workspace_bytes, as_stream(stream), &nb);
+}
+
+int dr_clip_adam_sched(int64_t n, float *params, float *grads, float *exp_avg,
+                       float *exp_avg_sq, double beta1, double beta2, double eps,
+                       float max_grad_norm, float grad_scale, const float *sched,
+                       float *grad_norm_out, void *workspace, size_t workspace_bytes,
+                       void *stream) {
+    if (n < 1 || !params || !grads || !exp_avg || !exp_avg_sq || !sched ||
+        (((uintptr_t)sched) & 7) || !(grad_scale > 0.0f))
+        return fail0(DR_ERR_INVALID, "dr_clip_adam_sched: bad arguments (sched 8-byte "
+                                     "aligned, grad_scale > 0)");
+    if (!workspace || workspace_bytes < dr_adam_workspace_bytes(n))
+        return fail0(DR_ERR_INVALID, "dr_clip_adam_sched: workspace too small");
+    const int nb = nblocks_stream(n);
+    float *part = static_cast<float *>(workspace);
+    hipStream_t st = as_stream(stream);
+    hipLaunchKernelGGL(sumsq_kernel, dim3(nb), dim3(kBlock), 0, st, n, grads, part, grad_scale);
+    const int rc = check_launch("dr_clip_adam_sched norm");
+    if (rc) return rc;
+    return launch_adam(n, params, grads, exp_avg, exp_avg_sq, 0.0, beta1, beta2, eps,
+                       max_grad_norm, 0, grad_norm_out, part, nb, st, "dr_clip_adam_sched", sched,
+                       grad_scale);
 }
 
 int dr_grad_finish_clip_adam(const dr_grad_finish *f, int64_t n, float *params, float *grads,

@@ -4,15 +4,19 @@ The env batch shards with no exchange at all: rank r owns global env ids
 [r*N, (r+1)*N) (its Philox streams are keyed by those ids).  PPO adds the
 only collectives on the hot path:
   * one broadcast of the flat parameter buffer at start (rank 0 -> all),
-  * the all-reduce (sum, then 1/world) of the flat fp32 gradient per
-    optimizer step -- 141,065 floats = 564 KB for the 2x256 net -- as two
-    buckets: everything but the first layer (started asynchronously as soon
-    as the fused backward has finished it, so it overlaps the first-layer
-    backward) and the first layer (8k floats) at the end.  Buckets are not
-    split further: at this size xGMI is latency-bound,
+  * ONE sum all-reduce of the flat fp32 gradient per optimizer step --
+    141,065 floats = 564 KB for the 2x256 net -- between the launch that
+    finishes the deferred gradient reductions and clip+Adam, which takes
+    the 1/world mean inside its norm and update (PPOTrainer._train_body,
+    grad_buckets=1, the default).  At this size an xGMI ring is latency-
+    bound, so the buffer is not split.  grad_buckets=2 keeps an older step
+    whose per-kernel finishes let everything but the first layer start as
+    an async bucket while the first-layer backward runs
+    (BucketedAllReduce),
   * one all-reduce of 3 episode-statistics scalars per logged update.
 Backend "nccl" is RCCL on ROCm; every function also runs under gloo (CPU
-tests, tests/test_dist_cpu.py).
+tests, tests/test_dist_cpu.py; two ranks sharing one GPU in the -m gpu
+tests, where RCCL refuses two ranks per device).
 """
 from __future__ import annotations
 
@@ -41,6 +45,15 @@ def allreduce_mean_(t: torch.Tensor, world: int, group=None) -> torch.Tensor:
 def allreduce_sum_(t: torch.Tensor, world: int, group=None) -> torch.Tensor:
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group)
+    return t
+
+
+def allreduce_flat_sum_(t: torch.Tensor, group=None) -> torch.Tensor:
+    """The per-optimizer-step gradient all-reduce: in-place sum over the
+    group's ranks, enqueued on the current stream (RCCL: the stream waits
+    for it, the host does not; capturable into a hipGraph).  Called even on
+    a one-rank group (PPOConfig.force_dp_path) so the collective path runs."""
+    dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group)
     return t
 
 

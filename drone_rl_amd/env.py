@@ -160,7 +160,12 @@ class DroneBatch:
         in-kernel random policy (step t draws random_actions(N, seed, step0+t,
         env_id_offset, lo, hi); `actions_out` (k,N,4) receives them if given).
         Returns (obs (k,N,obs_dim), rew (k,N), done (k,N)); no terminal obs or
-        VecMonitor counters (use step() for those)."""
+        VecMonitor counters (use step() for those).  Refused on a monitor=True
+        batch: the launch does not advance the running episode return /
+        length, so a later step() would report wrong episodes."""
+        if self.monitor:
+            raise ValueError("rollout() on a monitor=True batch would leave the VecMonitor "
+                             "episode counters stale; use step() or a monitor=False batch")
         k = int(k)
         n, od, dev = self.num_envs, self.obs_dim, self.device
         obs = torch.empty(k, n, od, dtype=torch.float32, device=dev) if obs_out is None else obs_out

@@ -291,6 +291,10 @@ class FusedTrainStep:
         self._ws = torch.empty(self.C * wmax * max(dims), **f32)
         self.tanh_ws = torch.empty(
             max(K.tanh_backward_workspace_bytes(m, n) for n in policy.net_arch) // 4 + 1, **f32)
+        # optional instrumentation: mark(name) is called on the host right
+        # after each kernel of the fused step is enqueued (bench.py records a
+        # HIP event there to time every kernel on the stream)
+        self.mark = None
 
     def gview(self, name):
         a, b, shape = self.pol.offsets[name]
@@ -381,7 +385,9 @@ class FusedTrainStep:
         preact = depth >= 2                   # top tanh applied inside the head kernel
         if defer_finish and (not self.can_defer() or on_ready is not None):
             raise ValueError("defer_finish needs a 2-hidden-layer net and no on_ready")
-        hs = hidden_forward(pol, obs, self._acts, self._acts2, rows, top_preact=preact)
+        mark = self.mark or _no_mark
+        hs = hidden_forward(pol, obs, self._acts, self._acts2, rows, top_preact=preact,
+                            mark=self.mark)
         gz = self._gz2[top]
         stats = head(hs["pi"][top], hs["vf"][top], pol.p("action.w"), pol.p("action.b"),
                      pol.p("value.w"), pol.p("value.b"), pol.log_std, actions, aux,
@@ -390,6 +396,7 @@ class FusedTrainStep:
                      self.gview(f"pi{top}.b"), self.gview(f"vf{top}.b"),
                      self.gview("log_std"), rows, preact=preact, adv_ready=adv_ready,
                      stats_out=stats_out, defer=defer_finish, **top_bias(pol, self._acts2))
+        mark("ppo_head")
         if depth == 1:                        # the head kernel gave grad_z of layer 0
             if rows is not None:
                 obs = obs.index_select(0, rows.long())
@@ -400,6 +407,7 @@ class FusedTrainStep:
             x = self._acts2[k - 1]
             n_in = x.shape[2]
             self._wgrad2(gz, x, pol.p2(k, "w", self.grad), defer=defer_finish)
+            mark("gemm_x6_wgrad")
             if k == 1 and on_ready is not None:
                 # all but the first layer's gradient is final from here on
                 on_ready(self.first_layer_end(), self.grad.numel())
@@ -409,12 +417,14 @@ class FusedTrainStep:
                 gemm_x6(gz, xw.bwd, g)       # images refreshed by hidden_forward
             else:
                 torch.bmm(gz, pol.p2(k, "w"), out=g)
+            mark("gemm_x6_bwd")
             if k == 1:
                 # first layer of both MLPs: tanh backward + weight/bias
                 # gradients fused, one launch
                 self._first(obs, g[0], x[0], self.gview("pi0.w"), self.gview("pi0.b"),
                             g[1], x[1], self.gview("vf0.w"), self.gview("vf0.b"), rows,
                             defer=defer_finish)
+                mark("first_layer_bwd")
             else:
                 gz = self._gz2[k - 1]
                 for j, pre in enumerate(("pi", "vf")):
@@ -512,7 +522,8 @@ def fusable(pol: ActorCritic) -> bool:
 
 
 @torch.no_grad()
-def hidden_forward(pol: ActorCritic, obs, acts, acts2=None, rows=None, top_preact=False):
+def hidden_forward(pol: ActorCritic, obs, acts, acts2=None, rows=None, top_preact=False,
+                   mark=None):
     """Hidden activations of the pi and vf MLPs into preallocated buffers
     acts[pre][k] (M, net_arch[k]); with acts2 (the (2, M, n) buffers that
     acts views) each layer's tanh runs once over both MLPs; with rows the
@@ -523,15 +534,19 @@ def hidden_forward(pol: ActorCritic, obs, acts, acts2=None, rows=None, top_preac
     top GEMMs run as ONE batched GEMM (no bias epilogue; 125 us against
     2 x 74 us for two addmm at M = 65,536, MI355X-tuned solutions)."""
     from . import ppo_kernels as K
+    mark = mark or _no_mark
     K.linear_tanh2(obs, pol.p("pi0.w"), pol.p("pi0.b"), acts["pi"][0],
                    pol.p("vf0.w"), pol.p("vf0.b"), acts["vf"][0], rows)
+    mark("linear_tanh")
     top = len(pol.net_arch) - 1
     for k in range(1, len(pol.net_arch)):
         if top_preact and k == top and acts2 is not None:
             xw = x6_weights(pol, acts2[k - 1].shape[1]) if k == 1 else None
             if xw is not None:
                 xw.refresh()                 # the weights may have changed since
+                mark("split_weights")
                 gemm_x6(acts2[k - 1], xw.fwd, acts2[k])
+                mark("gemm_x6_fwd")
             else:
                 torch.bmm(acts2[k - 1], pol.p2(k, "w").transpose(1, 2), out=acts2[k])
             continue
@@ -546,6 +561,10 @@ def hidden_forward(pol: ActorCritic, obs, acts, acts2=None, rows=None, top_preac
             for pre in ("pi", "vf"):
                 torch.tanh_(acts[pre][k])
     return acts
+
+
+def _no_mark(name):
+    pass
 
 
 def top_bias(pol: ActorCritic, acts2) -> dict:

@@ -8,11 +8,12 @@ with a loop whose every byte stays in HBM:
                       (Gaussian action, log-prob, clip)  ->  dr_step_monitored
                       (env physics + auto-reset + VecMonitor stats)
   advantages:         dr_gae (reverse scan, one thread per env)
-  update (epochs):    dr_permutation  ->  dr_gather_rows (minibatch)  ->
-                      policy fwd/bwd (torch autograd over one flat buffer)
-                      with the loss head from dr_ppo_loss  ->  [RCCL
+  update (epochs):    dr_permutation  ->  dr_gather_minibatch  ->  fused
+                      MLP forward / loss / backward (policy.FusedTrainStep)
+                      ->  one launch of the deferred reductions  ->  [RCCL
                       all-reduce of the flat grad when world > 1]  ->
-                      dr_clip_adam (clip_grad_norm_ + Adam, fused)
+                      clip_grad_norm_ + Adam (fused); the whole loop is one
+                      hipGraph replay on one GPU
 
 SB3-parity choices (documented deviations in DESIGN.md):
   * no value bootstrap at the 200-step limit (the reference's env is wrapped
@@ -72,6 +73,16 @@ class PPOConfig:
     # started asynchronously as soon as the fused backward finished it
     # (overlapping the first-layer backward), the first layer at the end
     grad_buckets: int = 1
+    # the data-parallel optimizer step (deferred finish -> gradient
+    # all-reduce -> clip+Adam from device scalars) even at world 1, where
+    # the all-reduce is skipped unless a process group is initialised:
+    # times the 8-GPU code path on one GPU (bench.py --extra, tests)
+    force_dp_path: bool = False
+    # capture the data-parallel training loop, RCCL all-reduces included,
+    # into the training hipGraph (backend "nccl" only; DRONERL_DP_GRAPH=1).
+    # Off by default: graph capture of RCCL collectives has only been run
+    # on a one-rank group here (no multi-GPU box for the builder)
+    dp_graph: bool = False
 
     @classmethod
     def sb3_defaults(cls, **kw):
@@ -137,6 +148,19 @@ class PPOTrainer:
         # launch before Adam (DRONERL_DEFER_FINISH=0: separate launches)
         self.defer_finish = (self.use_fused and self.fused.can_defer() and
                              os.environ.get("DRONERL_DEFER_FINISH", "1") != "0")
+        # data-parallel optimizer step on the same kernels as the single-GPU
+        # one: ONE finish launch of the deferred reductions, ONE all-reduce
+        # of the flat gradient, ONE clip+Adam (grad_buckets 2 keeps the
+        # older early-bucket step, whose finishes run per kernel)
+        dp_want = world_size > 1 or cfg.force_dp_path
+        self.dp_step = (dp_want and self.defer_finish and cfg.grad_buckets == 1)
+        # the summing all-reduce runs when there are ranks to sum over, or
+        # (force_dp_path) whenever a process group exists, so a one-rank
+        # RCCL group exercises the collective and its graph capture
+        self.dp_collective = self.dp_step and (
+            world_size > 1 or (D.dist.is_available() and D.dist.is_initialized()))
+        self.dp_graph = self.dp_step and (
+            cfg.dp_graph or os.environ.get("DRONERL_DP_GRAPH", "0") == "1")
         if self.use_fused:
             self.head = K.HeadLossBackward(M, cfg.net_arch[-1], dev, cfg.clip_range,
                                            cfg.ent_coef, cfg.vf_coef, cfg.normalize_advantage)
@@ -248,9 +272,18 @@ class PPOTrainer:
                 o.max_norm, float(self.head.clip), float(self.head.ent), float(self.head.vf),
                 self.head.norm)
 
+    def _train_fast(self) -> bool:
+        """The deferred-finish step with device-side Adam scalars: the
+        single-GPU step, or the data-parallel split step."""
+        return self.use_fused and self.defer_finish and (self.world == 1 or self.dp_step)
+
     def _train_graphable(self) -> bool:
-        return (self.train_graph and self.use_fused and self.defer_finish and
-                self.world == 1)
+        if not (self.train_graph and self._train_fast()):
+            return False
+        if not self.dp_collective:
+            return True
+        # a collective inside the captured loop: RCCL only, and opt-in
+        return self.dp_graph and D.dist.get_backend(self.pg) == "nccl"
 
     def _train_body(self, obs_flat, act_flat, nmb):
         """PPO.train's epochs x minibatches on the single-GPU fused path with
@@ -269,7 +302,15 @@ class PPOTrainer:
                 grad, _ = self.fused.step(self.mb_obs, self.mb_act, self.mb_aux, self.head,
                                           adv_ready=True, stats_out=self._tstats[j],
                                           defer_finish=True)
-                self.opt.step_finish_sched(grad, self.fused.finish, self._sched[j])
+                if self.dp_step:
+                    # finish -> one all-reduce (sum) of the 564 KB flat
+                    # gradient -> clip+Adam on its mean
+                    self.fused.finish.run(self.device)
+                    if self.dp_collective:
+                        D.allreduce_flat_sum_(grad, group=self.pg)
+                    self.opt.step_sched(grad, self._sched[j], 1.0 / self.world)
+                else:
+                    self.opt.step_finish_sched(grad, self.fused.finish, self._sched[j])
                 j += 1
 
     def _train_graphed(self):
@@ -290,7 +331,9 @@ class PPOTrainer:
         if self._tgraph is not None and key != self._tkey:
             self._tgraph = None
         self._tkey = key
-        if self._tgraph is not None:
+        if not self._train_graphable():
+            self._train_body(obs_flat, act_flat, nmb)       # eager (e.g. DP over gloo)
+        elif self._tgraph is not None:
             self._tgraph.replay()
         elif not self._twarm:
             self._train_body(obs_flat, act_flat, nmb)       # eager once: lazy init
@@ -310,7 +353,7 @@ class PPOTrainer:
 
     @torch.no_grad()
     def train(self):
-        if self._train_graphable():
+        if self._train_fast():
             return self._train_graphed()
         cfg = self.cfg
         T, N, M = cfg.n_steps, cfg.num_envs, cfg.batch_size

@@ -222,6 +222,19 @@ class ClipAdam:
             finish.ws.numel(), _s(self.p)))
         return self.grad_norm
 
+    def step_sched(self, grads: torch.Tensor, sched: torch.Tensor, grad_scale: float = 1.0):
+        """clip_grad_norm_ + Adam on grad_scale * grads (1 / world after a
+        summing all-reduce) with this step's scalars read on the device
+        from `sched` (dr_clip_adam_sched; graph-capturable, advances nothing
+        on the host).  After dr_grad_finish_run at grad_scale 1 this is
+        bitwise step_finish_sched."""
+        check(_lib.lib().dr_clip_adam_sched(
+            self.p.numel(), ptr(self.p), ptr(_f32(grads)), ptr(self.m), ptr(self.v),
+            float(self.b1), float(self.b2), float(self.eps), float(self.max_norm),
+            float(grad_scale), ptr(sched), ptr(self.grad_norm), ptr(self.ws), self.ws.numel(),
+            _s(self.p)))
+        return self.grad_norm
+
     def step(self, grads: torch.Tensor, lr=None):
         self.t += 1
         check(_lib.lib().dr_clip_adam(
@@ -386,3 +399,17 @@ class GradFinish:
     def __init__(self):
         self.desc = _lib.dr_grad_finish()
         self.ws = None
+
+    def _workspace(self, device):
+        need = _lib.lib().dr_grad_finish_workspace_bytes(ctypes.byref(self.desc))
+        if self.ws is None or self.ws.numel() < need:
+            self.ws = torch.empty(need, dtype=torch.uint8, device=device)
+        return self.ws
+
+    def run(self, device):
+        """dr_grad_finish_run: every deferred partial reduced into the flat
+        gradient (and the loss stats) on the current stream -- the
+        data-parallel step's finish, ahead of the gradient all-reduce."""
+        ws = self._workspace(device)
+        check(_lib.lib().dr_grad_finish_run(ctypes.byref(self.desc), ptr(ws), ws.numel(),
+                                            torch.cuda.current_stream(device).cuda_stream))

@@ -39,7 +39,7 @@
 extern "C" {
 #endif
 
-#define DR_ABI_VERSION 11
+#define DR_ABI_VERSION 12
 
 enum dr_status {
     DR_OK = 0,
@@ -479,6 +479,25 @@ int dr_grad_finish_clip_adam_sched(const dr_grad_finish *f, int64_t n, float *pa
                                    float max_grad_norm, const float *sched,
                                    float *grad_norm_out, void *workspace,
                                    size_t workspace_bytes, void *stream);
+
+/* The data-parallel split of dr_grad_finish_clip_adam_sched (SB3 PPO.train
+   + the north_star's one gradient all-reduce per optimizer step over ranks,
+   /root/reference/train.py:63-68): dr_grad_finish_run reduces every deferred
+   partial of `f` into the flat gradient (and the loss stats) in ONE launch;
+   the caller then sums the gradient over ranks (RCCL all-reduce) and
+   dr_clip_adam_sched applies clip_grad_norm_ + Adam to grad_scale * grads
+   (grad_scale = 1 / world: the mean) with the step's scalars read on the
+   device from `sched` (dr_adam_schedule).  At grad_scale 1 the pair is
+   bitwise dr_grad_finish_clip_adam_sched; both are graph-capturable.
+   dr_grad_finish_run's `workspace` >= dr_grad_finish_workspace_bytes(f);
+   dr_clip_adam_sched's >= dr_adam_workspace_bytes(n).  (ABI v12.) */
+int dr_grad_finish_run(const dr_grad_finish *f, void *workspace, size_t workspace_bytes,
+                   void *stream);
+int dr_clip_adam_sched(int64_t n, float *params, float *grads, float *exp_avg,
+                       float *exp_avg_sq, double beta1, double beta2, double eps,
+                       float max_grad_norm, float grad_scale, const float *sched,
+                       float *grad_norm_out, void *workspace, size_t workspace_bytes,
+                       void *stream);
 
 /* ---- fp32-accurate 256 x 256 layer GEMM on the bf16 matrix cores ---------
    Replaces the torch fp32 Linear of SB3's MlpExtractor 256 -> 256 layer

@@ -26,73 +26,14 @@ bounds instead of a fraction of the largest update:
   eps)^2 and through the clip factor (d c / c <= ||dg|| / ||g||), plus the
   fp32 rounding of the update itself and of the parameter (one ulp).
 """
-import numpy as np
 import pytest
 import torch
 
+from ppo_f64 import U, f64_reference, gamma
+
 pytestmark = pytest.mark.gpu
 
-U = 2.0 ** -24
-GAMMA = 2048 * U / (1 - 2048 * U)
-
-
-def _f64_reference(sd, arch, obs, act, old_logp, adv, ret, clip, vf_coef, normalize):
-    """SB3 PPO.train's minibatch loss in f64 with its gradient (SB3 names)
-    and the absolute-value envelope of every gradient entry."""
-    d = lambda x: torch.as_tensor(np.asarray(x), dtype=torch.float64)  # noqa: E731
-    W = {k: d(v).clone().requires_grad_(True) for k, v in sd.items()}
-    x = d(obs)
-    hs = {}
-    outs = {}
-    for net, head in (("policy_net", "action_net"), ("value_net", "value_net")):
-        h = x
-        lay = []
-        for k in range(len(arch)):
-            z = h @ W[f"mlp_extractor.{net}.{2 * k}.weight"].T + \
-                W[f"mlp_extractor.{net}.{2 * k}.bias"]
-            lay.append((h, z))
-            h = torch.tanh(z)
-            z.retain_grad()
-        hs[net] = (lay, h)
-        o = h @ W[f"{head}.weight"].T + W[f"{head}.bias"]
-        o.retain_grad()
-        outs[net] = o
-    mean, value = outs["policy_net"], outs["value_net"].flatten()
-    log_std = W["log_std"]
-    a = d(act)
-    z_std = (a - mean) / log_std.exp()
-    lp_dim = -0.5 * z_std ** 2 - log_std - 0.5 * np.log(2 * np.pi)
-    lp_dim.retain_grad()
-    log_prob = lp_dim.sum(1)
-    A = d(adv)
-    if normalize:
-        A = (A - A.mean()) / (A.std() + 1e-8)
-    ratio = torch.exp(log_prob - d(old_logp))
-    pol = -torch.min(A * ratio, A * torch.clamp(ratio, 1 - clip, 1 + clip)).mean()
-    vloss = torch.mean((d(ret) - value) ** 2)
-    loss = pol + vf_coef * vloss                 # ent_coef = 0 (SB3 default)
-    loss.backward()
-    g = {k: v.grad.detach().clone() for k, v in W.items()}
-    # envelope: the backward with |.| products (ent_coef = 0)
-    env = {}
-    for net, head in (("policy_net", "action_net"), ("value_net", "value_net")):
-        lay, htop = hs[net]
-        dout = outs[net].grad.detach().abs()                 # (M, 4) or (M, 1)
-        Wh = W[f"{head}.weight"].detach().abs()
-        env[f"{head}.weight"] = dout.T @ htop.detach().abs()
-        env[f"{head}.bias"] = dout.sum(0)
-        dh = dout @ Wh                                       # |dL/dh| envelope
-        for k in reversed(range(len(arch))):
-            h_in, z = lay[k]
-            th = torch.tanh(z.detach())
-            dz = dh * (1 - th ** 2).abs()
-            env[f"mlp_extractor.{net}.{2 * k}.weight"] = dz.T @ h_in.detach().abs()
-            env[f"mlp_extractor.{net}.{2 * k}.bias"] = dz.sum(0)
-            dh = dz @ W[f"mlp_extractor.{net}.{2 * k}.weight"].detach().abs()
-    # log_std: d lp_dim / d log_std = z^2 - 1 per row and dimension
-    env["log_std"] = (lp_dim.grad.detach() * (z_std.detach() ** 2 - 1)).abs().sum(0) + \
-        (lp_dim.grad.detach()).abs().sum(0)
-    return g, env
+GAMMA = gamma(2048)
 
 
 def test_train_one_minibatch_matches_f64_restatement_within_fp32_bounds():
@@ -116,7 +57,7 @@ def test_train_one_minibatch_matches_f64_restatement_within_fp32_bounds():
     g_gpu = {_sb3_name(name, 2): tr.fused.gview(name).detach().cpu().double() / c_gpu
              for name, _, _ in tr.policy.layout}
     sd1 = tr.policy.state_dict()
-    g_ref, env = _f64_reference(sd0, cfg.net_arch, obs, act, aux[:, 0], aux[:, 1], aux[:, 2],
+    g_ref, env = f64_reference(sd0, cfg.net_arch, obs, act, aux[:, 0], aux[:, 1], aux[:, 2],
                                 cfg.clip_range, cfg.vf_coef, cfg.normalize_advantage)
     # 1. gradient within the fp32 reduction-order bound, entrywise
     worst = 0.0
