@@ -197,8 +197,10 @@ def time_headline(args, n_envs, rank, world, device, steps, warmup, kmax):
     """The headline: `warmup` untimed then `steps` timed env steps of the
     batch through dr_rollout, in launches of at most kmax steps (actions
     pre-generated in HBM, outputs of every step written).  The timed launches
-    are one captured hipGraph (replayed once untimed first: its first launch
-    uploads it; the env simply runs those steps again on the same actions).
+    are one captured hipGraph when there are more than four of them
+    (replayed once untimed first: its first launch uploads it; the env simply
+    runs those steps again on the same actions), else direct C-ABI calls
+    with prebuilt arguments (repeated three times untimed first).
     Returns (wall seconds, GPU ms over the timed launches, launches, mean ep_num)."""
     import torch
     import torch.distributed as dist
@@ -227,14 +229,41 @@ def time_headline(args, n_envs, rank, world, device, steps, warmup, kmax):
         return n
     run(0, warmup)
     stream = torch.cuda.current_stream(device)
-    cs = torch.cuda.Stream(device)
-    cs.wait_stream(stream)
-    with torch.cuda.stream(cs):
-        g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g, stream=cs):
-            launches = run(warmup, total)
-    stream.wait_stream(cs)
-    g.replay()
+    launches = -(-steps // k0)
+    g = None
+    if launches > 4 and not args.no_graph:
+        # many launches: one graph replay instead of a host launch each
+        cs = torch.cuda.Stream(device)
+        cs.wait_stream(stream)
+        with torch.cuda.stream(cs):
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, stream=cs):
+                run(warmup, total)
+        stream.wait_stream(cs)
+        g.replay()
+        timed = g.replay
+    else:
+        # a few launches (the driver's --steps 20 is ONE): the C ABI called
+        # directly with prebuilt arguments (scripts/micro/launch_paths.py:
+        # 42.6 us host wall for one 20-step launch against 51.8 through a
+        # graph replay), after untimed repetitions of the same launches (the
+        # env simply runs those steps again on the same actions)
+        calls = []
+        t = warmup
+        while t < total:
+            k = min(k0, total - t)
+            calls.append((b.handle, k, acts[t].data_ptr(), obs.data_ptr(), rew.data_ptr(),
+                          done.data_ptr(), stream.cuda_stream))
+            t += k
+        fn = b.L.dr_rollout
+
+        rcs = []
+
+        def timed():
+            for c in calls:
+                rcs.append(fn(*c))
+        for _ in range(3):
+            timed()
     torch.cuda.synchronize(device)
     ev0 = torch.cuda.Event(enable_timing=True)
     ev1 = torch.cuda.Event(enable_timing=True)
@@ -243,13 +272,16 @@ def time_headline(args, n_envs, rank, world, device, steps, warmup, kmax):
     torch.cuda.synchronize(device)
     t0 = time.perf_counter()
     ev0.record(stream)
-    g.replay()
+    timed()
     ev1.record(stream)
     torch.cuda.synchronize(device)
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
     gpu_ms = ev0.elapsed_time(ev1)
+    if g is None and any(rcs):
+        from drone_rl_amd._lib import check
+        check(next(r for r in rcs if r), b.handle)
     if world > 1:
         t = torch.tensor([elapsed, gpu_ms], dtype=torch.float64, device=device)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -319,14 +351,20 @@ F32_MATRIX_PEAK_TFLOPS = 157.3     # MI355X f32 MFMA = f32 vector peak (spec)
 BF16_DENSE_PEAK_TFLOPS = 2500.0    # MI355X bf16 MFMA, dense (spec)
 
 
-def ppo_kernel_times(tr, reps=10):
+class _StopStep(Exception):
+    """Raised by the timing hook to end a fused step after its j-th kernel."""
+    pass
+
+
+def ppo_kernel_times(tr, reps=20):
     """Every kernel of one configs[2] optimizer step (one 65,536-row
     minibatch: gather, the fused forward / loss / backward, the deferred
-    finish + clip+Adam), enqueued eagerly `reps` times behind a spin kernel
-    that keeps the GPU busy while the host enqueues, with a HIP event on the
-    stream after each kernel: per-launch GPU time (kernel + its share of the
-    inter-kernel gap), averaged.  Runs after the timed region (it applies
-    `reps` more optimizer steps)."""
+    finish + clip+Adam) timed in the trainer's own launch conditions: for
+    j = 1 .. 9, `reps` repetitions of the step's first j kernels are captured
+    into a hipGraph (FusedTrainStep.mark stops the step after its j-th
+    kernel) and the replay is timed with HIP events on the stream; kernel j
+    takes T_j - T_(j-1) per repetition (its launch gap included).  Runs after
+    the timed region (it applies more optimizer steps)."""
     import torch
 
     from drone_rl_amd import ppo_kernels as K
@@ -337,18 +375,19 @@ def ppo_kernel_times(tr, reps=10):
     idx = tr.perm(seed=99, counter=0)[:M]
     stream = torch.cuda.current_stream(tr.device)
     sched = tr.opt.schedule(tr.opt.t + 1, 1).to(tr.device)
-    marks = []
+    names = []
 
-    def mark(name):
-        e = torch.cuda.Event(enable_timing=True)
-        e.record(stream)
-        marks.append((name, e))
-    torch.cuda.synchronize(tr.device)
-    torch.cuda._sleep(int(60e6))          # ~30 ms of spin: the host runs ahead
-    tr.fused.mark = mark
-    try:
-        mark("start")
-        for _ in range(reps):
+    def step_prefix(j):
+        seen = [0]
+
+        def mark(name):
+            if len(names) < 9 and name not in names:
+                names.append(name)
+            seen[0] += 1
+            if seen[0] == j:
+                raise _StopStep
+        tr.fused.mark = mark
+        try:
             K.gather_minibatch(idx, obs_flat, act_flat, tr.aux, tr.mb_obs, tr.mb_act,
                                tr.mb_aux, adv_part=tr.head.adv_part)
             mark("gather_minibatch")
@@ -356,13 +395,31 @@ def ppo_kernel_times(tr, reps=10):
                                     defer_finish=True)
             tr.opt.step_finish_sched(grad, tr.fused.finish, sched)
             mark("grad_finish_clip_adam")
-    finally:
-        tr.fused.mark = None
+        except _StopStep:
+            pass
+        finally:
+            tr.fused.mark = None
+
+    step_prefix(100)                     # eager once: the kernel order, lazy init
     torch.cuda.synchronize(tr.device)
-    acc = {}
-    for (_, e0), (name, e1) in zip(marks[:-1], marks[1:]):
-        acc[name] = acc.get(name, 0.0) + e0.elapsed_time(e1) * 1e3 / reps
-    return acc, (marks[-1][1], marks[0][1])
+    tj = [0.0]
+    for j in range(1, len(names) + 1):
+        cs = torch.cuda.Stream(tr.device)
+        cs.wait_stream(stream)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.stream(cs), torch.cuda.graph(g, stream=cs):
+            for _ in range(reps):
+                step_prefix(j)
+        stream.wait_stream(cs)
+        g.replay()                       # upload
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        g.replay()
+        e1.record(stream)
+        torch.cuda.synchronize(tr.device)
+        tj.append(e0.elapsed_time(e1) * 1e3 / reps)
+        del g
+    return {n: tj[i + 1] - tj[i] for i, n in enumerate(names)}
 
 
 def ppo_roofline(cfg, s_per_update, ktimes):
@@ -400,9 +457,7 @@ def ppo_roofline(cfg, s_per_update, ktimes):
            "basis": "fp32-equivalent FLOP per update (rollout forward 280,064 FLOP/sample + "
                     "3 x forward per sample and epoch, SURVEY.md 8d) / s_per_update, against "
                     "the f32 matrix peak",
-           "kernels_per_minibatch": kern,
-           "kernel_timing": "HIP events after each kernel of one optimizer step, eager, "
-                            "GPU kept busy ahead of the host; includes each launch's gap"}
+           "kernels_per_minibatch": kern}
     if x6 is not None:
         out["dominant_kernel"] = {"kernel": "gemm_x6_kernel (forward)", "bound": "mfma",
                                   "achieved": x6["bf16_mfma_tflops"],
@@ -475,8 +530,10 @@ def time_ppo(args, rank, world, device, force_dp=False, dp_graph=False, profile=
                       if world > 1 or tr.dp_collective else "none"},
            "last_update_stats": stats, "episodes": es}
     if profile and world == 1 and tr._train_fast() and not tr.dp_step:
-        kt, _ = ppo_kernel_times(tr)
-        res["roofline"] = ppo_roofline(cfg, el / K, kt)
+        res["roofline"] = ppo_roofline(cfg, el / K, ppo_kernel_times(tr))
+        res["roofline"]["kernel_timing"] = (
+            "per kernel of one optimizer step: graph replays of the step's first j kernels "
+            "x 20, timed by HIP events; kernel j = T_j - T_(j-1) (launch gap included)")
     tr.close()
     return res
 

@@ -1,0 +1,64 @@
+"""Host wall of ONE 20-step rollout-kernel launch at 65,536 envs (the driver's
+bench.py --steps 20 form) by launch path: graph replay, DroneBatch.rollout,
+and a raw ctypes call with prebuilt arguments.  Median of 200 trials, each
+bracketed by synchronize like bench.py's timed region."""
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
+import torch  # noqa: E402
+
+from drone_rl_amd import DroneBatch, random_actions  # noqa: E402
+from drone_rl_amd._lib import lib  # noqa: E402
+
+N, K = 65536, 20
+dev = torch.device("cuda", 0)
+b = DroneBatch(N, "gym", dtype=torch.float64, device=dev, seed=2025, auto_reset=True)
+b.reset()
+acts = torch.empty(K, N, 4, device=dev)
+for t in range(K):
+    random_actions(N, seed=7, step=t, out=acts[t])
+obs = torch.empty(K, N, 15, device=dev)
+rew = torch.empty(K, N, device=dev)
+done = torch.empty(K, N, dtype=torch.uint8, device=dev)
+st = torch.cuda.current_stream(dev)
+L = lib()
+fn = L.dr_rollout
+args = (b.handle, K, acts.data_ptr(), obs.data_ptr(), rew.data_ptr(), done.data_ptr(), st.cuda_stream)
+
+
+def py():
+    b.rollout(K, acts, obs_out=obs, rew_out=rew, done_out=done)
+
+
+def raw():
+    fn(*args)
+
+
+cs = torch.cuda.Stream(dev)
+cs.wait_stream(st)
+g = torch.cuda.CUDAGraph()
+with torch.cuda.stream(cs), torch.cuda.graph(g, stream=cs):
+    py()
+st.wait_stream(cs)
+res = {}
+for name, f in (("graph", g.replay), ("python", py), ("raw_ctypes", raw)):
+    for _ in range(20):
+        f()
+    torch.cuda.synchronize()
+    w, e = [], []
+    for _ in range(200):
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        t0 = time.perf_counter()
+        e0.record(st)
+        f()
+        e1.record(st)
+        torch.cuda.synchronize()
+        w.append(time.perf_counter() - t0)
+        e.append(e0.elapsed_time(e1) * 1e3)
+    w.sort()
+    e.sort()
+    res[name] = (round(w[100] * 1e6, 2), round(e[100], 2))
+print(res)

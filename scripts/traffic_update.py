@@ -1,0 +1,49 @@
+"""Per-launch HBM bytes of the headline rollout kernel from the PMC passes of
+scripts/rollout_traffic.sh, merged into profiles/traffic.json (read by
+bench.py for the headline's roofline.traffic).
+
+Bytes per launch = FETCH_SIZE x 2 (the gfx950 correction of
+MI355X_MICROARCH.md) + WRITE_SIZE, both KiB -> B, averaged over the
+env_rollout_kernel dispatches of each pass (the K-step launches only).
+Algorithmic bytes per launch = N x (K x 81 + 224)."""
+import csv
+import glob
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+N = 65536
+
+
+def avg(path, counter):
+    vals = []
+    for f in glob.glob(os.path.join(path, "**", "*counter_collection.csv"), recursive=True):
+        for r in csv.DictReader(open(f)):
+            if "env_rollout_kernel" in r["Kernel_Name"] and r["Counter_Name"] == counter:
+                vals.append(float(r["Counter_Value"]))
+    if not vals:
+        raise SystemExit(f"no {counter} rows under {path}")
+    return sum(vals) / len(vals), len(vals)
+
+
+def main():
+    out = sys.argv[1]
+    tj_path = os.path.join(ROOT, "profiles", "traffic.json")
+    tj = json.load(open(tj_path))
+    for k in (32, 20):
+        f, nf = avg(os.path.join(out, f"k{k}_FETCH_SIZE"), "FETCH_SIZE")
+        w, nw = avg(os.path.join(out, f"k{k}_WRITE_SIZE"), "WRITE_SIZE")
+        rd, wr = f * 2048, w * 1024
+        tj[f"rollout_f64_{N}_k{k}"] = {
+            "algorithmic_bytes_per_launch": N * (k * 81 + 224),
+            "hbm_bytes_per_launch": round(rd + wr), "read_bytes": round(rd),
+            "write_bytes": round(wr), "dispatches": [nf, nw],
+            "source": "scripts/rollout_traffic.sh (rocprofv3 --pmc FETCH_SIZE, WRITE_SIZE "
+                      "passes; FETCH_SIZE x2 gfx950 correction + WRITE_SIZE, KiB -> B)"}
+        print(k, json.dumps(tj[f"rollout_f64_{N}_k{k}"]))
+    json.dump(tj, open(tj_path, "w"), indent=1, sort_keys=True)
+
+
+if __name__ == "__main__":
+    main()
