@@ -37,6 +37,7 @@ The JSON line also carries
                 with the random policy drawn in the kernel.
 """
 import argparse
+import gc
 import json
 import os
 import sys
@@ -262,13 +263,18 @@ def time_headline(args, n_envs, rank, world, device, steps, warmup, kmax):
         def timed():
             for c in calls:
                 rcs.append(fn(*c))
-        for _ in range(3):
+        for _ in range(2):
             timed()
     torch.cuda.synchronize(device)
     ev0 = torch.cuda.Event(enable_timing=True)
     ev1 = torch.cuda.Event(enable_timing=True)
+    ev0.record(stream)          # the events' lazy creation stays out of the timed region
+    ev1.record(stream)
     if world > 1:
         dist.barrier()
+    if g is None:
+        timed()                 # the last untimed repetition right before the timed one
+    gc.disable()
     torch.cuda.synchronize(device)
     t0 = time.perf_counter()
     ev0.record(stream)
@@ -278,6 +284,7 @@ def time_headline(args, n_envs, rank, world, device, steps, warmup, kmax):
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    gc.enable()
     gpu_ms = ev0.elapsed_time(ev1)
     if g is None and any(rcs):
         from drone_rl_amd._lib import check

@@ -443,7 +443,8 @@ class PPOTrainer:
                 s = st.tolist()
                 logger({"update": self.num_updates, "timesteps": self.num_timesteps,
                         "fps": int(self.num_timesteps / (time.perf_counter() - t0)),
-                        **es, **dict(zip(K.PPOLoss.STATS, s))})
+                        **es, "eps_mean": float(self.env.get("eps").mean()),
+                        **dict(zip(K.PPOLoss.STATS, s))})
         return self
 
     # ------------------------------------------------------------ checkpoint

@@ -68,6 +68,7 @@ def run(steps=2_000_000, seed=0, n_steps=2048, batch=64, epochs=10, lr=3e-4, gam
     last_start = True
     ep_ret, ep_len = 0.0, 0
     ep_buf = deque(maxlen=100)
+    len_buf = deque(maxlen=100)
     hist = []
     t0 = time.perf_counter()
     done_steps = 0
@@ -91,6 +92,7 @@ def run(steps=2_000_000, seed=0, n_steps=2048, batch=64, epochs=10, lr=3e-4, gam
                 R[t] = r
                 if d:
                     ep_buf.append(float(ep_ret))
+                    len_buf.append(ep_len)
                     ep_ret, ep_len = 0.0, 0
                     obs = env.reset()
                 last_start = d
@@ -129,12 +131,13 @@ def run(steps=2_000_000, seed=0, n_steps=2048, batch=64, epochs=10, lr=3e-4, gam
         it += 1
         if it % log_every == 0 or done_steps >= steps:
             row = {"timesteps": done_steps, "ep_rew_mean": float(np.mean(ep_buf)) if ep_buf else None,
-                   "ep_len_mean": None, "eps": env.eps, "ep_num": env.ep_num,
+                   "ep_len_mean": float(np.mean(len_buf)) if len_buf else None,
+                   "eps": env.eps, "ep_num": env.ep_num,
                    "elapsed_s": round(time.perf_counter() - t0, 1)}
             hist.append(row)
             log(json.dumps(row))
     return {"seed": seed, "steps": done_steps, "final_ep_rew_mean": float(np.mean(ep_buf)),
-            "final_eps": env.eps, "episodes": env.ep_num, "history": hist,
+            "final_ep_len_mean": float(np.mean(len_buf)), "final_eps": env.eps, "episodes": env.ep_num, "history": hist,
             "elapsed_s": round(time.perf_counter() - t0, 1)}
 
 

@@ -43,22 +43,50 @@ with torch.cuda.stream(cs), torch.cuda.graph(g, stream=cs):
     py()
 st.wait_stream(cs)
 res = {}
-for name, f in (("graph", g.replay), ("python", py), ("raw_ctypes", raw)):
-    for _ in range(20):
-        f()
+
+
+def sync_dev():
     torch.cuda.synchronize()
-    w, e = [], []
-    for _ in range(200):
+
+
+def sync_ev_then_dev(e1):
+    e1.synchronize()
+    torch.cuda.synchronize()
+
+
+def trial(f, how):
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(st)
+    e1.record(st)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    e0.record(st)
+    f()
+    e1.record(st)
+    if how == "dev":
+        sync_dev()
+    else:
+        sync_ev_then_dev(e1)
+    return time.perf_counter() - t0, e0.elapsed_time(e1) * 1e3
+
+
+for name, f in (("graph", g.replay), ("python", py), ("raw_ctypes", raw)):
+    for how in ("dev", "ev"):
+        for _ in range(20):
+            f()
         torch.cuda.synchronize()
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        t0 = time.perf_counter()
-        e0.record(st)
-        f()
-        e1.record(st)
-        torch.cuda.synchronize()
-        w.append(time.perf_counter() - t0)
-        e.append(e0.elapsed_time(e1) * 1e3)
-    w.sort()
-    e.sort()
-    res[name] = (round(w[100] * 1e6, 2), round(e[100], 2))
-print(res)
+        time.sleep(0.5)                 # idle, then one single-shot trial
+        first = trial(f, how)
+        w, e = [], []
+        for _ in range(200):
+            a, b_ = trial(f, how)
+            w.append(a)
+            e.append(b_)
+        w.sort()
+        e.sort()
+        res[f"{name}/{how}"] = {"first": (round(first[0] * 1e6, 1), round(first[1], 1)),
+                                "median": (round(w[100] * 1e6, 1), round(e[100], 1)),
+                                "p10": round(w[20] * 1e6, 1), "p90": round(w[180] * 1e6, 1)}
+for k, v in res.items():
+    print(k, v)
