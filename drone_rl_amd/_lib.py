@@ -79,6 +79,7 @@ SIGNATURES = {
     "dr_reset_masked": (c_int, [_P, _P, _P, _P]),
     "dr_step": (c_int, [_P, _P, _P, _P, _P, _P, _P]),
     "dr_step_monitored": (c_int, [_P, _P, _P, _P, _P, _P, _P, _P, _P]),
+    "dr_step_monitored_trunc": (c_int, [_P] * 10),
     "dr_get_state": (c_int, [_P, c_int, _P, _P]),
     "dr_gather_state": (c_int, [_P, c_int, _P, c_int64, _P, _P]),
     "dr_set_state": (c_int, [_P, c_int, _P, _P]),

@@ -274,6 +274,9 @@ struct StepIO {
     float *ep_ret_out;
     int32_t *ep_len_out;
     int auto_reset;
+    // MON only, nullable: 1 where the episode ended at the step limit
+    // without a crash (the gymnasium TimeLimit "truncated" flag)
+    uint8_t *trunc_out;
 };
 
 // The five reset draws of env i starting episode `ep_new`, in the reference
@@ -788,6 +791,7 @@ __global__ __launch_bounds__(kEnvBlock) void env_step_kernel(EnvView<S> v,
     make_obs<S, OD>(st, ob, tvel);
 #endif
     if constexpr (MON) {
+        if (io.trunc_out && live) *at(io.trunc_out, i) = (uint8_t)(done && !crash);
         if (done) {               // VecMonitor: report, then restart counters
             *at(io.ep_ret_out, i) = ret;
             *at(io.ep_len_out, i) = len;
@@ -1197,7 +1201,8 @@ __global__ __launch_bounds__(kBlock) void env_step_quad_kernel(EnvView<S> v,
             if (d < (S)1) rw += (S)1;
         }
         step += 1;
-        const bool done = (pz < (S)0) || (pn > (S)50) || (step >= v.max_steps);
+        const bool crash = (pz < (S)0) || (pn > (S)50);
+        const bool done = crash || (step >= v.max_steps);
         const float rf = (float)rw;
         ob[0] = (float)p;
         ob[1] = (float)vel;
@@ -1269,6 +1274,7 @@ __global__ __launch_bounds__(kBlock) void env_step_quad_kernel(EnvView<S> v,
             io.rew[e] = rf;
             io.done[e] = (uint8_t)done;
             if constexpr (MON) {
+                if (io.trunc_out) io.trunc_out[e] = (uint8_t)(done && !crash);
                 if (done) {
                     io.ep_ret_out[e] = ret;
                     io.ep_len_out[e] = len;
@@ -1788,7 +1794,7 @@ int dr_reset_masked(dr_handle *h, const uint8_t *mask, float *obs_out, void *str
 static int step_common(dr_handle *h, const float *actions, float *obs_out,
                        float *rew_out, uint8_t *done_out, float *term_obs_out,
                        float *ep_ret_out, int32_t *ep_len_out, bool mon,
-                       void *stream) {
+                       void *stream, uint8_t *trunc_out = nullptr) {
     if (!h) return fail(nullptr, DR_ERR_INVALID, "dr_step: null handle");
     if (!actions || !obs_out || !rew_out || !done_out)
         return fail(h, DR_ERR_INVALID, "dr_step: actions/obs/rew/done must be non-null");
@@ -1801,7 +1807,7 @@ static int step_common(dr_handle *h, const float *actions, float *obs_out,
         if (rc) return rc;
     }
     StepIO io{actions, obs_out, rew_out, done_out, term_obs_out, ep_ret_out,
-              ep_len_out, h->cfg.auto_reset};
+              ep_len_out, h->cfg.auto_reset, trunc_out};
     DeviceGuard g(h->cfg.device);
     return mon ? dispatch_step<true>(h, io, as_stream(stream))
                : dispatch_step<false>(h, io, as_stream(stream));
@@ -1818,6 +1824,16 @@ int dr_step_monitored(dr_handle *h, const float *actions, float *obs_out,
                       float *ep_return_out, int32_t *ep_length_out, void *stream) {
     return step_common(h, actions, obs_out, rew_out, done_out, terminal_obs_out,
                        ep_return_out, ep_length_out, true, stream);
+}
+
+int dr_step_monitored_trunc(dr_handle *h, const float *actions, float *obs_out,
+                            float *rew_out, uint8_t *done_out, float *terminal_obs_out,
+                            float *ep_return_out, int32_t *ep_length_out,
+                            uint8_t *truncated_out, void *stream) {
+    if (!truncated_out)
+        return fail(h, DR_ERR_INVALID, "dr_step_monitored_trunc: truncated_out is null");
+    return step_common(h, actions, obs_out, rew_out, done_out, terminal_obs_out,
+                       ep_return_out, ep_length_out, true, stream, truncated_out);
 }
 
 static int rollout_common(dr_handle *h, int32_t k, RolloutIO io, bool gen, void *stream) {

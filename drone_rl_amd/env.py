@@ -125,10 +125,13 @@ class DroneBatch:
                                      _stream(self.device)), self.handle)
         return out
 
-    def step(self, actions: torch.Tensor, obs_out=None, rew_out=None, done_out=None):
+    def step(self, actions: torch.Tensor, obs_out=None, rew_out=None, done_out=None,
+             trunc_out=None):
         """Advance every env one step.  `actions` (N,4) f32 on the device.
         Returns (obs, rew, done) device tensors (the batch's own buffers unless
-        *_out are given: copy them before the next step if you keep them)."""
+        *_out are given: copy them before the next step if you keep them).
+        `trunc_out` (N,) u8, monitor=True only: 1 where the episode ended at
+        the step limit without a crash (dr_step_monitored_trunc)."""
         obs = self.obs if obs_out is None else obs_out
         rew = self.rew if rew_out is None else rew_out
         done = self.done if done_out is None else done_out
@@ -142,7 +145,15 @@ class DroneBatch:
         self._check_out(rew, (self.num_envs,), torch.float32)
         self._check_out(done, (self.num_envs,), torch.uint8)
         s = _stream(self.device)
-        if self.monitor:
+        if trunc_out is not None:
+            if not self.monitor:
+                raise ValueError("trunc_out needs a monitor=True batch")
+            self._check_out(trunc_out, (self.num_envs,), torch.uint8)
+            check(self.L.dr_step_monitored_trunc(self.handle, ptr(a), ptr(obs), ptr(rew),
+                                                 ptr(done), ptr(self.term_obs), ptr(self.ep_ret),
+                                                 ptr(self.ep_len), ptr(trunc_out), s),
+                  self.handle)
+        elif self.monitor:
             check(self.L.dr_step_monitored(self.handle, ptr(a), ptr(obs), ptr(rew), ptr(done),
                                            ptr(self.term_obs), ptr(self.ep_ret),
                                            ptr(self.ep_len), s), self.handle)
@@ -435,10 +446,12 @@ class DroneGymEnv:
         """Finish and save the recording."""
         self._recorder().stop_record()
 
-    def render(self, ax=None):
-        """Draw the drone (motors, arms, centre) and the target in 3-D from
-        the device state; grabs a frame when recording.  Returns the (4, 3)
-        motor positions drawn."""
+    def render(self, mode="human", close=False, ax=None):
+        """DroneGymEnv.render(mode="human", close=False) (drone.py:273-274):
+        draw the drone (motors, arms, centre) and the target in 3-D from the
+        device state; grabs a frame when recording.  `mode` and `close` are
+        accepted as the reference accepts them (it ignores both); `ax` is this
+        build's optional target axes.  Returns the (4, 3) motor positions."""
         return self._recorder().render(self.pos, self.euler, self.target, self.arm_length, ax)
 
     def close(self):

@@ -16,9 +16,11 @@ with a loop whose every byte stays in HBM:
                       hipGraph replay on one GPU
 
 SB3-parity choices (documented deviations in DESIGN.md):
-  * no value bootstrap at the 200-step limit (the reference's env is wrapped
-    by shimmy's GymV21 compat, so SB3 sees terminated=True, not truncated);
-    `bootstrap_timeouts=True` is not offered yet;
+  * no value bootstrap at the 200-step limit by default (the reference's env
+    is wrapped by shimmy's GymV21 compat, so SB3 sees terminated=True, not
+    truncated); `bootstrap_timeouts=True` opts into SB3's TimeLimit handling
+    (rewards[t] += gamma * V(terminal obs) where the episode hit the limit
+    without crashing, OnPolicyAlgorithm.collect_rollouts);
   * advantages normalised per minibatch (mean, unbiased std + 1e-8);
   * the flat rollout index is t*N + n (SB3 uses n*T + t after
     swap_and_flatten; a uniformly random permutation makes the two
@@ -83,6 +85,10 @@ class PPOConfig:
     # Off by default: graph capture of RCCL collectives has only been run
     # on a one-rank group here (no multi-GPU box for the builder)
     dp_graph: bool = False
+    # SB3's timeout bootstrap for envs that report TimeLimit truncation: at
+    # the 200-step limit (drone.py:155-157, no crash) add gamma * V(terminal
+    # obs) to that step's reward.  Off = the reference's semantics
+    bootstrap_timeouts: bool = False
 
     @classmethod
     def sb3_defaults(cls, **kw):
@@ -111,6 +117,7 @@ class PPOTrainer:
         self.tuned_gemms = use_tuned_gemms() if cfg.tuned_gemms else False
         self.env = DroneBatch(N, cfg.variant, device=dev, seed=cfg.seed,
                               env_id_offset=D.env_shard(rank, N)[0], monitor=True,
+                              keep_terminal_obs=cfg.bootstrap_timeouts,
                               dtype=torch.float64 if cfg.state_dtype == "f64" else torch.float32)
         if cfg.initial_eps:
             self.env.set("eps", torch.full((N,), float(cfg.initial_eps), dtype=torch.float64))
@@ -118,6 +125,12 @@ class PPOTrainer:
         # every rank starts from the same parameters (the seed is shared);
         # with world > 1 rank 0's copy is also broadcast (sync_params)
         self.policy = ActorCritic(od, 4, cfg.net_arch, dev, cfg.log_std_init, cfg.seed)
+        # one GEMM path for the rollout forward (N rows) AND the training
+        # forward (M rows): dr_gemm_x6 needs a multiple of 128 rows, and if
+        # only one of the two qualified the first epoch's ratio would no
+        # longer be exactly 1 (PolicyInference's guarantee)
+        if N % 128 or cfg.batch_size % 128:
+            self.policy.gemm_x6 = False
         self.opt = K.ClipAdam(self.policy.flat.data, cfg.learning_rate, eps=1e-5,
                               max_grad_norm=cfg.max_grad_norm)
         f32 = dict(dtype=torch.float32, device=dev)
@@ -133,6 +146,9 @@ class PPOTrainer:
         self.adv = torch.zeros(T, N, **f32)
         self.ret = torch.zeros(T, N, **f32)
         self.aux = torch.zeros(T * N, 3, **f32)                 # (old logp, adv, return)
+        # bootstrap_timeouts: per-step truncation flags (dr_step_monitored_trunc)
+        self.trunc = torch.zeros(T, N, dtype=torch.uint8, device=dev) \
+            if cfg.bootstrap_timeouts else None
         M = cfg.batch_size
         self.perm = K.Permuter(T * N, dev)
         self.mb_obs = torch.zeros(M, od, **f32)
@@ -252,7 +268,14 @@ class PPOTrainer:
             self.env.ep_ret = self.ep_ret[t]
             self.env.ep_len = self.ep_len[t]
             self.env.step(self.act_env, obs_out=self.obs[t + 1], rew_out=self.rewards[t],
-                          done_out=self.dones[t + 1])
+                          done_out=self.dones[t + 1],
+                          trunc_out=None if self.trunc is None else self.trunc[t])
+            if self.trunc is not None:
+                # SB3 collect_rollouts: rewards[idx] += gamma * V(terminal
+                # obs) for envs whose episode was truncated at the limit
+                _, v_term = fwd(self.env.term_obs)
+                self.rewards[t].add_(torch.where(self.trunc[t].bool(),
+                                                 v_term * self.cfg.gamma, 0.0))
             if self.trajectory is not None:
                 self.trajectory.on_step(self.dones[t + 1])
 

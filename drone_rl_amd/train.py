@@ -31,6 +31,23 @@ def checkpoint_path(path: str, rank: int, world: int) -> str:
     return f"{root}.rank{rank}{ext}"
 
 
+def resume_path(path: str, rank: int, world: int) -> str | None:
+    """The per-rank file to resume from: checkpoint_path(), or a file under
+    the name earlier versions wrote ('<checkpoint>.rank<r>', the extension
+    before the suffix), which is then used with a warning; None if neither
+    exists."""
+    ck = checkpoint_path(path, rank, world)
+    if os.path.exists(ck):
+        return ck
+    legacy = f"{path}.rank{rank}" if world > 1 else None
+    if legacy and os.path.exists(legacy):
+        import warnings
+        warnings.warn(f"resuming from the legacy per-rank checkpoint name {legacy!r}; "
+                      f"new checkpoints are written to {ck!r}")
+        return legacy
+    return None
+
+
 def main(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--envs", type=int, default=65536, help="envs per GPU")
@@ -39,6 +56,8 @@ def main(argv=None):
     ap.add_argument("--batch-size", type=int, default=65536)
     ap.add_argument("--epochs", type=int, default=10)
     ap.add_argument("--lr", type=float, default=3e-4)
+    ap.add_argument("--ent-coef", type=float, default=0.0,
+                    help="entropy coefficient (SB3 default 0.0)")
     ap.add_argument("--net", type=int, nargs="+", default=[256, 256])
     ap.add_argument("--state-dtype", choices=["f64", "f32"], default="f64")
     ap.add_argument("--seed", type=int, default=0)
@@ -58,6 +77,10 @@ def main(argv=None):
     ap.add_argument("--grad-buckets", type=int, choices=[1, 2], default=1,
                     help="data parallel: 1 = one gradient all-reduce per optimizer step; "
                          "2 = an early bucket overlapped with the first-layer backward")
+    ap.add_argument("--bootstrap-timeouts", action="store_true",
+                    help="SB3 TimeLimit handling: bootstrap V(terminal obs) into the reward "
+                         "of steps that end an episode at the 200-step limit without a "
+                         "crash (off = the reference's semantics)")
     ap.add_argument("--reset-num-timesteps", action=argparse.BooleanOptionalAction,
                     default=True,
                     help="after a resume, train --total-steps more (SB3's default, the "
@@ -70,8 +93,10 @@ def main(argv=None):
     torch.cuda.set_device(local)
     if world > 1:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    common = dict(num_envs=a.envs, learning_rate=a.lr, seed=a.seed, grad_buckets=a.grad_buckets,
+    common = dict(num_envs=a.envs, learning_rate=a.lr, ent_coef=a.ent_coef, seed=a.seed,
+                  grad_buckets=a.grad_buckets,
                   state_dtype=a.state_dtype, variant=a.variant, initial_eps=a.initial_eps,
+                  bootstrap_timeouts=a.bootstrap_timeouts,
                   eps_schedule=tuple((int(u), float(e)) for u, e in
                                      (kv.split(":") for kv in a.eps_schedule.split(",") if kv)))
     if a.sb3_defaults:
@@ -84,14 +109,15 @@ def main(argv=None):
         from .trajectory import TrajectoryRecorder
         tr.trajectory = TrajectoryRecorder(tr.env, out_dir=a.traj_dir)
     ck = checkpoint_path(a.checkpoint, rank, world)
+    src = resume_path(a.checkpoint, rank, world)
     # *.zip = stable-baselines3 PPO checkpoint (the reference's dd.zip,
     # train.py:10-31 / 70); anything else = this trainer's bit-exact resume file
     sb3 = a.checkpoint.endswith(".zip")
     total = int(a.total_steps)
-    if os.path.exists(ck):
-        tr.load_sb3(ck) if sb3 else tr.load(ck)
+    if src is not None:
+        tr.load_sb3(src) if sb3 else tr.load(src)
         if rank == 0:
-            print(json.dumps({"resumed": ck, "num_timesteps": tr.num_timesteps}), flush=True)
+            print(json.dumps({"resumed": src, "num_timesteps": tr.num_timesteps}), flush=True)
         if a.reset_num_timesteps:
             # SB3 learn(reset_num_timesteps=True), the reference's call
             # (train.py:63-68): every run trains --total-steps more steps and

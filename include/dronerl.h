@@ -164,6 +164,17 @@ int dr_step_monitored(dr_handle *h, const float *actions, float *obs_out,
                       float *terminal_obs_out, float *ep_return_out,
                       int32_t *ep_length_out, void *stream);
 
+/* dr_step_monitored plus the gymnasium TimeLimit split: truncated_out (N) u8
+   (non-null) gets 1 where the episode ended at the step limit without a
+   crash (drone.py:155-157 vs 154), 0 elsewhere.  The reference's env reports
+   both as terminated (SB3 sees it through shimmy's GymV21 compatibility), so
+   only PPOConfig.bootstrap_timeouts uses it: SB3's rewards[i] += gamma *
+   V(terminal_obs[i]) for truncated envs.  (ABI v12.) */
+int dr_step_monitored_trunc(dr_handle *h, const float *actions, float *obs_out,
+                            float *rew_out, uint8_t *done_out, float *terminal_obs_out,
+                            float *ep_return_out, int32_t *ep_length_out,
+                            uint8_t *truncated_out, void *stream);
+
 /* Device-side state access (parity injection, checkpointing, get_attr). */
 int dr_get_state(dr_handle *h, int field, void *out, void *stream);
 /* dr_get_state for k selected envs: out row j = field of env env_ids[j]

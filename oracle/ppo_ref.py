@@ -11,6 +11,8 @@ Reference call sites: /root/reference/train.py:36-43 (PPO defaults),
   ppo_loss_torch   PPO.train's loss expression on CPU, with autograd grads
                    w.r.t. (mean, log_std, values)
   clip_adam_torch  clip_grad_norm_(max_norm) + torch.optim.Adam step
+  timeout_bootstrap_numpy  OnPolicyAlgorithm.collect_rollouts' TimeLimit
+                   bootstrap (rewards[idx] += gamma * terminal_value)
 """
 import numpy as np
 import torch
@@ -32,6 +34,18 @@ def gae_numpy(rewards, values, episode_starts, last_values, dones, gamma, lam):
         last = delta + gamma * lam * nnt * last
         adv[step] = last
     return adv, adv + values
+
+
+def timeout_bootstrap_numpy(rewards, truncated, terminal_values, gamma):
+    """SB3 OnPolicyAlgorithm.collect_rollouts: for every env whose step ended
+    an episode by TimeLimit truncation (a terminal_observation and
+    TimeLimit.truncated in its info), rewards[idx] += gamma * V(terminal obs).
+    rewards (N,) f32, truncated (N,) bool, terminal_values (N,) f32; gamma a
+    python float multiplied into the f32 value tensor, as SB3 does."""
+    r = np.array(rewards, dtype=np.float32, copy=True)
+    tv = (np.float32(gamma) * np.asarray(terminal_values, np.float32)).astype(np.float32)
+    r[np.asarray(truncated, bool)] += tv[np.asarray(truncated, bool)]
+    return r
 
 
 def ppo_loss_torch(mean, log_std, values, actions, old_logp, adv, returns,

@@ -94,3 +94,24 @@ def _worker(rank, world, port):
 
 def test_dp_gloo_world2():
     mp.spawn(_worker, args=(2, _free_port()), nprocs=2, join=True)
+
+
+def test_resume_finds_the_legacy_per_rank_checkpoint(tmp_path):
+    """advisor r02: per-rank checkpoints are '<root>.rank<r><ext>'; a file
+    under the earlier '<checkpoint>.rank<r>' name is still resumed from
+    (with a warning) instead of silently starting over."""
+    import warnings
+
+    from drone_rl_amd.train import checkpoint_path, resume_path
+    ck = str(tmp_path / "dd.pt")
+    assert checkpoint_path(ck, 1, 2) == str(tmp_path / "dd.rank1.pt")
+    assert resume_path(ck, 1, 2) is None
+    legacy = tmp_path / "dd.pt.rank1"
+    legacy.write_bytes(b"x")
+    with warnings.catch_warnings(record=True) as w:
+        warnings.simplefilter("always")
+        assert resume_path(ck, 1, 2) == str(legacy)
+    assert any("legacy" in str(x.message) for x in w)
+    (tmp_path / "dd.rank1.pt").write_bytes(b"y")
+    assert resume_path(ck, 1, 2) == str(tmp_path / "dd.rank1.pt")
+    assert resume_path(ck, 0, 1) is None

@@ -246,3 +246,21 @@ def test_rollout_graph_is_bitwise_eager(cfg):
     assert torch.equal(a.env.get("ep_num"), b.env.get("ep_num"))
     a.close()
     b.close()
+
+
+@pytest.mark.parametrize("num_envs", [1000, 1024])
+def test_rollout_and_first_epoch_share_one_gemm_path(num_envs):
+    """advisor r02: the 256x256 layer's GEMM path is chosen once per trainer
+    (dr_gemm_x6 only when the rollout's N rows AND the minibatch's M rows are
+    multiples of 128), so the first epoch's ratio is exactly 1: with one
+    epoch of one minibatch, approx_kl and clip_fraction are exactly 0."""
+    from drone_rl_amd.ppo import PPOConfig, PPOTrainer
+    cfg = PPOConfig(num_envs=num_envs, n_steps=32, batch_size=num_envs * 32, n_epochs=1,
+                    seed=6)
+    tr = PPOTrainer(cfg)
+    assert tr.policy.gemm_x6 == (num_envs % 128 == 0)
+    tr.collect_rollouts()
+    st = dict(zip(("loss", "policy_loss", "value_loss", "entropy_loss", "clip_fraction",
+                   "approx_kl"), tr.train().tolist()))
+    assert st["approx_kl"] == 0.0 and st["clip_fraction"] == 0.0, st
+    tr.close()

@@ -62,3 +62,19 @@ def test_eval_gif_like_reference_test_py(tmp_path):
     assert r["frames"] == 6 and np.isfinite(r["return"])
     im = PIL.open(out)
     assert im.format == "GIF" and im.n_frames == 6
+
+
+@pytest.mark.gpu
+def test_gym_render_keeps_the_reference_signature():
+    """advisor r02: DroneGymEnv.render(mode="human", close=False) as the
+    reference declares it (drone.py:273); callers passing a mode still draw."""
+    import matplotlib
+    matplotlib.use("Agg")
+    from drone_rl_amd import DroneGymEnv
+    env = DroneGymEnv()
+    env.reset()
+    for args, kw in (((), {}), (("human",), {}), (("rgb_array", False), {}),
+                     ((), {"mode": "human", "close": False})):
+        m = env.render(*args, **kw)
+        assert np.asarray(m).shape == (4, 3)
+    env.close()
