@@ -1,16 +1,18 @@
 #!/bin/bash
 # configs[2] PPO on the GYM variant (65,536 envs, 2x256, T=32, minibatches of
 # 65,536) with a staged curriculum: eps 0 (target (0,0,1)) until update
-# START, then +0.05 every EVERY updates up to eps 1.0, then held (drone.py:
+# START, then +INC every EVERY updates for STAGES stages (default 0.05 x 20:
+# up to eps 1.0), then held (drone.py:
 # 68-73's per-env bump keeps running on top; it never fires at a few hundred
 # episodes per env).  JSON lines every 10 updates, one log per seed.
-#   START EVERY UPDATES EPOCHS ENT TAG SEEDS: environment overrides
+#   START EVERY INC STAGES UPDATES EPOCHS ENT EVAL_EPS TAG SEEDS: environment
+#   overrides
 cd "$(dirname "$0")/.."
 mkdir -p gpurun_out
 START=${START:-300}; EVERY=${EVERY:-20}; UPDATES=${UPDATES:-800}; EPOCHS=${EPOCHS:-10}
-ENT=${ENT:-0.0}
+ENT=${ENT:-0.0}; INC=${INC:-0.05}; STAGES=${STAGES:-20}
 TAG=${TAG:-r03_ppo_c3_staged}
-SCHED=$(python3 -c "print(','.join(f'{$START + $EVERY * i}:{0.05 * (i + 1):.2f}' for i in range(20)))")
+SCHED=$(python3 -c "print(','.join(f'{$START + $EVERY * i}:{$INC * (i + 1):.2f}' for i in range($STAGES)))")
 STEPS=$((UPDATES * 2097152))
 for SEED in ${SEEDS:-0 1 2}; do
   timeout -k 10 600 python -u -m drone_rl_amd.train --eps-schedule "$SCHED" \
