@@ -44,7 +44,8 @@ constexpr double kDt = 0.02;
 // DR_ABLATE (diagnostic builds only, scripts/micro/ablate.sh; never set in
 // the product build): 1 = f32 trig, 2 = no auto-reset, 3 = no LDS obs
 // staging, 4 = divides by reciprocal multiplies, 5 = constant reset draws,
-// 6 = no physics.
+// 6 = no physics, 7 = rollout kernel without its obs stores, 8 = rollout
+// kernel without the auto-reset.
 #ifndef DR_ABLATE
 #define DR_ABLATE 0
 #endif
@@ -953,7 +954,7 @@ __global__ __launch_bounds__(kEnvBlock) void env_rollout_kernel(EnvView<S> v, Ro
             st_out(at(io.done + row, i), (uint8_t)done);
         }
         if constexpr (GYMLIKE) {
-            if (done && io.auto_reset) {
+            if (done && io.auto_reset && DR_ABLATE != 8) {
                 step = 0;
                 reset_any = true;
                 if constexpr (VAR == DR_VARIANT_GYM) {
@@ -977,7 +978,10 @@ __global__ __launch_bounds__(kEnvBlock) void env_rollout_kernel(EnvView<S> v, Ro
         }
         // (plain stores for these outputs measured the same: 60.2 / 62.2 us
         // per 32-step launch at 65,536 envs)
-        store_obs_wave<OD, RPW>(reinterpret_cast<float *>(sh4), ob, io.obs + row * OD, n_);
+        if (DR_ABLATE != 7)
+            store_obs_wave<OD, RPW>(reinterpret_cast<float *>(sh4), ob, io.obs + row * OD, n_);
+        else
+            asm volatile("" ::"v"(ob[0]), "v"(ob[5]), "v"(ob[14 % OD]));
     };
 
     if constexpr (GEN) {

@@ -28,7 +28,9 @@ class _Tap:
 
     def on_step(self, dones):
         t = self.t
-        self.rows.append((self.tr.env.term_obs.clone(), self.tr.ep_len[t].clone(),
+        term = self.tr.env.term_obs
+        self.rows.append((term.clone() if term is not None else None,
+                          self.tr.ep_len[t].clone(),
                           self.tr.trunc[t].clone() if self.tr.trunc is not None else None))
         self.t += 1
 
