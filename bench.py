@@ -367,7 +367,7 @@ def ppo_kernel_times(tr, reps=20):
     """Every kernel of one configs[2] optimizer step (one 65,536-row
     minibatch: gather, the fused forward / loss / backward, the deferred
     finish + clip+Adam) timed in the trainer's own launch conditions: for
-    j = 1 .. 9, `reps` repetitions of the step's first j kernels are captured
+    j = 1 .. (number of kernels), `reps` repetitions of the step's first j kernels are captured
     into a hipGraph (FusedTrainStep.mark stops the step after its j-th
     kernel) and the replay is timed with HIP events on the stream; kernel j
     takes T_j - T_(j-1) per repetition (its launch gap included).  Runs after
@@ -384,11 +384,11 @@ def ppo_kernel_times(tr, reps=20):
     sched = tr.opt.schedule(tr.opt.t + 1, 1).to(tr.device)
     names = []
 
-    def step_prefix(j):
+    def step_prefix(j, record=False):
         seen = [0]
 
         def mark(name):
-            if len(names) < 9 and name not in names:
+            if record and name not in names:
                 names.append(name)
             seen[0] += 1
             if seen[0] == j:
@@ -407,7 +407,7 @@ def ppo_kernel_times(tr, reps=20):
         finally:
             tr.fused.mark = None
 
-    step_prefix(100)                     # eager once: the kernel order, lazy init
+    step_prefix(100, record=True)        # eager once: the kernel order, lazy init
     torch.cuda.synchronize(tr.device)
     tj = [0.0]
     for j in range(1, len(names) + 1):
@@ -440,6 +440,7 @@ def ppo_roofline(cfg, s_per_update, ktimes):
     gemm_flop = 2 * 2 * M * 256 * 256            # both nets, one fp32 GEMM
     rows = {"gather_minibatch": 2 * (15 + 4 + 3) * 4,
             "linear_tanh": 15 * 4 + 2 * 256 * 4,
+            "pack_first": 15 * 4 + 16 * 4,
             "ppo_head": 2 * 1024 + 2 * 1024 + 44,
             "first_layer_bwd": 2 * 2 * 1024 + 60}
     kern = {}

@@ -89,6 +89,15 @@ namespace {
 // 1: raise the wave's issue priority around its MFMA cluster; 2: static
 // s_setprio 1 for waves 4-7 (the arbitration losers) before the loop
 // (A/B knob)
+// DR_X6_NOCOMP (diagnostic, wrong by construction): L1 without forming A
+#ifndef DR_X6_NOCOMP
+#define DR_X6_NOCOMP 0
+#endif
+// 1: in the first-layer-fused form the SIMD partners form the next A stage on
+// either side of their MFMAs (see the L1 loop); 0: both before
+#ifndef DR_X6_L1_SPLIT
+#define DR_X6_L1_SPLIT 1
+#endif
 #ifndef DR_X6_PRIO
 #define DR_X6_PRIO 0
 #endif
@@ -210,6 +219,12 @@ constexpr int A32_STAGE = XBM * XBK * 4;             // 16 KB
 constexpr int LDS_WB = 0;
 constexpr int LDS_A32 = 2 * B_STAGE;
 constexpr int LDS_TOTAL = 2 * B_STAGE + 3 * A32_STAGE;
+// First-layer-fused form (L1): the A stages are computed in the kernel, two
+// stages ahead into a 2-stage ring, from the tile's observation rows (16
+// floats per row, the 16th zero), staged per tile by LDS-DMA into a 2-tile
+// ring after it: 96 + 32 + 16 = 144 KB.
+constexpr int OBS_TILE = XBM * 16 * 4;               // 8 KB
+constexpr int LDS_OBS = 2 * B_STAGE + 2 * A32_STAGE;
 
 // global_load_lds_dwordx4 by inline asm: lane l's 16 bytes land at LDS
 // byte lds_base + 16 l.  Issued by hand because hipcc's waitcnt pass drains
@@ -237,11 +252,22 @@ __device__ inline int swz32(int row, int chunk) {
 // the f32 A fragments it reads from LDS into the three bf16 planes in
 // registers, right before its MFMAs.  Waits are counted by hand (vmcnt
 // retires in issue order), with a raw s_barrier per stage.
-__global__ __launch_bounds__(XTHREADS) void gemm_x6_kernel(const float *__restrict__ A,
-                                                           const uint8_t *__restrict__ img,
-                                                           float *__restrict__ C, int64_t m,
-                                                           int ntiles, int nt) {
+// L1 (first-layer fusion): A = tanh(obs W0^T + b0) is not read but formed
+// here, with linear_tanh_kernel's exact arithmetic (acc = 0, fmaf over the 15
+// inputs in order, + bias, tanh_fast), so the result is bitwise that of
+// dr_linear_tanh2 followed by dr_gemm_x6; it is also written to h1 when
+// non-null (the weight gradient and the first-layer backward read it).
+//   l1_obs16 (m, 16) rows: the 15 observations, then 0
+//   l1_w0p   (batch, 256, 16): W0 row k (15 floats), then b0[k] (restrict:
+//            read-only in the kernel, so its wave-uniform loads are scalar)
+//   l1_h1    (batch, m, 256) side output, nullable
+template <bool L1>
+__global__ __launch_bounds__(XTHREADS) void gemm_x6_kernel(
+    const float *__restrict__ A, const uint8_t *__restrict__ img, float *__restrict__ C,
+    int64_t m, int ntiles, int nt, const float *__restrict__ l1_obs16,
+    const float *__restrict__ l1_w0p, float *__restrict__ l1_h1) {
     __shared__ __attribute__((aligned(16))) uint8_t sh[LDS_TOTAL];
+    constexpr int NA = L1 ? 2 : 3;          // A-stage ring depth
     const int tid = threadIdx.x, lane = tid & 63;
     const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int wm = XWAVES == 8 ? wid >> 2 : 0, wn = wid & 3;
@@ -267,13 +293,76 @@ __global__ __launch_bounds__(XTHREADS) void gemm_x6_kernel(const float *__restri
         const int t = tile_of(g), b = net_of(t);
         const float *src = A + ((int64_t)b * m + (int64_t)(t - b * tiles_per_net) * XBM) * XK +
                            (g & 7) * XBK;
-        uint8_t *dst = sh + LDS_A32 + (g % 3) * A32_STAGE;
+        uint8_t *dst = sh + LDS_A32 + (g % NA) * A32_STAGE;
 #pragma unroll
         for (int i = 0; i < A32_STAGE / 1024 / XWAVES; ++i) {
             const int ins = wid + XWAVES * i;
             const int row = ins * 8 + a_row_l;
             const int chunk = a_chk_l ^ ((row >> 1) & 7);
             glds16(src + (int64_t)row * XK + chunk * 4, lds_addr(dst + ins * 1024));
+        }
+    };
+
+    // L1: the observation rows of a tile (128 x 64 B) by LDS-DMA, one 1-KB
+    // wave-instruction per wave into obs buffer j & 1 for the block's j-th
+    // tile; lane L fills the 16-B slot (row L >> 2, chunk L & 3) with global
+    // chunk (L & 3) ^ (row & 3) of that row (the reads below are then
+    // conflict-free: 16 consecutive rows hit 16 distinct bank quads)
+    auto issue_obs = [&](int j) {
+        const int t = (int)blockIdx.x + j * (int)gridDim.x, b = net_of(t);
+        const int row = wid * 16 + (lane >> 2), chunk = (lane & 3) ^ (row & 3);
+        const float *src = l1_obs16 + ((int64_t)(t - b * tiles_per_net) * XBM + row) * 16 +
+                           chunk * 4;
+        glds16(src, lds_addr(sh + LDS_OBS + (j & 1) * OBS_TILE + wid * 1024));
+    };
+    // L1: stage s of A = tanh(obs W0^T + b0): wave w forms the 4 columns
+    // k = 32 (s & 7) + 4 w .. + 3 (weights wave-uniform: scalar loads) of
+    // tile rows lane and lane + 64; each row's 4 values are one 16-B LDS
+    // chunk of the A stage (and one 16-B store of h1)
+    auto compute_a = [&](int s_) {
+        const int t = tile_of(s_), b = net_of(t), j = s_ >> 3;
+        const int k0 = (s_ & 7) * XBK + 4 * wid;
+        const float *obs_t = reinterpret_cast<const float *>(sh + LDS_OBS + (j & 1) * OBS_TILE);
+        uint8_t *dst = sh + LDS_A32 + (s_ % NA) * A32_STAGE;
+        const float *wq = l1_w0p + ((int64_t)b * XN + k0) * 16;
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const int r = lane + 64 * h;
+            // two columns at a time (their 32 weights in SGPRs), the 15
+            // inputs one 16-B LDS chunk at a time; each column keeps
+            // linear_tanh's fmaf order i = 0 .. 14
+            float o[4];
+#pragma unroll
+            for (int qp = 0; qp < 4; qp += 2) {
+                float acc[2] = {0.f, 0.f};
+#pragma unroll
+                for (int c = 0; c < 4; ++c) {
+                    const float4 v = *reinterpret_cast<const float4 *>(obs_t + r * 16 +
+                                                                        ((c ^ (r & 3)) << 2));
+                    const float xc[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) {
+                        const int i = 4 * c + u;
+                        if (i < 15) {
+#pragma unroll
+                            for (int q = 0; q < 2; ++q)
+                                acc[q] = fmaf(xc[u], wq[(qp + q) * 16 + i], acc[q]);
+                        }
+                    }
+                }
+#pragma unroll
+                for (int q = 0; q < 2; ++q) o[qp + q] = tanh_fast(acc[q] + wq[(qp + q) * 16 + 15]);
+                __builtin_amdgcn_sched_barrier(0);
+            }
+            const float4 ov = make_float4(o[0], o[1], o[2], o[3]);
+            *reinterpret_cast<float4 *>(dst + swz32(r, wid)) = ov;
+            if (l1_h1)
+                *reinterpret_cast<float4 *>(
+                    l1_h1 + ((int64_t)b * m + (int64_t)(t - b * tiles_per_net) * XBM + r) * XK +
+                    k0) = ov;
+            // one row at a time: the register file is nearly full here (the
+            // next step's fragments and 128 accumulators are live)
+            __builtin_amdgcn_sched_barrier(0);
         }
     };
 
@@ -304,7 +393,7 @@ __global__ __launch_bounds__(XTHREADS) void gemm_x6_kernel(const float *__restri
             f.a[0][0].x += 1.0f;
             return;
         }
-        const uint8_t *SA = sh + LDS_A32 + (g % 3) * A32_STAGE;
+        const uint8_t *SA = sh + LDS_A32 + (g % NA) * A32_STAGE;
         const uint8_t *SB = sh + LDS_WB + (g & 1) * B_STAGE;
 #pragma unroll
         for (int i = 0; i < XMT; ++i) {
@@ -404,6 +493,68 @@ __global__ __launch_bounds__(XTHREADS) void gemm_x6_kernel(const float *__restri
     // the image of g + 2 and the A rows of g + 3 into stage g's (now free)
     // buffers; read stage g + 1's step-0 fragments during step 1's MFMAs.
     // VMEM ops per wave: 6 image + 2 A loads per stage, 16 stores per tile.
+    if constexpr (L1) {
+        // Per wave and iteration g after the barrier: the image of g + 2 (6
+        // LDS-DMA), at a tile's first iteration the next tile's observation
+        // rows (1), the 2 h1 stores of stage g + 2 (h1 non-null), and after
+        // a tile's last MFMAs its 16 output stores.  The barrier of g needs
+        // the image of g + 1: everything older than iteration g - 1's
+        // observation load, h1 stores and output stores.
+        const bool h1s = l1_h1 != nullptr;
+        auto wait_bar = [&](int n) {
+            __builtin_amdgcn_sched_barrier(0);
+            switch (n) {
+                case 1: asm volatile("s_waitcnt vmcnt(1) lgkmcnt(0)\n\ts_barrier" ::: "memory"); break;
+                case 2: asm volatile("s_waitcnt vmcnt(2) lgkmcnt(0)\n\ts_barrier" ::: "memory"); break;
+                case 3: asm volatile("s_waitcnt vmcnt(3) lgkmcnt(0)\n\ts_barrier" ::: "memory"); break;
+                case 16: asm volatile("s_waitcnt vmcnt(16) lgkmcnt(0)\n\ts_barrier" ::: "memory"); break;
+                case 18: asm volatile("s_waitcnt vmcnt(18) lgkmcnt(0)\n\ts_barrier" ::: "memory"); break;
+                default: asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory"); break;
+            }
+        };
+        zero_acc();
+        issue_b(0);
+        issue_b(1);                               // G >= 8
+        issue_obs(0);
+        wait_bar(0);                              // tile 0's observations visible
+        compute_a(0);
+        compute_a(1);
+        wait_bar(0);                              // A stages 0, 1 visible
+        Frag f0, f1;
+        read_frag(0, 0, f0);
+        for (int g = 0; g < G; ++g) {
+            read_frag(g, 1, f1);
+            mfma_step(f0);
+            int n = 0;
+            if (g > 0 && g + 1 < G) {
+                const int p = g - 1;              // what iteration g - 1 issued after its image load
+                n = (h1s && p + 2 < G ? 2 : 0) +
+                    ((p & 7) == 0 && (p >> 3) + 1 < nmine ? 1 : 0) + ((p & 7) == 7 ? 16 : 0);
+            }
+            wait_bar(n);
+            if (g + 2 < G) issue_b(g + 2);
+            if ((g & 7) == 0 && (g >> 3) + 1 < nmine) issue_obs((g >> 3) + 1);
+            // The SIMD partners (waves w and w + 4) form the next A stage at
+            // different times: waves 0-3 before this half-stage's MFMAs,
+            // waves 4-7 after them, so one partner's VALU runs beside the
+            // other's MFMAs (DR_X6_L1_SPLIT=0: every wave before)
+            const bool early = !DR_X6_L1_SPLIT || wid < XWAVES / 2;
+            __builtin_amdgcn_sched_barrier(0);
+            if (early && g + 2 < G && !DR_X6_NOCOMP) compute_a(g + 2);
+            __builtin_amdgcn_sched_barrier(0);
+            if (g + 1 < G) read_frag(g + 1, 0, f0);
+            __builtin_amdgcn_sched_barrier(0);
+            mfma_step(f1);
+            __builtin_amdgcn_sched_barrier(0);
+            if (!early && g + 2 < G && !DR_X6_NOCOMP) compute_a(g + 2);
+            __builtin_amdgcn_sched_barrier(0);
+            if ((g & 7) == 7) {
+                epilogue(g);
+                zero_acc();
+            }
+        }
+        return;
+    }
     zero_acc();
     issue_b(0);
     issue_a(0);
@@ -770,6 +921,37 @@ __global__ __launch_bounds__(XTHREADS) void gemm_x6_wgrad_kernel(
         }
 }
 
+// The L1 operands: w0p[b][k] = (W0[b][k][0..15), b0[b][k]) and, when obs is
+// given, obs16[r] = (obs[r][0..15), 0).  One thread per 16-float row.
+__global__ __launch_bounds__(256) void pack_first_kernel(int batch, const float *__restrict__ w0,
+                                                         const float *__restrict__ b0,
+                                                         float *__restrict__ w0p, int64_t m,
+                                                         const float *__restrict__ obs,
+                                                         float *__restrict__ obs16) {
+    const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    const int64_t nw = (int64_t)batch * XN;
+    if (t < nw) {
+        float r[16];
+#pragma unroll
+        for (int i = 0; i < 15; ++i) r[i] = w0[t * 15 + i];
+        r[15] = b0[t];
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+            reinterpret_cast<float4 *>(w0p + t * 16)[q] =
+                make_float4(r[4 * q], r[4 * q + 1], r[4 * q + 2], r[4 * q + 3]);
+    } else if (obs && t - nw < m) {
+        const int64_t i = t - nw;
+        float r[16];
+#pragma unroll
+        for (int c = 0; c < 15; ++c) r[c] = obs[i * 15 + c];
+        r[15] = 0.f;
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+            reinterpret_cast<float4 *>(obs16 + i * 16)[q] =
+                make_float4(r[4 * q], r[4 * q + 1], r[4 * q + 2], r[4 * q + 3]);
+    }
+}
+
 int fail_g(int code, const std::string &msg) {
     set_global_error(msg);
     return code;
@@ -843,13 +1025,51 @@ int dr_gemm_x6(int64_t batch, int64_t m, const float *a, const void *img, float 
         const char *e = getenv("DRONERL_X6_NT");
         return e && e[0] == '1' ? 1 : 0;
     }();
-    hipLaunchKernelGGL(gemm_x6_kernel, dim3(grid), dim3(XTHREADS), 0,
+    hipLaunchKernelGGL(gemm_x6_kernel<false>, dim3(grid), dim3(XTHREADS), 0,
                        static_cast<hipStream_t>(stream), a, static_cast<const uint8_t *>(img),
-                       c, m, ntiles, nt);
+                       c, m, ntiles, nt, nullptr, nullptr, nullptr);
     const hipError_t e = hipGetLastError();
     return e == hipSuccess
                ? DR_OK
                : fail_g(DR_ERR_HIP, std::string("gemm_x6_kernel: ") + hipGetErrorString(e));
+}
+
+int dr_gemm_x6_l1_pack(int64_t batch, const float *w0, const float *b0, float *w0p, int64_t m,
+                       const float *obs, float *obs16, void *stream) {
+    if (batch < 1 || batch > 2 || !w0 || !b0 || !w0p || (((uintptr_t)w0p) & 15) ||
+        (obs && (m < 1 || !obs16 || (((uintptr_t)obs16) & 15))))
+        return fail_g(DR_ERR_INVALID, "dr_gemm_x6_l1_pack: bad arguments");
+    const int64_t n = batch * XN + (obs ? m : 0);
+    hipLaunchKernelGGL(pack_first_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
+                       static_cast<hipStream_t>(stream), (int)batch, w0, b0, w0p, m, obs, obs16);
+    const hipError_t e = hipGetLastError();
+    return e == hipSuccess ? DR_OK
+                           : fail_g(DR_ERR_HIP, std::string("pack_first_kernel: ") +
+                                                    hipGetErrorString(e));
+}
+
+int dr_gemm_x6_l1(int64_t batch, int64_t m, const float *obs16, const float *w0p, const void *img,
+                  float *c, float *h1, void *stream) {
+    if (batch < 1 || batch > 2 || m < XBM || m % XBM || m > (int64_t(1) << 26) || !obs16 ||
+        !w0p || !img || !c || ((((uintptr_t)obs16) | ((uintptr_t)w0p) | ((uintptr_t)img) |
+                                ((uintptr_t)c) | ((uintptr_t)h1)) & 15))
+        return fail_g(DR_ERR_INVALID,
+                      "dr_gemm_x6_l1: bad arguments (m must be a positive multiple of 128, "
+                      "pointers 16-byte aligned)");
+    int dev = 0, n_cu = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        n_cu < 1)
+        n_cu = 256;
+    const int ntiles = (int)(batch * (m / XBM));
+    const int grid = ntiles < n_cu ? ntiles : n_cu;
+    hipLaunchKernelGGL(gemm_x6_kernel<true>, dim3(grid), dim3(XTHREADS), 0,
+                       static_cast<hipStream_t>(stream), nullptr,
+                       static_cast<const uint8_t *>(img), c, m, ntiles, 0, obs16, w0p, h1);
+    const hipError_t e = hipGetLastError();
+    return e == hipSuccess ? DR_OK
+                           : fail_g(DR_ERR_HIP, std::string("gemm_x6_kernel<L1>: ") +
+                                                    hipGetErrorString(e));
 }
 
 int dr_gemm_x6_wgrad(int64_t batch, int64_t m, int64_t chunks, const float *g, const float *h,

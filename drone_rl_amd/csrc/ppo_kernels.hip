@@ -812,25 +812,7 @@ __device__ inline float wave_allsum(float x) {
            __int_as_float(__builtin_amdgcn_readlane(__float_as_int(x), 32));
 }
 
-// Branch-free f32 tanh (<= 2 ulp): odd Taylor polynomial through x^15 for
-// |x| < 0.55 (truncation < 0.5 ulp there), 1 - 2 / (e^{2|x|} + 1) above
-// (hardware exp2 / rcp, the cancellation costs <= 2 ulp at the switch),
-// sign restored; NaN propagates, +-inf -> +-1.  The device library's tanhf
-// branches per element, which costs ~3x the instructions in a wave.
-__device__ inline float tanh_fast(float x) {
-    const float ax = fabsf(x);
-    const float z = ax * ax;
-    float p = fmaf(z, -929569.0f / 638512875.0f, 21844.0f / 6081075.0f);
-    p = fmaf(z, p, -1382.0f / 155925.0f);
-    p = fmaf(z, p, 62.0f / 2835.0f);
-    p = fmaf(z, p, -17.0f / 315.0f);
-    p = fmaf(z, p, 2.0f / 15.0f);
-    p = fmaf(z, p, -1.0f / 3.0f);
-    const float small = fmaf(ax * z, p, ax);
-    const float e = __builtin_amdgcn_exp2f(ax * 2.8853900817779268f);  // e^{2|x|}
-    const float large = fmaf(-2.0f, __builtin_amdgcn_rcpf(e + 1.0f), 1.0f);
-    return copysignf(ax < 0.55f ? small : large, x);
-}
+// tanh_fast: common.h (shared with the first-layer-fused GEMM, gemm_x6.hip)
 
 __device__ inline float4 ld4(const float *p) { return *reinterpret_cast<const float4 *>(p); }
 

@@ -108,3 +108,36 @@ def test_gemm_x6_wgrad_as_accurate_as_fp32(m, chunks):
     assert torch.equal(ws, ws2)
     assert L.dr_gemm_x6_wgrad(2, m, 3 * chunks + 1, ptr(G), ptr(H), ptr(ws), s) == \
         _lib.DR_ERR_INVALID
+
+
+@pytest.mark.parametrize("m", [128, 4096, 65536])
+def test_first_layer_fused_forward_is_bitwise_the_two_launches(m):
+    """dr_gemm_x6_l1 (the first layer formed in the 256x256 GEMM's prologue)
+    against dr_linear_tanh2 + dr_gemm_x6: h1 and z bitwise equal (the fused
+    kernel repeats linear_tanh's fmaf order and tanh; the MFMA stream is the
+    same), so the rollout forward (two launches) and the training forward
+    (fused, DRONERL_X6_L1=1) see identical network outputs."""
+    from drone_rl_amd import ppo_kernels as K
+    from drone_rl_amd.policy import ActorCritic, gemm_x6, gemm_x6_l1, x6_weights
+    dev = torch.device("cuda", 0)
+    pol = ActorCritic(15, 4, (256, 256), dev, 0.0, 3)
+    with torch.no_grad():
+        pol.flat.add_(torch.randn_like(pol.flat) * 0.05)      # non-zero biases too
+    g = torch.Generator(device=dev).manual_seed(m)
+    obs = torch.randn(m, 15, generator=g, device=dev) * 2.0
+    obs[0, 3] = 0.0
+    xw = x6_weights(pol, m)
+    xw.refresh()
+    h_ref = torch.empty(2, m, 256, device=dev)
+    K.linear_tanh2(obs, pol.p("pi0.w"), pol.p("pi0.b"), h_ref[0], pol.p("vf0.w"),
+                   pol.p("vf0.b"), h_ref[1])
+    z_ref = torch.empty(2, m, 256, device=dev)
+    gemm_x6(h_ref, xw.fwd, z_ref)
+    obs16 = torch.full((m, 16), float("nan"), device=dev)
+    h = torch.full((2, m, 256), float("nan"), device=dev)
+    z = torch.full((2, m, 256), float("nan"), device=dev)
+    gemm_x6_l1(pol, obs, obs16, xw, h, z)
+    torch.cuda.synchronize()
+    assert torch.equal(obs16[:, :15], obs) and (obs16[:, 15] == 0).all()
+    assert torch.equal(h, h_ref)
+    assert torch.equal(z, z_ref)
