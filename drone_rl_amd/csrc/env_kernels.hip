@@ -41,6 +41,23 @@ constexpr double kFactor = kArm / 1.4142135623730951;  // L / np.sqrt(2)
 constexpr float kKyaw32 = 0.01f;  // python float * np.float32 -> f32 (NEP 50)
 constexpr double kDt = 0.02;
 
+// Rollout kernel (A/B knobs): DR_RO_PIPE 1 = a full wave's obs rows of step
+// t are read back from the LDS staging buffer at the top of step t + 1 and
+// stored after its physics (two staging buffers per wave), so the LDS round
+// trip hides behind the physics; DR_RO_VM13 1 = the action-load wait counts
+// every younger store of a full wave (vmcnt(13)) instead of vmcnt(4), which
+// also waited for the previous step's reward / done stores.
+#ifndef DR_RO_PIPE
+#define DR_RO_PIPE 0
+#endif
+#ifndef DR_RO_VM13
+#define DR_RO_VM13 0
+#endif
+// DR_RO_PRESC 1 = the next step's Euler sincos formed inside the current
+// step's physics block (physics_step_mixed<PRE>)
+#ifndef DR_RO_PRESC
+#define DR_RO_PRESC 0
+#endif
 // DR_ABLATE (diagnostic builds only, scripts/micro/ablate.sh; never set in
 // the product build): 1 = f32 trig, 2 = no auto-reset, 3 = no LDS obs
 // staging, 4 = divides by reciprocal multiplies, 5 = constant reset draws,
@@ -457,8 +474,14 @@ __device__ inline MotorMix motor_mix(float4 act) {
                     ((-a0 + a1) + a2) - a3, ((a0 - a1) + a2) - a3};
 }
 
-template <typename S, int VAR>
-__device__ inline S physics_step_mixed(S st[F_N], MotorMix mx, S dt, bool &crash) {
+// PRE (the K-step rollout kernel): the Euler sincos of this step arrives in
+// sc_in (computed at the end of the previous step) and the next step's is
+// returned in sc_out, formed from the updated angles in the same basic block
+// as the position / reward chain, so it leaves the step's critical path.
+// The same m_sincos3 on the same angles: bitwise the non-PRE step.
+template <typename S, int VAR, bool PRE = false>
+__device__ inline S physics_step_mixed(S st[F_N], MotorMix mx, S dt, bool &crash,
+                                       const S *sc_in = nullptr, S *sc_out = nullptr) {
 #if DR_ABLATE == 6
     // diagnostic: no physics (loads / stores / reset / obs as built)
 #pragma unroll
@@ -476,7 +499,15 @@ __device__ inline S physics_step_mixed(S st[F_N], MotorMix mx, S dt, bool &crash
     // One sincos per angle: a shared range reduction yields exactly the
     // separate sin() and cos() results at half the instructions.
     S sn[3], cs[3];
-    m_sincos3(&st[F_EUL], sn, cs);
+    if constexpr (PRE) {
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            sn[k] = sc_in[k];
+            cs[k] = sc_in[3 + k];
+        }
+    } else {
+        m_sincos3(&st[F_EUL], sn, cs);
+    }
     DR_STAMP(1);
     const S sph = sn[0], cph = cs[0], sth = sn[1], cth = cs[1], sps = sn[2], cps = cs[2];
     // R(old euler) column 2 (drone.py:169-173): thrust is body-z only.
@@ -511,6 +542,7 @@ __device__ inline S physics_step_mixed(S st[F_N], MotorMix mx, S dt, bool &crash
     st[F_EUL + 0] += ed0 * dt;
     st[F_EUL + 1] += ed1 * dt;
     st[F_EUL + 2] += ed2 * dt;
+    if constexpr (PRE) m_sincos3(&st[F_EUL], sc_out, sc_out + 3);
 
     // Angular dynamics, diagonal inertia, old omega (135-139).
 #if DR_ABLATE == 4
@@ -867,7 +899,7 @@ __global__ __launch_bounds__(kEnvBlock) void env_rollout_kernel(EnvView<S> v, Ro
                                                                 FieldPtrs<S> fp) {
     constexpr int OD = VAR == DR_VARIANT_GYM ? 15 : (VAR == DR_VARIANT_MOVING ? 18 : 12);
     constexpr bool GYMLIKE = VAR != DR_VARIANT_VECTORIZED;
-    __shared__ float4 sh4[kEnvBlock * OD / 4];
+    __shared__ float4 sh4[(DR_RO_PIPE ? 2 : 1) * kEnvBlock * OD / 4];
     const int64_t n_ = v.n;
     const int64_t base = (int64_t)blockIdx.x * (DR_ENV_WPB * RPW);
     const int lane_ = threadIdx.x & 63;
@@ -875,6 +907,30 @@ __global__ __launch_bounds__(kEnvBlock) void env_rollout_kernel(EnvView<S> v, Ro
     const bool live = i_own < n_;
     const int64_t i = live ? i_own : n_ - 1;
     const uint64_t gid = (uint64_t)(v.env_id_offset + i);
+    // DR_RO_PIPE: this wave's rows are all live and every step's obs rows
+    // start 16-byte aligned (wave-uniform; else the unpipelined staging)
+    const int64_t wbase_ = base + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) * RPW;
+    const bool pipe = DR_RO_PIPE && !GEN && RPW == 64 && wbase_ + RPW <= n_ &&
+                      (((uintptr_t)io.obs) & 15) == 0 && ((n_ * OD) & 3) == 0 &&
+                      ((wbase_ * OD) & 3) == 0;
+    constexpr int NQ = (64 * OD + 255) / 256;     // float4 stores per lane and step
+    float4 *const stg0 = sh4 + (threadIdx.x >> 6) * (64 * OD / 4);
+    float4 *const stg1 = stg0 + kEnvBlock * OD / 4;
+    float4 pend[NQ];                               // step t - 1's rows, read back
+    (void)pend;
+    // read back step t's staged rows (issued early), then store them
+    auto pipe_read = [&](int t) {
+        const float4 *src = (t & 1) ? stg1 : stg0;
+#pragma unroll
+        for (int q = 0; q < NQ; ++q)
+            if (q * 64 + lane_ < 64 * OD / 4) pend[q] = src[q * 64 + lane_];
+    };
+    auto pipe_store = [&](int t) {
+        float4 *dst = reinterpret_cast<float4 *>(io.obs + ((int64_t)t * n_ + wbase_) * OD);
+#pragma unroll
+        for (int q = 0; q < NQ; ++q)
+            if (q * 64 + lane_ < 64 * OD / 4) st_out(&dst[q * 64 + lane_], pend[q]);
+    };
 
     S st[F_N];
 #pragma unroll
@@ -928,6 +984,10 @@ __global__ __launch_bounds__(kEnvBlock) void env_rollout_kernel(EnvView<S> v, Ro
     // step (a scalar load and its wait on the critical path)
     int32_t max_steps;
     asm volatile("v_mov_b32 %0, %1" : "=v"(max_steps) : "s"(v.max_steps));
+    // DR_RO_PRESC: this step's Euler sincos, formed at the end of the
+    // previous step (physics_step_mixed<PRE>); (0, 1) after a reset
+    S sc[6];
+    if (DR_RO_PRESC) m_sincos3(&st[F_EUL], sc, sc + 3);
     // one step from the action's motor mixes: the body of env_step_kernel
     // on registers
     auto step_one = [&](const MotorMix mx, const int t) {
@@ -942,10 +1002,19 @@ __global__ __launch_bounds__(kEnvBlock) void env_rollout_kernel(EnvView<S> v, Ro
                 nd_ok = true;
             }
         }
+        if (DR_RO_PIPE && pipe && t > 0) pipe_read(t - 1);
         if constexpr (VAR == DR_VARIANT_MOVING)
             moving_target(cen, mp, step + 1, (float)v.dt, &st[F_TGT], tvel);
         bool crash;
-        const S r = physics_step_mixed<S, VAR>(st, mx, v.dt, crash);
+        S sc_next[6];
+        const S r = DR_RO_PRESC
+                        ? physics_step_mixed<S, VAR, true>(st, mx, v.dt, crash, sc, sc_next)
+                        : physics_step_mixed<S, VAR>(st, mx, v.dt, crash);
+        if (DR_RO_PRESC) {
+#pragma unroll
+            for (int k = 0; k < 6; ++k) sc[k] = sc_next[k];
+        }
+        if (DR_RO_PIPE && pipe && t > 0) pipe_store(t - 1);
         step += 1;
         const bool done = live && (crash || (step >= max_steps));
         const int64_t row = (int64_t)t * n_;
@@ -969,6 +1038,15 @@ __global__ __launch_bounds__(kEnvBlock) void env_rollout_kernel(EnvView<S> v, Ro
                 // (drone.py:61, 68-70), carried on in registers
                 ep_num += 1;
                 if (ep_num % 2000 == 0) eps += 0.1;
+                // the reset's Euler angles are +0: sincos(+0) = (+0, 1)
+                // exactly (m_sincos3: k = 0, r = +0)
+                if (DR_RO_PRESC) {
+#pragma unroll
+                    for (int k = 0; k < 3; ++k) {
+                        sc[k] = (S)0;
+                        sc[3 + k] = (S)1;
+                    }
+                }
             }
         }
         make_obs<S, OD>(st, ob, tvel);
@@ -978,10 +1056,15 @@ __global__ __launch_bounds__(kEnvBlock) void env_rollout_kernel(EnvView<S> v, Ro
         }
         // (plain stores for these outputs measured the same: 60.2 / 62.2 us
         // per 32-step launch at 65,536 envs)
-        if (DR_ABLATE != 7)
-            store_obs_wave<OD, RPW>(reinterpret_cast<float *>(sh4), ob, io.obs + row * OD, n_);
-        else
+        if (DR_ABLATE == 7) {
             asm volatile("" ::"v"(ob[0]), "v"(ob[5]), "v"(ob[14 % OD]));
+        } else if (pipe) {
+            float *sw = reinterpret_cast<float *>((t & 1) ? stg1 : stg0);
+#pragma unroll
+            for (int k = 0; k < OD; ++k) sw[lane_ * OD + k] = ob[k];
+        } else {
+            store_obs_wave<OD, RPW>(reinterpret_cast<float *>(sh4), ob, io.obs + row * OD, n_);
+        }
     };
 
     if constexpr (GEN) {
@@ -1039,7 +1122,15 @@ __global__ __launch_bounds__(kEnvBlock) void env_rollout_kernel(EnvView<S> v, Ro
         // (62.9 us per 32-step launch with 335 MB of distinct actions
         // against 50.5 with one cache-resident action set).
         auto act_step = [&](f4v &r, const int t) {
-            if (t >= 2) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+            if (t >= 2) {
+                // younger than step t's action load (issued at the top of step
+                // t - 2): each of steps t - 2 and t - 1 issues its reward,
+                // done and NQ obs-row stores, step t - 1 the next load
+                if (DR_RO_VM13 && pipe && NQ == 4)
+                    asm volatile("s_waitcnt vmcnt(13)" ::: "memory");
+                else
+                    asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+            }
             const MotorMix mx = motor_mix(make_float4(r.x, r.y, r.z, r.w));
             asm volatile("" ::"v"(mx.thr), "v"(mx.phi), "v"(mx.theta), "v"(mx.psi));
             __builtin_amdgcn_sched_barrier(0);
@@ -1057,6 +1148,10 @@ __global__ __launch_bounds__(kEnvBlock) void env_rollout_kernel(EnvView<S> v, Ro
         // a wave with no live lane never waited for its loads: none may
         // still be writing registers the code below reuses
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    if (DR_RO_PIPE && pipe && io.k > 0) {          // the last step's rows
+        pipe_read(io.k - 1);
+        pipe_store(io.k - 1);
     }
     if (live) {
 #pragma unroll

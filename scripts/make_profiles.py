@@ -7,6 +7,8 @@
                                         by bench.py for roofline.traffic
   profiles/<round>_bench[_extra].json   the bench.py JSON lines of the session
   profiles/<round>_pmc_rollout.json     the K-step rollout kernel's PMC summary
+  profiles/<round>_pmc_x6.json          the x6 GEMM's PMC summary
+  (+ the headline rollout kernel's traffic into traffic.json, traffic_update.py)
 Usage: python scripts/make_profiles.py r01
 """
 import json
@@ -23,7 +25,7 @@ src = os.path.join(ROOT, "gpurun_out")
 ks = os.path.join(src, "prof", "run_kernel_stats.csv")
 if os.path.exists(ks):
     shutil.copy(ks, os.path.join(out, f"{rnd}_kernel_stats.csv"))
-for name in ("bench.json", "bench_extra.json"):       # the bench lines themselves
+for name in ("bench.json", "bench_extra.json", "bench_steps20.json"):   # the bench lines
     if os.path.exists(os.path.join(src, name)):
         shutil.copy(os.path.join(src, name), os.path.join(out, f"{rnd}_{name}"))
 traffic = {}
@@ -50,5 +52,12 @@ for tag, key, n in (("n65536", "f64_65536", 65536), ("n4m", "f64_4194304", 41943
 rs = os.path.join(src, "pmc_rollout", "summary.json")     # scripts/micro/rollout_pmc.sh
 if os.path.exists(rs):
     shutil.copy(rs, os.path.join(out, f"{rnd}_pmc_rollout.json"))
+gx = os.path.join(src, "pmc_gx6", "summary.json")         # scripts/micro/gemm_x6_pmc.sh
+if os.path.exists(gx):
+    shutil.copy(gx, os.path.join(out, f"{rnd}_pmc_x6.json"))
 json.dump(traffic, open(tpath, "w"), indent=1, sort_keys=True)
+rt = os.path.join(src, "pmc_rollout_traffic")            # scripts/rollout_traffic.sh
+if os.path.isdir(rt):
+    subprocess.run([sys.executable, os.path.join(ROOT, "scripts", "traffic_update.py"), rt],
+                   check=True)
 print(json.dumps(traffic, indent=1))

@@ -14,13 +14,31 @@ for grp in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY 
   if [ $rc -ne 0 ]; then tail -5 "$OUT/p$i.log"; exit $rc; fi
 done
 python3 - "$OUT" <<'PY'
-import csv, glob, sys, collections
+import csv, glob, json, sys, collections
 out = sys.argv[1]
 acc = collections.defaultdict(list)
 for f in glob.glob(out + "/p*/run_counter_collection.csv"):
     for r in csv.DictReader(open(f)):
         if "gemm_x6_kernel" in r["Kernel_Name"]:
             acc[r["Counter_Name"]].append(float(r["Counter_Value"]))
-for k, v in sorted(acc.items()):
-    print(f"{k:28s} {sum(v)/len(v):.4g}  (n={len(v)})")
+m = {k: sum(v) / len(v) for k, v in acc.items()}
+for k, v in sorted(m.items()):
+    print(f"{k:28s} {v:.4g}  (n={len(acc[k])})")
+res = {"workload": "scripts/micro/gemm_x6_bench.py --reps 10 (both nets, 65,536 rows, forward "
+                   "and input-gradient forms; cold inputs), rocprofv3 --pmc, two passes "
+                   "(scripts/micro/gemm_x6_pmc.sh); per-dispatch averages of gemm_x6_kernel",
+       "counters_per_dispatch": {k: round(v, 1) for k, v in sorted(m.items())}}
+w = m.get("SQ_WAVE_CYCLES")
+if w:
+    res["wait_any_frac"] = round(m["SQ_WAIT_ANY"] / w, 3)
+    res["wait_inst_any_frac"] = round(m["SQ_WAIT_INST_ANY"] / w, 3)
+    res["active_inst_any_frac"] = round(m["SQ_ACTIVE_INST_ANY"] / w, 3)
+if "SQ_VALU_MFMA_BUSY_CYCLES" in m and "GRBM_GUI_ACTIVE" in m:
+    # MFMA busy cycles are summed over all SIMDs (cycles); GUI_ACTIVE over the 8 XCDs
+    per_simd = m["SQ_VALU_MFMA_BUSY_CYCLES"] / 1024.0
+    res["mfma_busy_frac"] = round(per_simd / (m["GRBM_GUI_ACTIVE"] / 8.0), 3)
+if "SQ_LDS_BANK_CONFLICT" in m:
+    res["lds_bank_conflict_cycles"] = m["SQ_LDS_BANK_CONFLICT"]
+json.dump(res, open(out + "/summary.json", "w"), indent=1)
+print(json.dumps({k: v for k, v in res.items() if k != "counters_per_dispatch"}))
 PY

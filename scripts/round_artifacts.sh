@@ -26,6 +26,8 @@ if [ "$WHAT" = main ]; then
   step smoke 200 python -c "import __graft_entry__ as g; g.smoke()"
   step bench 300 python bench.py
   grep '^{' $OUT/bench.log > $OUT/bench.json || true
+  step bench_steps20 300 python bench.py --steps 20 --warmup 5
+  grep '^{' $OUT/bench_steps20.log > $OUT/bench_steps20.json || true
   step bench_extra 300 python bench.py --no-cpu-baseline --extra
   grep '^{' $OUT/bench_extra.log > $OUT/bench_extra.json || true
   export TMPDIR=/tmp
@@ -38,5 +40,7 @@ if [ "$WHAT" = pmc ]; then
   step pmc_n65536 400 bash scripts/pmc.sh n65536 --steps 50 --ppo-updates 0
   step pmc_n4m 400 bash scripts/pmc.sh n4m --envs 4194304 --steps 20 --warmup 5 --ppo-updates 0
   step pmc_rollout 300 bash scripts/micro/rollout_pmc.sh
+  step rollout_traffic 400 bash scripts/rollout_traffic.sh
+  step pmc_x6 300 bash scripts/micro/gemm_x6_pmc.sh
 fi
 echo "== done"
