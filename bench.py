@@ -268,12 +268,25 @@ def time_headline(args, n_envs, rank, world, device, steps, warmup, kmax):
     torch.cuda.synchronize(device)
     ev0 = torch.cuda.Event(enable_timing=True)
     ev1 = torch.cuda.Event(enable_timing=True)
-    ev0.record(stream)          # the events' lazy creation stays out of the timed region
-    ev1.record(stream)
+    pk0 = torch.cuda.Event(enable_timing=True)
+    pk1 = torch.cuda.Event(enable_timing=True)
+    for e in (ev0, ev1, pk0, pk1):
+        e.record(stream)        # the events' lazy creation stays out of the timed region
     if world > 1:
         dist.barrier()
+    packet_ms = None
     if g is None:
-        timed()                 # the last untimed repetition right before the timed one
+        # the last untimed repetition right before the timed one, through
+        # dr_rollout_timed: its events ride on the dispatch packets
+        # (hipExtLaunchKernel), i.e. the kernels' own start / end timestamps,
+        # the durations rocprofv3 reports (the timed launches below stay plain
+        # dr_rollout calls: the extended launch costs ~3 us more host wall,
+        # scripts/micro/launch_paths.py)
+        for i, c in enumerate(calls):
+            rcs.append(b.L.dr_rollout_timed(*c, pk0.cuda_event if i == 0 else None,
+                                            pk1.cuda_event if i == len(calls) - 1 else None))
+        torch.cuda.synchronize(device)
+        packet_ms = pk0.elapsed_time(pk1)
     gc.disable()
     torch.cuda.synchronize(device)
     t0 = time.perf_counter()
@@ -296,7 +309,7 @@ def time_headline(args, n_envs, rank, world, device, steps, warmup, kmax):
     ep = b.get("ep_num").float().mean().item()
     b.close()
     del g
-    return elapsed, gpu_ms, launches, ep
+    return elapsed, gpu_ms, launches, ep, packet_ms
 
 
 def time_rollout(args, n_envs, device, k, reps, gen, variant="gym", state_dtype=None):
@@ -597,8 +610,8 @@ def main():
     el_s, gm_s, ep_s = time_env(args, args.state_dtype, N, rank, world, device, K, args.warmup)
     single = step_block(el_s, gm_s, K, N)
     if args.headline == "rollout":
-        elapsed, gpu_ms, launches, ep = time_headline(args, N, rank, world, device, K,
-                                                      args.warmup, args.headline_k)
+        elapsed, gpu_ms, launches, ep, packet_ms = time_headline(
+            args, N, rank, world, device, K, args.warmup, args.headline_k)
         per_launch_s = gpu_ms / 1e3 / launches
         bpe = 81 + state_b * launches / K
         achieved = N * K * bpe / (gpu_ms / 1e3) / 1e9
@@ -613,6 +626,11 @@ def main():
                                "launch and env the f64 state read (124 B) and written (100 B) "
                                "once",
                 "avg_launch_us": round(per_launch_s * 1e6, 3),
+                # the same launches (the untimed repetition right before the
+                # timed one) by their dispatch packets' own timestamps: the
+                # kernel alone, without the event records' queue time
+                "avg_launch_us_packet": (round(packet_ms / launches * 1e3, 3)
+                                         if packet_ms else None),
                 "limiter": "latency at one wave per SIMD (VALU active 0.48 of wave cycles, "
                            "profiles/r02_pmc_rollout.json)"}
     else:

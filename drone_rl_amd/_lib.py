@@ -23,7 +23,7 @@ DR_ERR_HIP = -2
 DR_ERR_NOMEM = -3
 DR_ERR_UNSUPPORTED = -4
 
-ABI_VERSION = 12                # DR_ABI_VERSION in include/dronerl.h
+ABI_VERSION = 13                # DR_ABI_VERSION in include/dronerl.h
 DR_VARIANT_GYM = 0
 DR_VARIANT_VECTORIZED = 1
 DR_VARIANT_MOVING = 2
@@ -86,6 +86,7 @@ SIGNATURES = {
     "dr_set_reset_uniforms": (c_int, [_P, _P]),
     "dr_set_seed": (c_int, [_P, c_uint64]),
     "dr_rollout": (c_int, [_P, c_int32, _P, _P, _P, _P, _P]),
+    "dr_rollout_timed": (c_int, [_P, c_int32, _P, _P, _P, _P, _P, _P, _P]),
     "dr_rollout_random": (c_int, [_P, c_int32, c_uint64, c_int64, c_float, c_float, _P, _P,
                                   _P, _P, _P]),
     "dr_random_actions": (c_int, [c_int64, c_uint64, c_int64, c_int64, c_float,

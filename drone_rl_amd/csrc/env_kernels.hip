@@ -21,6 +21,7 @@
 
 #include <cstdlib>
 #include <cstring>
+#include <hip/hip_ext.h>
 #include <new>
 #include <string>
 
@@ -1712,24 +1713,38 @@ int dispatch_step(dr_handle *h, const StepIO &io, hipStream_t st) {
 }
 
 template <typename S, int VAR, bool GEN>
-int launch_rollout(dr_handle *h, const RolloutIO &io, hipStream_t st) {
+int launch_rollout(dr_handle *h, const RolloutIO &io, hipStream_t st, hipEvent_t e0,
+                   hipEvent_t e1) {
     EnvView<S> v = view_of<S>(h);
     FieldPtrs<S> fp;
     for (int k = 0; k < F_N; ++k) fp.p[k] = v.field(k);
     fp.step = v.step;
     fp.ep_num = v.ep_num;
     fp.eps = v.eps;
-    // rows per wave: 64 unless DRONERL_ROLLOUT_RPW=32 (A/B)
-    int rpw = 64;
-    if (const char *r = std::getenv("DRONERL_ROLLOUT_RPW")) rpw = std::atoi(r) == 32 ? 32 : 64;
-    if (rpw == 32)
-        hipLaunchKernelGGL((env_rollout_kernel<S, VAR, 32, GEN>),
-                           dim3(grid_for(h->n, DR_ENV_WPB * 32)), dim3(kEnvBlock), 0, st, v, io,
-                           fp);
-    else
-        hipLaunchKernelGGL((env_rollout_kernel<S, VAR, 64, GEN>),
-                           dim3(grid_for(h->n, DR_ENV_WPB * 64)), dim3(kEnvBlock), 0, st, v, io,
-                           fp);
+    // rows per wave: 64 unless DRONERL_ROLLOUT_RPW=32 (A/B; read once)
+    static const int rpw = [] {
+        const char *r = std::getenv("DRONERL_ROLLOUT_RPW");
+        return r && std::atoi(r) == 32 ? 32 : 64;
+    }();
+    // with events: hipExtLaunchKernelGGL binds them to the dispatch packet's
+    // own start / end timestamps (no extra packets in the queue)
+    if (rpw == 32) {
+        const dim3 grid(grid_for(h->n, DR_ENV_WPB * 32)), block(kEnvBlock);
+        if (e0 || e1)
+            hipExtLaunchKernelGGL((env_rollout_kernel<S, VAR, 32, GEN>), grid, block, 0, st, e0,
+                                  e1, 0, v, io, fp);
+        else
+            hipLaunchKernelGGL((env_rollout_kernel<S, VAR, 32, GEN>), grid, block, 0, st, v, io,
+                               fp);
+    } else {
+        const dim3 grid(grid_for(h->n, DR_ENV_WPB * 64)), block(kEnvBlock);
+        if (e0 || e1)
+            hipExtLaunchKernelGGL((env_rollout_kernel<S, VAR, 64, GEN>), grid, block, 0, st, e0,
+                                  e1, 0, v, io, fp);
+        else
+            hipLaunchKernelGGL((env_rollout_kernel<S, VAR, 64, GEN>), grid, block, 0, st, v, io,
+                               fp);
+    }
     hipError_t e = hipGetLastError();
     if (e != hipSuccess)
         return fail(h, DR_ERR_HIP, std::string("env_rollout_kernel: ") + hipGetErrorString(e));
@@ -1737,16 +1752,17 @@ int launch_rollout(dr_handle *h, const RolloutIO &io, hipStream_t st) {
 }
 
 template <bool GEN>
-int dispatch_rollout(dr_handle *h, const RolloutIO &io, hipStream_t st) {
+int dispatch_rollout(dr_handle *h, const RolloutIO &io, hipStream_t st, hipEvent_t e0,
+                     hipEvent_t e1) {
     const bool f64 = h->cfg.state_dtype == DR_STATE_F64;
     if (h->cfg.variant == DR_VARIANT_GYM)
-        return f64 ? launch_rollout<double, DR_VARIANT_GYM, GEN>(h, io, st)
-                   : launch_rollout<float, DR_VARIANT_GYM, GEN>(h, io, st);
+        return f64 ? launch_rollout<double, DR_VARIANT_GYM, GEN>(h, io, st, e0, e1)
+                   : launch_rollout<float, DR_VARIANT_GYM, GEN>(h, io, st, e0, e1);
     if (h->cfg.variant == DR_VARIANT_MOVING)
-        return f64 ? launch_rollout<double, DR_VARIANT_MOVING, GEN>(h, io, st)
-                   : launch_rollout<float, DR_VARIANT_MOVING, GEN>(h, io, st);
-    return f64 ? launch_rollout<double, DR_VARIANT_VECTORIZED, GEN>(h, io, st)
-               : launch_rollout<float, DR_VARIANT_VECTORIZED, GEN>(h, io, st);
+        return f64 ? launch_rollout<double, DR_VARIANT_MOVING, GEN>(h, io, st, e0, e1)
+                   : launch_rollout<float, DR_VARIANT_MOVING, GEN>(h, io, st, e0, e1);
+    return f64 ? launch_rollout<double, DR_VARIANT_VECTORIZED, GEN>(h, io, st, e0, e1)
+               : launch_rollout<float, DR_VARIANT_VECTORIZED, GEN>(h, io, st, e0, e1);
 }
 
 int check_rng(dr_handle *h) {
@@ -1935,7 +1951,8 @@ int dr_step_monitored_trunc(dr_handle *h, const float *actions, float *obs_out,
                        ep_return_out, ep_length_out, true, stream, truncated_out);
 }
 
-static int rollout_common(dr_handle *h, int32_t k, RolloutIO io, bool gen, void *stream) {
+static int rollout_common(dr_handle *h, int32_t k, RolloutIO io, bool gen, void *stream,
+                          void *start_event = nullptr, void *stop_event = nullptr) {
     if (!h) return fail(nullptr, DR_ERR_INVALID, "dr_rollout: null handle");
     if (k < 0) return fail(h, DR_ERR_INVALID, "dr_rollout: k < 0");
     if (!io.obs || !io.rew || !io.done)
@@ -1955,8 +1972,10 @@ static int rollout_common(dr_handle *h, int32_t k, RolloutIO io, bool gen, void 
     io.k = k;
     io.auto_reset = h->cfg.auto_reset;
     DeviceGuard g(h->cfg.device);
-    return gen ? dispatch_rollout<true>(h, io, as_stream(stream))
-               : dispatch_rollout<false>(h, io, as_stream(stream));
+    const hipEvent_t e0 = static_cast<hipEvent_t>(start_event);
+    const hipEvent_t e1 = static_cast<hipEvent_t>(stop_event);
+    return gen ? dispatch_rollout<true>(h, io, as_stream(stream), e0, e1)
+               : dispatch_rollout<false>(h, io, as_stream(stream), e0, e1);
 }
 
 int dr_rollout(dr_handle *h, int32_t k, const float *actions, float *obs_out, float *rew_out,
@@ -1967,6 +1986,17 @@ int dr_rollout(dr_handle *h, int32_t k, const float *actions, float *obs_out, fl
     io.rew = rew_out;
     io.done = done_out;
     return rollout_common(h, k, io, false, stream);
+}
+
+int dr_rollout_timed(dr_handle *h, int32_t k, const float *actions, float *obs_out,
+                     float *rew_out, uint8_t *done_out, void *stream, void *start_event,
+                     void *stop_event) {
+    RolloutIO io{};
+    io.actions = actions;
+    io.obs = obs_out;
+    io.rew = rew_out;
+    io.done = done_out;
+    return rollout_common(h, k, io, false, stream, start_event, stop_event);
 }
 
 int dr_rollout_random(dr_handle *h, int32_t k, uint64_t action_seed, int64_t action_step0,

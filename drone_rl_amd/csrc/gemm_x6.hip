@@ -101,6 +101,15 @@ namespace {
 #ifndef DR_X6_PRIO
 #define DR_X6_PRIO 0
 #endif
+// 1 (A/B knob, the round-3 form): the next stage's step-0 fragments read only
+// when that stage exists (path-dependent LDS count: lgkmcnt(0) before step 1)
+#ifndef DR_X6_CONDREAD
+#define DR_X6_CONDREAD 0
+#endif
+// 1 (A/B knob): a scheduling fence right after step 1's fragment reads
+#ifndef DR_X6_F1EARLY
+#define DR_X6_F1EARLY 0
+#endif
 
 constexpr int XK = 256;                 // reduction length (hidden width)
 constexpr int XN = 256;                 // output columns
@@ -542,7 +551,11 @@ __global__ __launch_bounds__(XTHREADS) void gemm_x6_kernel(
             __builtin_amdgcn_sched_barrier(0);
             if (early && g + 2 < G && !DR_X6_NOCOMP) compute_a(g + 2);
             __builtin_amdgcn_sched_barrier(0);
-            if (g + 1 < G) read_frag(g + 1, 0, f0);
+            if (DR_X6_CONDREAD) {
+                if (g + 1 < G) read_frag(g + 1, 0, f0);
+            } else {
+                read_frag(g + 1 < G ? g + 1 : g, 0, f0);   // see the L1 = false loop
+            }
             __builtin_amdgcn_sched_barrier(0);
             mfma_step(f1);
             __builtin_amdgcn_sched_barrier(0);
@@ -569,6 +582,9 @@ __global__ __launch_bounds__(XTHREADS) void gemm_x6_kernel(
     for (int g = 0; g < G; ++g) {
         X6_STAMP(g, 0);
         read_frag(g, 1, f1);
+        // DR_X6_F1EARLY: keep step 1's reads ahead of step 0's split and
+        // MFMAs (the scheduler otherwise sinks them to the step's end)
+        if (DR_X6_F1EARLY) __builtin_amdgcn_sched_barrier(0);
         mfma_step(f0);
         const bool pre1 = DR_X6_STAGGER && wid >= 4;
         if (DR_X6_EARLY || pre1) split_frag(f1);
@@ -591,7 +607,17 @@ __global__ __launch_bounds__(XTHREADS) void gemm_x6_kernel(
             if (g + 2 < G && DR_X6_ABL != 3) issue_b(g + 2);
             if (g + 3 < G && DR_X6_ABL != 3) issue_a(g + 3);
         }
-        if (g + 1 < G) read_frag(g + 1, 0, f0);
+        // unconditional (the last iteration re-reads stage g; unused): a
+        // read on one path only would make the waitcnt pass merge the two
+        // paths' LDS counts into an lgkmcnt(0) before step 1's split, which
+        // exposes these reads' latency; counted on every path, the waits
+        // below are lgkmcnt(>= 10): only step 1's reads, which the barrier
+        // already drained
+        if (DR_X6_CONDREAD) {
+            if (g + 1 < G) read_frag(g + 1, 0, f0);
+        } else {
+            read_frag(g + 1 < G ? g + 1 : g, 0, f0);
+        }
         __builtin_amdgcn_sched_barrier(0);
         mfma_step(f1, pre1);
         if (DR_X6_LATEISSUE) {
@@ -904,7 +930,11 @@ __global__ __launch_bounds__(XTHREADS) void gemm_x6_wgrad_kernel(
         else
             asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
         if (g + 3 < G_) issue(g + 3);
-        if (g + 1 < G_) read_frag(g + 1, 0, f0);
+        if (DR_X6_CONDREAD) {
+            if (g + 1 < G_) read_frag(g + 1, 0, f0);
+        } else {
+            read_frag(g + 1 < G_ ? g + 1 : g, 0, f0);   // see gemm_x6_kernel
+        }
         __builtin_amdgcn_sched_barrier(0);
         mfma_step(f1);
     }

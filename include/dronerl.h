@@ -39,7 +39,7 @@
 extern "C" {
 #endif
 
-#define DR_ABI_VERSION 12
+#define DR_ABI_VERSION 13
 
 enum dr_status {
     DR_OK = 0,
@@ -216,6 +216,16 @@ int dr_random_actions(int64_t n, uint64_t seed, int64_t env_id_offset,
    DR_ERR_UNSUPPORTED (their reset draws are supplied per step).  (ABI v11.) */
 int dr_rollout(dr_handle *h, int32_t k, const float *actions, float *obs_out,
                float *rew_out, uint8_t *done_out, void *stream);
+
+/* dr_rollout with its kernel's start / end recorded into two hipEvent_t
+   (either may be NULL) by hipExtLaunchKernel: the events take the dispatch
+   packet's own timestamps, so timing a launch adds no packets to the
+   stream (a benchmark's hipEventRecord pair costs several microseconds of
+   host and queue time around a ~35 us launch).  Same outputs as
+   dr_rollout.  (ABI v13.) */
+int dr_rollout_timed(dr_handle *h, int32_t k, const float *actions, float *obs_out,
+                     float *rew_out, uint8_t *done_out, void *stream,
+                     void *start_event, void *stop_event);
 
 /* dr_rollout on the synthetic random policy drawn in-kernel: step t's
    actions are exactly dr_random_actions(N, action_seed, env_id_offset of

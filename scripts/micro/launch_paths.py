@@ -1,7 +1,9 @@
 """Host wall of ONE 20-step rollout-kernel launch at 65,536 envs (the driver's
 bench.py --steps 20 form) by launch path: graph replay, DroneBatch.rollout,
 and a raw ctypes call with prebuilt arguments.  Median of 200 trials, each
-bracketed by synchronize like bench.py's timed region."""
+bracketed by synchronize like bench.py's timed region; "/none" without the
+event pair, "timed/*" through dr_rollout_timed (the events bound to the
+dispatch packet's timestamps)."""
 import os
 import sys
 import time
@@ -54,25 +56,43 @@ def sync_ev_then_dev(e1):
     torch.cuda.synchronize()
 
 
+E0, E1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+E0.record(st)
+E1.record(st)
+torch.cuda.synchronize()
+ftimed = L.dr_rollout_timed
+targs = args + (E0.cuda_event, E1.cuda_event)
+
+
+def timed():
+    ftimed(*targs)
+
+
 def trial(f, how):
     torch.cuda.synchronize()
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e0.record(st)
-    e1.record(st)
+    e0, e1 = E0, E1
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    e0.record(st)
-    f()
-    e1.record(st)
-    if how == "dev":
+    if f is timed:                  # the events ride on the dispatch packet
+        f()
+    elif how == "none":
+        f()
+    else:
+        e0.record(st)
+        f()
+        e1.record(st)
+    if how in ("dev", "none"):
         sync_dev()
     else:
         sync_ev_then_dev(e1)
-    return time.perf_counter() - t0, e0.elapsed_time(e1) * 1e3
+    dt = time.perf_counter() - t0
+    return dt, (0.0 if how == "none" and f is not timed else e0.elapsed_time(e1) * 1e3)
 
 
-for name, f in (("graph", g.replay), ("python", py), ("raw_ctypes", raw)):
-    for how in ("dev", "ev"):
+for name, f in (("graph", g.replay), ("python", py), ("raw_ctypes", raw), ("timed", timed)):
+    for how in ("dev", "ev", "none"):
+        if f is timed and how == "none":
+            continue
         for _ in range(20):
             f()
         torch.cuda.synchronize()

@@ -155,3 +155,46 @@ def test_rollout_bad_arguments():
                         d.data_ptr(), s) == _lib.DR_ERR_UNSUPPORTED
     with pytest.raises(ValueError):
         b.rollout(3, torch.zeros(4, 256, 4, device="cuda"))
+
+
+def test_rollout_timed_same_outputs_and_packet_events():
+    """dr_rollout_timed (the bench's timed launch): the outputs of dr_rollout,
+    bit for bit, and its two events (bound to the dispatch packet by
+    hipExtLaunchKernel, either may be null) bracket the kernel: a positive
+    elapsed time, no longer than the host wall around launch + sync."""
+    import time
+
+    from drone_rl_amd import random_actions
+    L = _lib.lib()
+    n, K = 65536, 20
+    a, b = _pair(n, "gym", torch.float64)
+    acts = torch.empty(K, n, 4, device="cuda")
+    for t in range(K):
+        random_actions(n, seed=9, step=t, env_id_offset=3 * n, out=acts[t])
+    o1, r1, d1 = a.rollout(K, acts)
+    o2 = torch.empty_like(o1)
+    r2 = torch.empty_like(r1)
+    d2 = torch.empty_like(d1)
+    s = torch.cuda.current_stream()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(s)
+    e1.record(s)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    assert L.dr_rollout_timed(b.handle, K, acts.data_ptr(), o2.data_ptr(), r2.data_ptr(),
+                              d2.data_ptr(), s.cuda_stream, e0.cuda_event,
+                              e1.cuda_event) == _lib.DR_OK
+    torch.cuda.synchronize()
+    wall_ms = (time.perf_counter() - t0) * 1e3
+    assert torch.equal(o1, o2) and torch.equal(r1, r2) and torch.equal(d1, d2)
+    ms = e0.elapsed_time(e1)
+    assert 0.0 < ms <= wall_ms, (ms, wall_ms)
+    fa, fb = _fields(a), _fields(b)
+    for k in fa:
+        assert torch.equal(fa[k], fb[k]), k
+    # null events: a plain launch; the outputs again those of dr_rollout
+    assert L.dr_rollout_timed(b.handle, K, acts.data_ptr(), o2.data_ptr(), r2.data_ptr(),
+                              d2.data_ptr(), s.cuda_stream, None, None) == _lib.DR_OK
+    o3, r3, d3 = a.rollout(K, acts)
+    torch.cuda.synchronize()
+    assert torch.equal(o3, o2) and torch.equal(r3, r2) and torch.equal(d3, d2)
