@@ -1173,6 +1173,313 @@ __global__ __launch_bounds__(kEnvBlock) void env_rollout_kernel(EnvView<S> v, Ro
 }
 
 // ----------------------------------------------------------------------------
+// Warp-specialised K-step rollout (dr_rollout's default launch form).
+// 512-thread blocks of 256 envs: waves 0-3, the PHYSICS waves (one per SIMD),
+// run the steps on registers exactly as env_rollout_kernel does, with no
+// global load inside the step loop (its only global stores are a reset's
+// ep_num / eps); waves 4-7, the MEMORY waves
+// (wave p + 4 shares SIMD p with physics wave p), move the bytes: each loads
+// its partner's actions by LDS-DMA kWsAhead + 1 steps ahead into a ring of
+// LDS slots (GEN: draws the random policy's actions into them), and streams
+// its partner's finished outputs -- obs rows, reward, done, staged in LDS by
+// the physics wave -- to HBM.  One s_barrier per step hands the slots over.  At one physics wave per SIMD, env_rollout_kernel's
+// wave issues its own stores and action loads between steps (the write
+// stream alone is ~0.9 us per step at 65,536 envs); here
+// that issue and its back-pressure sit on the memory waves, beside the
+// physics.
+//
+// Outputs are bitwise those of env_rollout_kernel (the same physics, reset
+// and Philox code on the same registers; only where the bytes travel
+// differs); tests/test_rollout_gpu.py checks both forms against K dr_step.
+//
+// Step t / phase t (B_t = the barrier that ends physics step t):
+//   physics: action t from slot t % NA (landed before B_(t-1)), the step,
+//            outputs into slot t & 1, lgkmcnt(0), B_t
+//   memory:  after B_(t-1): LDS-DMA action t + D + 1 into slot (t + D + 1) % NA
+//            (its previous action, t - 1, was read before B_(t-1)); load
+//            slot (t - 1) & 1 and store it to HBM (physics writes that slot
+//            again only after B_t); wait for action t + 1 (vmcnt, counted by
+//            hand: vmcnt counts loads and stores in issue order), B_t.
+//   After the last barrier the memory waves store step K - 1's outputs.
+// ----------------------------------------------------------------------------
+// DR_WS_ABL (diagnostic builds, wrong by construction; timing only):
+// 1 = the memory waves store no outputs; 2 = the physics waves skip the
+// physics (the state only advances by the action's thrust)
+#ifndef DR_WS_ABL
+#define DR_WS_ABL 0
+#endif
+// A/B knobs: DR_WS_PRIO 1 = the physics waves at s_setprio 1 (they win issue
+// arbitration against their memory-wave partner); DR_WS_RA = steps per
+// group of the next-reset Philox draw-ahead
+#ifndef DR_WS_PRIO
+#define DR_WS_PRIO 0
+#endif
+#ifndef DR_WS_RA
+#define DR_WS_RA 8
+#endif
+constexpr int kWsEnvs = 256;                 // envs per block: 4 physics waves
+constexpr int kWsThreads = 2 * kWsEnvs;
+constexpr int kWsAhead = 2;                  // D
+constexpr int kWsNA = kWsAhead + 2;          // action ring slots
+
+// global_load_lds_dwordx4: lane l's 16 bytes land at LDS byte lds_base + 16 l
+// (the wave's 64 actions as one 1-KB slot).  It clobbers m0, which the
+// compiler reserves (and sets before each of its own uses).
+#pragma clang diagnostic push
+#pragma clang diagnostic ignored "-Winline-asm"
+__device__ inline void ws_glds16(const void *gptr, uint32_t lds_base) {
+    asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off"
+                 ::"v"(gptr), "s"(lds_base)
+                 : "memory", "m0");
+}
+#pragma clang diagnostic pop
+
+template <int OD>
+struct WsLds {
+    float obs[2][kWsEnvs * OD];              // per slot: 4 waves x 64 rows x OD
+    float rew[2][kWsEnvs];
+    uint8_t done[2][kWsEnvs];
+    float4 act[kWsNA][kWsEnvs];
+};
+
+template <typename S, int VAR, bool GEN>
+__global__ __launch_bounds__(kWsThreads) void env_rollout_ws_kernel(EnvView<S> v, RolloutIO io,
+                                                                    FieldPtrs<S> fp) {
+    constexpr int OD = VAR == DR_VARIANT_GYM ? 15 : (VAR == DR_VARIANT_MOVING ? 18 : 12);
+    constexpr bool GYMLIKE = VAR != DR_VARIANT_VECTORIZED;
+    constexpr int NQ = (64 * OD / 4 + 63) / 64;  // float4 rows-stores per lane and step
+    // the hand-counted wait assumes NQ obs + 1 reward + 1 done store per phase
+    constexpr int S_OPS = NQ + 2;
+    __shared__ __attribute__((aligned(16))) WsLds<OD> sh;
+    const int64_t n_ = v.n;
+    const int K = io.k;
+    const int lane = threadIdx.x & 63;
+    const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int p = wid & 3;                        // physics wave / partner index
+    const int64_t wbase = (int64_t)blockIdx.x * kWsEnvs + p * 64;
+    const int64_t i_own = wbase + lane;
+    const bool live = i_own < n_;
+    const int64_t i = live ? i_own : n_ - 1;
+
+    if (wid >= 4) {
+        // ---------------- memory wave ----------------
+        const int64_t nvalid = (n_ - wbase) < 64 ? (n_ - wbase) : 64;
+        // full: 64 live rows and 16-byte aligned obs rows at every step; else
+        // (the ragged last wave) scalar stores and vmcnt(0) waits
+        const bool full = nvalid == 64 && (((uintptr_t)io.obs) & 15) == 0 &&
+                          ((n_ * OD) & 3) == 0;
+        const float4 *acts = reinterpret_cast<const float4 *>(io.actions);
+        // GEN: the memory wave draws the random policy's action itself
+        // (random_actions_kernel's Philox word for step a_step0 + t) into the
+        // slot, off the physics wave's instruction stream
+        const uint64_t gid = (uint64_t)(v.env_id_offset + i);
+        auto load_act = [&](int t) {
+            if constexpr (GEN) {
+                const uint64_t s = io.a_step0 + (uint64_t)t;
+                uint32_t ak0 = io.a_k0, ak1 = io.a_k1;
+                asm volatile("" : "+s"(ak0), "+s"(ak1));
+                const u32x4 r = philox4x32_10(
+                    u32x4{(uint32_t)s, (uint32_t)(s >> 32), (uint32_t)gid,
+                          TAG_ACTION ^ (uint32_t)(gid >> 32)},
+                    ak0, ak1);
+                const float4 act = make_float4(io.a_lo + io.a_span * u01_f32(r.x),
+                                               io.a_lo + io.a_span * u01_f32(r.y),
+                                               io.a_lo + io.a_span * u01_f32(r.z),
+                                               io.a_lo + io.a_span * u01_f32(r.w));
+                sh.act[t % kWsNA][p * 64 + lane] = act;
+                if (io.act_out && live)
+                    st_out(at(reinterpret_cast<float4 *>(io.act_out) + (int64_t)t * n_, i), act);
+            } else if (nvalid > 0) {
+                ws_glds16(at(acts + (int64_t)t * n_, i),
+                          (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void *)
+                              &sh.act[t % kWsNA][p * 64]);
+            }
+        };
+        auto store_out = [&](int t) {
+            if (nvalid <= 0 || DR_WS_ABL == 1) return;
+            const int so = t & 1;
+            const int64_t row = (int64_t)t * n_;
+            const float *src = &sh.obs[so][p * 64 * OD];
+            float *dst = io.obs + (row + wbase) * OD;
+            const float r = sh.rew[so][p * 64 + lane];
+            const uint8_t d = sh.done[so][p * 64 + lane];
+            if (full) {
+                float4 q[NQ];
+#pragma unroll
+                for (int j = 0; j < NQ; ++j)
+                    if (j * 64 + lane < 64 * OD / 4)
+                        q[j] = reinterpret_cast<const float4 *>(src)[j * 64 + lane];
+#pragma unroll
+                for (int j = 0; j < NQ; ++j)
+                    if (j * 64 + lane < 64 * OD / 4)
+                        st_out(reinterpret_cast<float4 *>(dst) + j * 64 + lane, q[j]);
+            } else {
+                for (int q = lane; q < (int)nvalid * OD; q += 64) st_out(dst + q, src[q]);
+            }
+            if (live) {
+                st_out(at(io.rew + row, i_own), r);
+                st_out(at(io.done + row, i_own), d);
+            }
+        };
+        for (int t = 0; t <= kWsAhead && t < K; ++t) load_act(t);
+        if (!GEN) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // actions 0 .. D
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");   // B_(-1)
+        for (int t = 0; t < K; ++t) {
+            if (t + kWsAhead + 1 < K) load_act(t + kWsAhead + 1);
+            if (t >= 1) store_out(t - 1);
+            // action t + 1 must have landed before B_t (actions 0 .. D did
+            // before B_(-1)).  Younger than its load (issued at phase t - D)
+            // in the steady state: D + 1 phases of S_OPS stores and D loads;
+            // elsewhere at least this phase's S_OPS stores (t >= D >= 1).  A
+            // ragged wave waits for every op.
+            if (!GEN && t + 1 < K && t + 1 > kWsAhead) {
+                __builtin_amdgcn_sched_barrier(0);
+                if (!full)
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                else if (t >= kWsAhead + 1 && t + kWsAhead + 1 < K)
+                    asm volatile("s_waitcnt vmcnt(%0)" ::"n"((kWsAhead + 1) * S_OPS + kWsAhead)
+                                 : "memory");
+                else
+                    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(S_OPS) : "memory");
+            }
+            asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");   // B_t
+        }
+        if (K > 0) store_out(K - 1);
+        return;
+    }
+
+    // ---------------- physics wave ----------------
+    const uint64_t gid = (uint64_t)(v.env_id_offset + i);
+    S st[F_N];
+#pragma unroll
+    for (int k = F_EUL; k < F_N - 3; ++k) st[k] = *at(fp.p[k], i);
+#pragma unroll
+    for (int k = 0; k < F_EUL; ++k) st[k] = *at(fp.p[k], i);
+    S cen[3];
+    float mp[9], tvel[3];
+    if constexpr (VAR == DR_VARIANT_GYM) {
+#pragma unroll
+        for (int k = F_TGT; k < F_N; ++k) st[k] = *at(fp.p[k], i);
+    } else if constexpr (VAR == DR_VARIANT_MOVING) {
+#pragma unroll
+        for (int k = 0; k < 3; ++k) cen[k] = *at(fp.p[F_TGT + k], i);
+#pragma unroll
+        for (int k = 0; k < 9; ++k) mp[k] = *at(v.mot + k * v.stride, i);
+    } else {
+        st[F_TGT + 0] = (S)0;
+        st[F_TGT + 1] = (S)0;
+        st[F_TGT + 2] = (S)10.0;
+    }
+    int32_t step = *at(fp.step, i);
+    int32_t ep_num = 0;
+    double eps = 0.0;
+    if constexpr (GYMLIKE) {
+        ep_num = *at(fp.ep_num, i);
+        eps = *at(fp.eps, i);
+    }
+    // every state load landed before the loop (else the compiler waits for
+    // them at their first uses inside it, as vmcnt(0))
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    bool reset_any = false;
+    float ob[OD];
+    EnvView<S> vk = v;
+    // the next reset's Philox blocks drawn ahead, once per group of steps
+    // (env_rollout_kernel)
+    constexpr int kResetAhead = DR_WS_RA;
+    if (DR_WS_PRIO) __builtin_amdgcn_s_setprio(1);
+    constexpr int NB = VAR == DR_VARIANT_MOVING ? 4 : 1;
+    u32x4 nd[NB] = {};
+    bool nd_ok = false;
+    int32_t max_steps;
+    asm volatile("v_mov_b32 %0, %1" : "=v"(max_steps) : "s"(v.max_steps));
+    asm volatile("s_barrier" ::: "memory");                          // B_(-1)
+    for (int t = 0; t < K; ++t) {
+        asm volatile("" : "+s"(vk.seed_lo), "+s"(vk.seed_hi));
+        const MotorMix mx = motor_mix(sh.act[t % kWsNA][p * 64 + lane]);
+        if constexpr (GYMLIKE) {
+            if (t % kResetAhead == 0 && !nd_ok) {
+#pragma unroll
+                for (int b = 0; b < NB; ++b)
+                    nd[b] = philox4x32_10(u32x4{(uint32_t)(ep_num + 1), (uint32_t)gid,
+                                                (uint32_t)(gid >> 32), TAG_RESET | (uint32_t)b},
+                                          vk.seed_lo, vk.seed_hi);
+                nd_ok = true;
+            }
+        }
+        if constexpr (VAR == DR_VARIANT_MOVING)
+            moving_target(cen, mp, step + 1, (float)v.dt, &st[F_TGT], tvel);
+        bool crash;
+        S r;
+        if (DR_WS_ABL == 2) {
+            st[F_VEL + 2] += (S)mx.thr * v.dt;
+            st[F_POS + 2] += st[F_VEL + 2] * v.dt;
+            crash = st[F_POS + 2] < (S)0;
+            r = st[F_POS + 2];
+        } else {
+            r = physics_step_mixed<S, VAR>(st, mx, v.dt, crash);
+        }
+        step += 1;
+        const bool done = live && (crash || (step >= max_steps));
+        if constexpr (GYMLIKE) {
+            if (done && io.auto_reset) {
+                step = 0;
+                reset_any = true;
+                // a second reset within the group: draw its blocks here (the
+                // same words the reset would draw; always passing the array
+                // keeps it in registers -- a pointer-or-null argument put it
+                // on the scratch stack)
+                if (!nd_ok) {
+#pragma unroll
+                    for (int b = 0; b < NB; ++b)
+                        nd[b] = philox4x32_10(u32x4{(uint32_t)(ep_num + 1), (uint32_t)gid,
+                                                    (uint32_t)(gid >> 32),
+                                                    TAG_RESET | (uint32_t)b},
+                                              vk.seed_lo, vk.seed_hi);
+                }
+                if constexpr (VAR == DR_VARIANT_GYM) {
+                    gym_reset_regs(vk, i, 0, st, ep_num, eps, &nd[0]);
+                } else {
+                    moving_reset_regs(vk, i, 0, st, cen, mp, ep_num, eps, nd);
+                    moving_target(cen, mp, 0, (float)v.dt, &st[F_TGT], tvel);
+                }
+                nd_ok = false;
+                ep_num += 1;
+                if (ep_num % 2000 == 0) eps += 0.1;
+            }
+        }
+        make_obs<S, OD>(st, ob, tvel);
+        if (!live) {
+#pragma unroll
+            for (int k = 0; k < OD; ++k) ob[k] = 0.f;
+        }
+        const int so = t & 1;
+        float *srow = &sh.obs[so][(p * 64 + lane) * OD];
+#pragma unroll
+        for (int k = 0; k < OD; ++k) srow[k] = ob[k];
+        sh.rew[so][p * 64 + lane] = (float)r;
+        sh.done[so][p * 64 + lane] = (uint8_t)done;
+        __builtin_amdgcn_sched_barrier(0);
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");   // B_t
+    }
+    if (live) {
+#pragma unroll
+        for (int k = 0; k < 12; ++k) st_out(at(fp.p[k], i), st[k]);
+        st_out(at(fp.step, i), step);
+        if (reset_any) {
+            if constexpr (VAR == DR_VARIANT_GYM) {
+#pragma unroll
+                for (int k = F_TGT; k < F_N; ++k) *at(fp.p[k], i) = st[k];
+            } else if constexpr (VAR == DR_VARIANT_MOVING) {
+#pragma unroll
+                for (int k = 0; k < 3; ++k) *at(fp.p[F_TGT + k], i) = cen[k];
+#pragma unroll
+                for (int k = 0; k < 9; ++k) *at(v.mot + k * v.stride, i) = mp[k];
+            }
+        }
+    }
+}
+
+// ----------------------------------------------------------------------------
 // Quad kernel: 4 lanes per env (one DPP quad), lane k < 3 owns component k of
 // pos / vel / euler / omega / target.  Every lane runs the SAME instruction
 // stream on its own component (SIMD-uniform: selects, never lane-divergent
@@ -1726,9 +2033,22 @@ int launch_rollout(dr_handle *h, const RolloutIO &io, hipStream_t st, hipEvent_t
         const char *r = std::getenv("DRONERL_ROLLOUT_RPW");
         return r && std::atoi(r) == 32 ? 32 : 64;
     }();
+    // the warp-specialised form unless DRONERL_ROLLOUT_WS=0 or rpw 32 (A/B)
+    static const bool ws = [] {
+        const char *r = std::getenv("DRONERL_ROLLOUT_WS");
+        return !(r && std::atoi(r) == 0);
+    }();
     // with events: hipExtLaunchKernelGGL binds them to the dispatch packet's
     // own start / end timestamps (no extra packets in the queue)
-    if (rpw == 32) {
+    if (ws && rpw == 64) {
+        const dim3 grid(grid_for(h->n, kWsEnvs)), block(kWsThreads);
+        if (e0 || e1)
+            hipExtLaunchKernelGGL((env_rollout_ws_kernel<S, VAR, GEN>), grid, block, 0, st, e0,
+                                  e1, 0, v, io, fp);
+        else
+            hipLaunchKernelGGL((env_rollout_ws_kernel<S, VAR, GEN>), grid, block, 0, st, v, io,
+                               fp);
+    } else if (rpw == 32) {
         const dim3 grid(grid_for(h->n, DR_ENV_WPB * 32)), block(kEnvBlock);
         if (e0 || e1)
             hipExtLaunchKernelGGL((env_rollout_kernel<S, VAR, 32, GEN>), grid, block, 0, st, e0,
