@@ -1219,7 +1219,17 @@ __global__ __launch_bounds__(kEnvBlock) void env_rollout_kernel(EnvView<S> v, Ro
 #endif
 constexpr int kWsEnvs = 256;                 // envs per block: 4 physics waves
 constexpr int kWsThreads = 2 * kWsEnvs;
-constexpr int kWsAhead = 2;                  // D
+// DR_WS_PRE (A/B knob; measured 1-2 us slower per 32-step launch, so 0):
+// 1: the physics wave reads action t + 1 from LDS at the top of
+// step t (its LDS latency hidden behind the step), so the memory waves land
+// it one barrier earlier: loads D = 3 steps ahead; 0: action t read at the
+// top of step t, D = 2.  Ring slots: D + 2 (PRE: action 0 is read after
+// B_(-1), in phase 0, when action D + 1 is issued; so slot 0 must not be its
+// slot).
+#ifndef DR_WS_PRE
+#define DR_WS_PRE 0
+#endif
+constexpr int kWsAhead = DR_WS_PRE ? 3 : 2;  // D
 constexpr int kWsNA = kWsAhead + 2;          // action ring slots
 
 // global_load_lds_dwordx4: lane l's 16 bytes land at LDS byte lds_base + 16 l
@@ -1327,17 +1337,19 @@ __global__ __launch_bounds__(kWsThreads) void env_rollout_ws_kernel(EnvView<S> v
         for (int t = 0; t < K; ++t) {
             if (t + kWsAhead + 1 < K) load_act(t + kWsAhead + 1);
             if (t >= 1) store_out(t - 1);
-            // action t + 1 must have landed before B_t (actions 0 .. D did
-            // before B_(-1)).  Younger than its load (issued at phase t - D)
-            // in the steady state: D + 1 phases of S_OPS stores and D loads;
-            // elsewhere at least this phase's S_OPS stores (t >= D >= 1).  A
+            // action a = t + 1 + PRE must have landed before B_t (actions
+            // 0 .. D did before B_(-1)).  It was issued first in phase
+            // q = a - D - 1 = t - (D - PRE); younger in the steady state: q's
+            // S_OPS stores and D - PRE phases of one load and S_OPS stores;
+            // elsewhere at least this phase's S_OPS stores (t >= 1 here).  A
             // ragged wave waits for every op.
-            if (!GEN && t + 1 < K && t + 1 > kWsAhead) {
+            constexpr int AH = kWsAhead - DR_WS_PRE;
+            if (!GEN && t + 1 + DR_WS_PRE < K && t + 1 + DR_WS_PRE > kWsAhead) {
                 __builtin_amdgcn_sched_barrier(0);
                 if (!full)
                     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                else if (t >= kWsAhead + 1 && t + kWsAhead + 1 < K)
-                    asm volatile("s_waitcnt vmcnt(%0)" ::"n"((kWsAhead + 1) * S_OPS + kWsAhead)
+                else if (t >= AH + 1 && t + kWsAhead + 1 < K)
+                    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(S_OPS + AH * (S_OPS + 1))
                                  : "memory");
                 else
                     asm volatile("s_waitcnt vmcnt(%0)" ::"n"(S_OPS) : "memory");
@@ -1393,9 +1405,17 @@ __global__ __launch_bounds__(kWsThreads) void env_rollout_ws_kernel(EnvView<S> v
     int32_t max_steps;
     asm volatile("v_mov_b32 %0, %1" : "=v"(max_steps) : "s"(v.max_steps));
     asm volatile("s_barrier" ::: "memory");                          // B_(-1)
+    float4 a_next = sh.act[0][p * 64 + lane];
     for (int t = 0; t < K; ++t) {
         asm volatile("" : "+s"(vk.seed_lo), "+s"(vk.seed_hi));
-        const MotorMix mx = motor_mix(sh.act[t % kWsNA][p * 64 + lane]);
+        float4 a_cur;
+        if (DR_WS_PRE) {
+            a_cur = a_next;
+            if (t + 1 < K) a_next = sh.act[(t + 1) % kWsNA][p * 64 + lane];
+        } else {
+            a_cur = sh.act[t % kWsNA][p * 64 + lane];
+        }
+        const MotorMix mx = motor_mix(a_cur);
         if constexpr (GYMLIKE) {
             if (t % kResetAhead == 0 && !nd_ok) {
 #pragma unroll
