@@ -42,6 +42,7 @@
 // net_arch [256, 256], /root/reference/train.py:36-43) -- torch fp32 Linear.
 
 #include <cstdlib>
+#include <type_traits>
 
 #include "common.h"
 
@@ -242,6 +243,14 @@ constexpr int LDS_OBS = 2 * B_STAGE + 2 * A32_STAGE;
 __device__ inline void glds16(const void *gptr, uint32_t lds_base) {
     asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off"
                  ::"v"(gptr), "s"(lds_base)
+                 : "memory", "m0");
+}
+// The same with the global address split into a wave-uniform 64-bit base
+// (SGPRs) and a 32-bit per-lane byte offset (the saddr form): a loop of
+// these keeps one offset VGPR instead of a 64-bit address per instruction.
+__device__ inline void glds16_s(const void *sbase, uint32_t voff, uint32_t lds_base) {
+    asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, %1"
+                 ::"v"(voff), "s"(sbase), "s"(lds_base)
                  : "memory", "m0");
 }
 __device__ inline uint32_t lds_addr(const uint8_t *p) {
@@ -631,6 +640,277 @@ __global__ __launch_bounds__(XTHREADS) void gemm_x6_kernel(
             epilogue(g);
             zero_acc();
         }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Ping-pong form of gemm_x6_kernel<false> (A/B form, DRONERL_X6_PP=1: the
+// same tiles, LDS images and per-output MFMA order, so bitwise the same C;
+// measured slower, 143-148 vs 121-125 us: in-kernel stamps show the MFMA
+// interval at ~1,300 cycles for its 24 MFMAs, not 768 -- the partner's
+// split VALU, LDS-DMA and fragment reads share the SIMD's vector issue with
+// the MFMAs, so alternating the roles does not take them off the MFMA
+// wave's path).
+//
+// The two waves of each SIMD alternate roles once per barrier interval
+// (MI355X_MICROARCH.md, two waves per SIMD): while one wave issues the 24
+// MFMAs of a k16 step back to back, its partner reads and splits the
+// fragments of its next step (and issues LDS-DMA / output stores), so the
+// matrix pipe is not left idle while a wave splits.  Group A = waves 0-3
+// (tile rows 0-63), group B = waves 4-7 (rows 64-127); u = global k16 step
+// (stage g = u >> 1, half s = u & 1), U = 2 G steps per block:
+//   interval 2u - 1: A prep(u)       B MFMA(u - 1)
+//   interval 2u    : A MFMA(u)       B prep(u)
+// (interval -1: A prep(0), B idle; the last, 2U - 1: A stores its rows of
+// the last tile).  Every interval ends in a barrier, the
+// same count for both groups.  A wave holds ONE step's fragments (prep fills
+// them, its next interval's MFMAs consume them), 48 VGPRs beside the 128
+// accumulator registers.
+//
+// LDS: stage g (B image slot g & 1, A rows slot g % 3) is read in intervals
+// 4g - 1 .. 4g + 2.  Its slots are refilled after the barrier that ends
+// 4g + 2: the image of g + 2 by group A in interval 4g + 3, the A rows of
+// g + 3 by group B in 4g + 4; each group waits for its own DMA at the end of
+// interval 4h + 2 (h = g + 1 resp. g + 2) before the barrier that publishes
+// stage h + 1 for its first read at 4h + 3.  A tile's outputs are stored by
+// a group in the prep interval after its last MFMA step (A: 32T + 31, B:
+// 32T + 32; B's last tile after the loop).
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(XTHREADS) void gemm_x6_pp_kernel(const float *__restrict__ A,
+                                                              const uint8_t *__restrict__ img,
+                                                              float *__restrict__ C, int64_t m,
+                                                              int ntiles, int nt) {
+    static_assert(XWAVES == 8, "the ping-pong kernel pairs waves w and w + 4");
+    __shared__ __attribute__((aligned(16))) uint8_t sh[LDS_TOTAL];
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int grp = wid >> 2, wq = wid & 3;
+    const int wm = grp, wn = wq;
+    const int tiles_per_net = (int)(m / XBM);
+    const int nmine = (ntiles - (int)blockIdx.x + (int)gridDim.x - 1) / (int)gridDim.x;
+    const int G = nmine * XKC;
+    const int U = 2 * G;
+
+    auto tile_of = [&](int g) { return (int)blockIdx.x + (g >> 3) * (int)gridDim.x; };
+    auto net_of = [&](int t) { return t / tiles_per_net; };
+    // stage g's weight image by NW waves (index w of NW); addresses as a
+    // uniform base plus one per-lane offset (glds16_s)
+    const uint32_t voff_b = (uint32_t)lane * 16;
+    // (NW = 4 or 8: the compile-time count of waves sharing the stage)
+    auto issue_b = [&](int g, int w, auto nw) {
+        constexpr int NW = decltype(nw)::value;
+        const uint8_t *src = img + (int64_t)net_of(tile_of(g)) * W_IMG + (g & 7) * B_STAGE;
+        uint8_t *dst = sh + LDS_WB + (g & 1) * B_STAGE;
+#pragma unroll
+        for (int q = 0; q < B_STAGE / 1024 / NW; ++q) {
+            const int ins = w + NW * q;
+            glds16_s(src + ins * 1024, voff_b, lds_addr(dst + ins * 1024));
+        }
+    };
+    // A rows: instruction ins moves rows 8 ins + (lane >> 3); lane L fills LDS
+    // chunk L & 7 with global chunk (L & 7) ^ ((row >> 1) & 7), which depends
+    // on ins only through its parity: two offset VGPRs
+    uint32_t voff_a[2];
+#pragma unroll
+    for (int par = 0; par < 2; ++par) {
+        const int chunk = (lane & 7) ^ (((lane >> 4) + 4 * par) & 7);
+        voff_a[par] = (uint32_t)(((lane >> 3) * XK + chunk * 4) * 4);
+    }
+    auto issue_a = [&](int g, int w, auto nw) {
+        constexpr int NW = decltype(nw)::value;
+        const int t = tile_of(g), b = net_of(t);
+        const float *src = A + ((int64_t)b * m + (int64_t)(t - b * tiles_per_net) * XBM) * XK +
+                           (g & 7) * XBK;
+        uint8_t *dst = sh + LDS_A32 + (g % 3) * A32_STAGE;
+#pragma unroll
+        for (int q = 0; q < A32_STAGE / 1024 / NW; ++q) {
+            const int ins = w + NW * q;          // NW even: ins & 1 == w & 1
+            glds16_s(src + (int64_t)ins * 8 * XK, voff_a[w & 1], lds_addr(dst + ins * 1024));
+        }
+    };
+    using N4 = std::integral_constant<int, 4>;
+    using N8 = std::integral_constant<int, 8>;
+
+    const int fr = lane & 31, fh = lane >> 5;
+    int a_off[2][2][2], b_off[2][2];
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            a_off[i][s][0] = swz32(wm * 64 + i * 32 + fr, 4 * s + 2 * fh);
+            a_off[i][s][1] = swz32(wm * 64 + i * 32 + fr, 4 * s + 2 * fh + 1);
+        }
+#pragma unroll
+        for (int j = 0; j < 2; ++j) b_off[j][s] = swz(wn * 64 + j * 32 + fr, 2 * s + fh);
+    }
+    bf16x8_t fa[2][3], fb[2][3];           // one step's split A planes and weight planes
+    f32x16_t acc_h[2][2], acc_l[2][2];
+    auto zero_acc = [&]() {
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                acc_h[i][j] = (f32x16_t){};
+                acc_l[i][j] = (f32x16_t){};
+            }
+    };
+    // fragments of k16 step u: f32 A rows (split here) and the weight planes
+    auto prep = [&](int u) {
+        const int g = u >> 1, s = u & 1;
+        const uint8_t *SA = sh + LDS_A32 + (g % 3) * A32_STAGE;
+        const uint8_t *SB = sh + LDS_WB + (g & 1) * B_STAGE;
+        float4 ra[2][2];
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            ra[i][0] = *reinterpret_cast<const float4 *>(SA + a_off[i][s][0]);
+            ra[i][1] = *reinterpret_cast<const float4 *>(SA + a_off[i][s][1]);
+        }
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int p = 0; p < 3; ++p)
+                fb[j][p] = *reinterpret_cast<const bf16x8_t *>(SB + p * B_PLANE + b_off[j][s]);
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            const float x[8] = {ra[i][0].x, ra[i][0].y, ra[i][0].z, ra[i][0].w,
+                                ra[i][1].x, ra[i][1].y, ra[i][1].z, ra[i][1].w};
+            u32x4_t h, mm, l;
+            split8(x, h, mm, l);
+            fa[i][0] = __builtin_bit_cast(bf16x8_t, h);
+            fa[i][1] = __builtin_bit_cast(bf16x8_t, mm);
+            fa[i][2] = __builtin_bit_cast(bf16x8_t, l);
+        }
+    };
+    // the products of gemm_x6_kernel's mfma_step, in its order
+    auto mfma = [&]() {
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                const bf16x8_t *w = fb[j];
+                acc_h[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w[0], fa[i][0],
+                                                                      acc_h[i][j], 0, 0, 0);
+                f32x16_t &t = acc_l[i][j];
+                t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w[1], fa[i][0], t, 0, 0, 0);
+                t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w[0], fa[i][1], t, 0, 0, 0);
+                t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w[2], fa[i][0], t, 0, 0, 0);
+                t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w[0], fa[i][2], t, 0, 0, 0);
+                t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w[1], fa[i][1], t, 0, 0, 0);
+            }
+    };
+    // the group's rows of the tile that stage g belongs to (16 float4 per lane)
+    auto epilogue = [&](int g) {
+        const int t = tile_of(g), b = net_of(t);
+        float *Cb = C + ((int64_t)b * m + (int64_t)(t - b * tiles_per_net) * XBM) * XN;
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                const f32x16_t v = acc_h[i][j] + acc_l[i][j];
+                float *c = Cb + (int64_t)(wm * 64 + i * 32 + fr) * XN + wn * 64 + j * 32 + 4 * fh;
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const float4 o = make_float4(v[4 * q], v[4 * q + 1], v[4 * q + 2],
+                                                 v[4 * q + 3]);
+                    if (nt)
+                        store_nt(reinterpret_cast<float4 *>(c + 8 * q), o);
+                    else
+                        *reinterpret_cast<float4 *>(c + 8 * q) = o;
+                }
+            }
+    };
+    auto bar = [&]() {
+        __builtin_amdgcn_sched_barrier(0);
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
+    };
+
+    // prologue: stages 0, 1 (image and A rows) and the A rows of 2, by all
+    // eight waves, all landed
+    issue_b(0, wid, N8{});
+    issue_a(0, wid, N8{});
+    issue_b(1, wid, N8{});
+    issue_a(1, wid, N8{});
+    issue_a(2, wid, N8{});
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    zero_acc();
+    bar();
+    // Each group runs its own straight-line loop (one k16 step u per
+    // iteration: a prep interval and an MFMA interval), so the register
+    // allocator sees one fragment set and one accumulator set per path; both
+    // loops end 2U + 1 intervals after the prologue barrier.
+    if (grp == 0) {
+        for (int u = 0; u < U; ++u) {
+            X6_STAMP(u, 0);
+            // interval 2u - 1: the image of stage u/2 + 1 (u even >= 2, i.e.
+            // 4g + 3 with g = u/2 - 1), this step's fragments, then the
+            // stores of a tile whose last step was u - 1
+            if ((u & 1) == 0 && u >= 2 && (u >> 1) + 1 < G) issue_b((u >> 1) + 1, wq, N4{});
+            prep(u);
+            if (u >= 16 && (u & 15) == 0) {
+                epilogue((u - 1) >> 1);
+                zero_acc();
+            }
+            X6_STAMP(u, 1);
+            bar();
+            X6_STAMP(u, 2);
+            // interval 2u: MFMA(u); for odd u = 2h + 1 it is interval 4h + 2:
+            // wait for the image of stage h + 1 (issued in iteration 2h;
+            // younger: that iteration's tile stores, h % 8 == 0, h >= 8)
+            mfma();
+            if (u & 1) {
+                const int h = (u - 1) >> 1;
+                __builtin_amdgcn_sched_barrier(0);
+                if (h >= 8 && (h & 7) == 0)
+                    asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+                else
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            }
+            X6_STAMP(u, 3);
+            bar();
+        }
+        // interval 2U - 1: the last tile's rows
+        epilogue(G - 1);
+        bar();
+    } else {
+        bar();                                   // interval -1
+        for (int u = 0; u < U; ++u) {
+            X6_STAMP(u, 0);
+            // interval 2u: the A rows of stage u/2 + 2 (u even >= 2, i.e.
+            // 4g + 4 with g = u/2 - 1), this step's fragments, a finished
+            // tile's stores
+            if ((u & 1) == 0 && u >= 2 && (u >> 1) + 2 < G) issue_a((u >> 1) + 2, wq, N4{});
+            prep(u);
+            if (u >= 16 && (u & 15) == 0) {
+                epilogue((u - 1) >> 1);
+                zero_acc();
+            }
+            if (u & 1) {
+                // interval 4h + 2 (u = 2h + 1): wait for the A rows of stage
+                // h + 1 (issued in iteration 2h - 2); younger: the A rows of
+                // iteration 2h (stage h + 2, h >= 1) and the tile stores of
+                // iteration 2h - 2 (h % 8 == 1, h >= 9) or 2h (h % 8 == 0, h >= 8)
+                const int h = (u - 1) >> 1;
+                const bool st = (h >= 9 && (h & 7) == 1) || (h >= 8 && (h & 7) == 0);
+                const bool a2 = h >= 1 && h + 2 < G;
+                __builtin_amdgcn_sched_barrier(0);
+                if (st && a2)
+                    asm volatile("s_waitcnt vmcnt(20)" ::: "memory");
+                else if (st)
+                    asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+                else if (a2)
+                    asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+                else
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            }
+            X6_STAMP(u, 1);
+            bar();
+            X6_STAMP(u, 2);
+            mfma();                              // interval 2u + 1
+            X6_STAMP(u, 3);
+            bar();
+        }
+        epilogue(G - 1);
     }
 }
 
@@ -1055,9 +1335,21 @@ int dr_gemm_x6(int64_t batch, int64_t m, const float *a, const void *img, float 
         const char *e = getenv("DRONERL_X6_NT");
         return e && e[0] == '1' ? 1 : 0;
     }();
-    hipLaunchKernelGGL(gemm_x6_kernel<false>, dim3(grid), dim3(XTHREADS), 0,
-                       static_cast<hipStream_t>(stream), a, static_cast<const uint8_t *>(img),
-                       c, m, ntiles, nt, nullptr, nullptr, nullptr);
+    // DRONERL_X6_PP=1 (A/B knob, read once): the ping-pong schedule
+    // (measured slower: 143-148 vs 121-125 us)
+    static const int pp = [] {
+        const char *e = getenv("DRONERL_X6_PP");
+        return e && e[0] == '1' ? 1 : 0;
+    }();
+    if (pp)
+        hipLaunchKernelGGL(gemm_x6_pp_kernel, dim3(grid), dim3(XTHREADS), 0,
+                           static_cast<hipStream_t>(stream), a,
+                           static_cast<const uint8_t *>(img), c, m, ntiles, nt);
+    else
+        hipLaunchKernelGGL(gemm_x6_kernel<false>, dim3(grid), dim3(XTHREADS), 0,
+                           static_cast<hipStream_t>(stream), a,
+                           static_cast<const uint8_t *>(img), c, m, ntiles, nt, nullptr,
+                           nullptr, nullptr);
     const hipError_t e = hipGetLastError();
     return e == hipSuccess
                ? DR_OK

@@ -2,7 +2,10 @@
 (s_memtime, shader clock): for blocks 0-7, every wave, stages 0-63:
   a = MFMA step 0 issued (from stage start), b = wait + barrier,
   c = step-1 fragment reads issued + MFMA step 1 issued.
-Usage: python scripts/micro/gemm_x6_stamps.py path/to/lib.so"""
+Usage: python scripts/micro/gemm_x6_stamps.py path/to/lib.so [pp]
+pp: the ping-pong kernel's stamps (per k16 step u: 0 = start, 1 = first
+interval's work done, 2 = after its barrier, 3 = second interval's work
+done; group A = waves 0-3 prep then MFMA, group B = waves 4-7 MFMA then prep)."""
 import ctypes
 import os
 import sys
@@ -33,6 +36,19 @@ torch.cuda.synchronize()
 buf = np.zeros(8 * 8 * 64 * 4, np.uint64)
 assert L.dr_x6_diag_stamps(buf.ctypes.data, buf.nbytes) == 0
 st = buf.reshape(8, 8, 64, 4).astype(np.int64)
+if len(sys.argv) > 2 and sys.argv[2] == "pp":
+    U = 64
+    w1 = st[..., 1] - st[..., 0]            # first interval's work
+    b1 = st[..., 2] - st[..., 1]            # first barrier wait
+    w2 = st[..., 3] - st[..., 2]            # second interval's work
+    b2 = st[:, :, 1:, 0] - st[:, :, :-1, 3]  # second barrier wait (to the next step)
+    for name, sl in (("A (prep | MFMA)", slice(0, 4)), ("B (MFMA | prep)", slice(4, 8))):
+        print(f"group {name}: work1 {np.median(w1[:, sl, 2:]):.0f}  bar1 {np.median(b1[:, sl, 2:]):.0f}  "
+              f"work2 {np.median(w2[:, sl, 2:]):.0f}  bar2 {np.median(b2[:, sl, 2:]):.0f}  "
+              f"(p90 work1 {np.percentile(w1[:, sl, 2:], 90):.0f}, work2 {np.percentile(w2[:, sl, 2:], 90):.0f})")
+    step = st[:, :, 1:, 0] - st[:, :, :-1, 0]
+    print(f"cycles per k16 step (median): {np.median(step):.0f}; MFMA-only per SIMD per step: 1536")
+    sys.exit(0)
 G = 32
 st = st[:, :, :G]
 a = st[..., 1] - st[..., 0]
