@@ -50,9 +50,10 @@ BYTES_PER_ENV_STEP = {"f64": 305, "f32": 197}
 # moving-target variant: + 9 f32 motion params read, + 3 f32 obs written
 BYTES_PER_ENV_STEP_MOVING = {"f64": 353, "f32": 245}
 HBM_PEAK_GBS = 8000.0      # MI355X HBM3E spec (MI355X_MICROARCH.md)
-# SQ_ACTIVE_INST_VALU / SQ_WAVE_CYCLES of the K = 32 rollout kernel at 65,536
-# envs (profiles/r02_pmc_rollout.json): one wave per SIMD, latency-bound
-PMC_ROLLOUT_VALU_ACTIVE = {"actions_from_hbm": 0.481, "random_policy_in_kernel": 0.502}
+# SQ_ACTIVE_INST_VALU over the physics waves' share of SQ_WAVE_CYCLES of the
+# K = 32 rollout kernel at 65,536 envs (profiles/r03_pmc_rollout.json, the
+# warp-specialised kernel; an upper bound, the memory waves' VALU included)
+PMC_ROLLOUT_VALU_ACTIVE = {"actions_from_hbm": 0.54, "random_policy_in_kernel": 0.644}
 
 
 def parse():
@@ -620,7 +621,7 @@ def main():
         roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                 "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": tr,
                 "traffic_GBs": round(tr / per_launch_s / 1e9, 1) if tr else None,
-                "kernel": "env_rollout_kernel", "steps_per_launch": kh, "launches": launches,
+                "kernel": "env_rollout_ws_kernel", "steps_per_launch": kh, "launches": launches,
                 "bytes_per_env_step": round(bpe, 2),
                 "bytes_basis": "per env-step 16 action + 60 obs + 4 reward + 1 done; per "
                                "launch and env the f64 state read (124 B) and written (100 B) "
@@ -631,8 +632,9 @@ def main():
                 # kernel alone, without the event records' queue time
                 "avg_launch_us_packet": (round(packet_ms / launches * 1e3, 3)
                                          if packet_ms else None),
-                "limiter": "latency at one wave per SIMD (VALU active 0.48 of wave cycles, "
-                           "profiles/r02_pmc_rollout.json)"}
+                "limiter": "the physics waves' f64 step at one physics wave per SIMD "
+                           "(memory waves stream the outputs beside them; with no physics "
+                           "the stream alone takes ~31 us per 32 steps, DESIGN.md section 3)"}
     else:
         elapsed, gpu_ms, ep = el_s, gm_s, ep_s
         roof = single["roofline"]
@@ -691,7 +693,7 @@ def main():
         # (bitwise the K single steps; tests/test_rollout_gpu.py)
         k, sb = args.rollout_k, (8 if args.state_dtype == "f64" else 4)
         state_b = (15 * sb + 4) + (12 * sb + 4)   # state in + out once per launch
-        ro = {"kernel": "env_rollout_kernel", "k": k, "envs": N, "launches": 10}
+        ro = {"kernel": "env_rollout_ws_kernel", "k": k, "envs": N, "launches": 10}
         for gen in (False, True):
             pl = time_rollout(args, N, device, k, 10, gen)
             bpe = (65 if gen else 81) + state_b / k

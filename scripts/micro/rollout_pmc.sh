@@ -1,7 +1,10 @@
 #!/bin/bash
 # PMC passes over scripts/micro/rollout_bench.py at 65,536 envs, K = 32
 # (one counter group per run): VALU instruction count and issue occupancy
-# of env_rollout_kernel.
+# of the rollout kernel (env_rollout_ws_kernel: half its waves are memory
+# waves, so the per-physics-wave figures divide by SQ_WAVES / 2 and count
+# the memory waves' few VALU too -- upper bounds; env_rollout_kernel with
+# DRONERL_ROLLOUT_WS=0).
 cd "$(dirname "$0")/../.."
 OUT=$PWD/gpurun_out/pmc_rollout
 mkdir -p "$OUT"
@@ -16,23 +19,30 @@ for grp in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY 
   if [ $rc -ne 0 ]; then tail -5 "$OUT/p$i.log"; exit $rc; fi
 done
 python3 - "$OUT" <<'PY'
-import csv, glob, json, sys, collections
+import csv, glob, json, re, sys, collections
 out = sys.argv[1]
 res = {"workload": "scripts/micro/rollout_bench.py --envs 65536 --ks 32 --reps 5 (f64 gym, "
                    "one action set), rocprofv3 --pmc, two passes (scripts/micro/rollout_pmc.sh)"}
-for tag in ("64, false>", "64, true>"):   # actions from HBM / in-kernel random policy
+for tag in ("false", "true"):   # actions from HBM / in-kernel random policy
     acc = collections.defaultdict(list)
+    ws = False
+    pat = re.compile(r"env_rollout(_ws)?_kernel<double, 0, (64, )?" + tag + ">")
     for f in glob.glob(out + "/p*/run_counter_collection.csv"):
         for r in csv.DictReader(open(f)):
-            if "env_rollout_kernel<double, 0, " + tag in r["Kernel_Name"]:
+            mt = pat.search(r["Kernel_Name"])
+            if mt:
+                ws = ws or bool(mt.group(1))
                 acc[r["Counter_Name"]].append(float(r["Counter_Value"]))
     m = {k: sum(v) / len(v) for k, v in acc.items()}
     w, K = m["SQ_WAVES"], 32
-    res["random_policy_in_kernel" if "true" in tag else "actions_from_hbm"] = {
+    pw = w / 2 if ws else w                 # physics waves
+    res["random_policy_in_kernel" if tag == "true" else "actions_from_hbm"] = {
+        "kernel": "env_rollout_ws_kernel" if ws else "env_rollout_kernel",
         "counters_per_launch": {k: round(v, 1) for k, v in sorted(m.items())},
-        "valu_insts_per_wave_step": round(m["SQ_INSTS_VALU"] / w / K, 1),
-        "salu_insts_per_wave_step": round(m["SQ_INSTS_SALU"] / w / K, 1),
-        "valu_active_frac_of_wave_cycles": round(m["SQ_ACTIVE_INST_VALU"] / m["SQ_WAVE_CYCLES"], 3),
+        "valu_insts_per_wave_step": round(m["SQ_INSTS_VALU"] / pw / K, 1),
+        "salu_insts_per_wave_step": round(m["SQ_INSTS_SALU"] / pw / K, 1),
+        "valu_active_frac_of_wave_cycles": round(m["SQ_ACTIVE_INST_VALU"] /
+                                                 (m["SQ_WAVE_CYCLES"] * pw / w), 3),
         "any_active_frac": round(m["SQ_ACTIVE_INST_ANY"] / m["SQ_WAVE_CYCLES"], 3),
         "wait_any_frac": round(m["SQ_WAIT_ANY"] / m["SQ_WAVE_CYCLES"], 3),
         "wait_inst_any_frac": round(m["SQ_WAIT_INST_ANY"] / m["SQ_WAVE_CYCLES"], 3),

@@ -20,7 +20,7 @@ def avg(path, counter):
     vals = []
     for f in glob.glob(os.path.join(path, "**", "*counter_collection.csv"), recursive=True):
         for r in csv.DictReader(open(f)):
-            if "env_rollout_kernel" in r["Kernel_Name"] and r["Counter_Name"] == counter:
+            if "env_rollout" in r["Kernel_Name"] and r["Counter_Name"] == counter:
                 vals.append(float(r["Counter_Value"]))
     if not vals:
         raise SystemExit(f"no {counter} rows under {path}")
