@@ -2053,11 +2053,26 @@ int launch_rollout(dr_handle *h, const RolloutIO &io, hipStream_t st, hipEvent_t
         const char *r = std::getenv("DRONERL_ROLLOUT_RPW");
         return r && std::atoi(r) == 32 ? 32 : 64;
     }();
-    // the warp-specialised form unless DRONERL_ROLLOUT_WS=0 or rpw 32 (A/B)
-    static const bool ws = [] {
+    // The warp-specialised form while its grid is at most one block per CU
+    // (n <= 256 x CUs: 65,536 envs on MI355X), where one physics wave per
+    // SIMD has nothing else to overlap with; above that the one-role kernel
+    // already runs two or more waves per SIMD, and the warp-specialised one
+    // measured equal (gym, 131,072 / 1,048,576 envs) or slower (in-kernel
+    // policy at 2^20; the moving variant, whose 175 VGPRs fit one 512-thread
+    // block per CU).  DRONERL_ROLLOUT_WS=0 / 1 forces either (A/B).
+    static const int ws_env = [] {
         const char *r = std::getenv("DRONERL_ROLLOUT_WS");
-        return !(r && std::atoi(r) == 0);
+        return r ? (std::atoi(r) != 0 ? 1 : 0) : -1;
     }();
+    static const int n_cu = [] {
+        int dev = 0, c = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+            c < 1)
+            c = 256;
+        return c;
+    }();
+    const bool ws = ws_env >= 0 ? ws_env == 1 : h->n <= (int64_t)kWsEnvs * n_cu;
     // with events: hipExtLaunchKernelGGL binds them to the dispatch packet's
     // own start / end timestamps (no extra packets in the queue)
     if (ws && rpw == 64) {
