@@ -198,3 +198,24 @@ def test_rollout_timed_same_outputs_and_packet_events():
     o3, r3, d3 = a.rollout(K, acts)
     torch.cuda.synchronize()
     assert torch.equal(o3, o2) and torch.equal(r3, r2) and torch.equal(d3, d2)
+
+
+@pytest.mark.parametrize("ws,variant,n", [
+    ("1", "gym", 131072 + 320),     # warp-specialised form at two blocks per CU, ragged
+    ("1", "moving", 70000),         # warp-specialised moving variant above one block per CU
+    ("0", "gym", 65536),            # the one-role kernel where the default is warp-specialised
+])
+def test_rollout_forms_outside_their_default(ws, variant, n):
+    """Both kernel forms of dr_rollout stay bitwise equal to K dr_step launches
+    in the regimes the size rule does not pick them for (DRONERL_ROLLOUT_WS
+    forces a form; it is read once per process, hence the subprocess)."""
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, DRONERL_ROLLOUT_WS=ws, PYTHONPATH=root)
+    r = subprocess.run([sys.executable, os.path.join(root, "tests", "rollout_form_worker.py"),
+                        variant, str(n), "37"], env=env, capture_output=True, text=True,
+                       timeout=100)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    assert "ok" in r.stdout
