@@ -915,6 +915,234 @@ __global__ __launch_bounds__(XTHREADS) void gemm_x6_pp_kernel(const float *__res
 }
 
 // ---------------------------------------------------------------------------
+// Cooperative-split form of gemm_x6_kernel<false> (dr_gemm_x6's default;
+// DRONERL_X6_CS=0 restores gemm_x6_kernel).  The same tiles, weight image and
+// per-output MFMA order, so bitwise the same C.
+//
+// In gemm_x6_kernel every wave splits the f32 A fragments it reads, and the
+// four waves that share a row half split the same values: 176 VALU per wave
+// and stage beside its 48 MFMAs, on a SIMD whose vector issue the MFMAs, the
+// LDS-DMA and the fragment reads also need (the stamps of the ping-pong form
+// above).  Here the block splits each A stage once: every wave moves 16 rows
+// of the f32 stage by LDS-DMA into its own part of one 16-KB A32 buffer and
+// splits exactly those rows (8 k per lane), writing the three planes into a
+// double-buffered plane image in the weight image's layout (row r, 16-B
+// chunk c at swz(r, c)); the waves then read bf16 plane fragments (6
+// ds_read_b128 per k16 step instead of 4 f32 reads and 88 VALU).  No wave
+// reads another wave's A32 rows, so that buffer needs no barrier: the wave's
+// own vmcnt orders its reads behind its DMA.  LDS: the image ring (2 x 48
+// KB) + the plane ring (2 x 24 KB) + A32 (16 KB) = 160 KB.
+//
+// Iteration g (stage g), per wave:
+//   1. split stage g + 1 (its A rows issued in iteration g - 1, waited by a
+//      hand count) into planes (g + 1) & 1, read by nobody since the barrier
+//      that ended iteration g - 1 (they held stage g - 1)
+//   2. fragments of step 1 of stage g; MFMAs of step 0
+//   3. wait: image g + 1 landed; plane writes and fragment reads done;
+//      barrier B_g
+//   4. LDS-DMA: A rows of stage g + 2, then image g + 2 into slot g & 1
+//   5. fragments of step 0 of stage g + 1; MFMAs of step 1 of stage g
+//   6. after a tile's last stage: its 16 float4 stores
+// Measured: 117-121 vs 124-128 us for both nets at 65,536 rows.
+// ---------------------------------------------------------------------------
+constexpr int CS_PLANE = XBM * 64;                   // 8 KB: 128 rows x 32 bf16
+constexpr int CS_STAGE = 3 * CS_PLANE;               // 24 KB
+constexpr int CS_LDS_AP = 2 * B_STAGE;               // the plane ring after the image ring
+constexpr int CS_LDS_A32 = 2 * B_STAGE + 2 * CS_STAGE;  // one f32 A stage (16 KB) after it
+constexpr int CS_LDS = CS_LDS_A32 + A32_STAGE;       // 160 KB: all of the CU's LDS
+
+__global__ __launch_bounds__(XTHREADS) void gemm_x6_cs_kernel(const float *__restrict__ A,
+                                                              const uint8_t *__restrict__ img,
+                                                              float *__restrict__ C, int64_t m,
+                                                              int ntiles, int nt) {
+    static_assert(XWAVES == 8, "512-thread blocks: one split unit (row, 8 k) per thread");
+    __shared__ __attribute__((aligned(16))) uint8_t sh[CS_LDS];
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wm = wid >> 2, wn = wid & 3;
+    const int tiles_per_net = (int)(m / XBM);
+    const int nmine = (ntiles - (int)blockIdx.x + (int)gridDim.x - 1) / (int)gridDim.x;
+    const int G = nmine * XKC;
+
+    auto tile_of = [&](int g) { return (int)blockIdx.x + (g >> 3) * (int)gridDim.x; };
+    auto net_of = [&](int t) { return t / tiles_per_net; };
+    const uint32_t voff_b = (uint32_t)lane * 16;
+    auto issue_b = [&](int g) {
+        const uint8_t *src = img + (int64_t)net_of(tile_of(g)) * W_IMG + (g & 7) * B_STAGE;
+        uint8_t *dst = sh + LDS_WB + (g & 1) * B_STAGE;
+#pragma unroll
+        for (int q = 0; q < B_STAGE / 1024 / XWAVES; ++q) {
+            const int ins = wid + XWAVES * q;
+            glds16_s(src + ins * 1024, voff_b, lds_addr(dst + ins * 1024));
+        }
+    };
+    // A: each wave moves 16 rows of the f32 stage by LDS-DMA (pieces wid and
+    // wid + 8: rows 8 wid .. + 7 and 64 + 8 wid .. + 7, the A32 layout of
+    // gemm_x6_kernel) into the one A32 buffer and splits exactly those rows,
+    // so no other wave reads them: its own vmcnt orders its reads behind its
+    // own DMA, no barrier.  Lane L: row sr (L < 32: the first piece), k
+    // chunk sc (8 k = f32 chunks 2 sc, 2 sc + 1).
+    const int sr = (lane < 32 ? 8 * wid : 64 + 8 * wid) + ((lane & 31) >> 2), sc = lane & 3;
+    uint32_t voff_a[2];
+#pragma unroll
+    for (int par = 0; par < 2; ++par) {
+        const int chunk = (lane & 7) ^ (((lane >> 4) + 4 * par) & 7);
+        voff_a[par] = (uint32_t)(((lane >> 3) * XK + chunk * 4) * 4);
+    }
+    auto issue_a = [&](int g) {
+        const int t = tile_of(g), b = net_of(t);
+        const float *src = A + ((int64_t)b * m + (int64_t)(t - b * tiles_per_net) * XBM) * XK +
+                           (g & 7) * XBK;
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+            const int ins = wid + XWAVES * q;
+            glds16_s(src + (int64_t)ins * 8 * XK, voff_a[ins & 1],
+                     lds_addr(sh + CS_LDS_A32 + ins * 1024));
+        }
+    };
+    auto split_stage = [&](int g) {
+        const uint8_t *SA = sh + CS_LDS_A32;
+        const float4 v0 = *reinterpret_cast<const float4 *>(SA + swz32(sr, 2 * sc));
+        const float4 v1 = *reinterpret_cast<const float4 *>(SA + swz32(sr, 2 * sc + 1));
+        const float x[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
+        u32x4_t h, mm, l;
+        split8(x, h, mm, l);
+        uint8_t *dst = sh + CS_LDS_AP + (g & 1) * CS_STAGE + swz(sr, sc);
+        *reinterpret_cast<u32x4_t *>(dst) = h;
+        *reinterpret_cast<u32x4_t *>(dst + CS_PLANE) = mm;
+        *reinterpret_cast<u32x4_t *>(dst + 2 * CS_PLANE) = l;
+    };
+
+    const int fr = lane & 31, fh = lane >> 5;
+    int a_off[2][2], b_off[2][2];
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+#pragma unroll
+        for (int i = 0; i < 2; ++i) a_off[i][s] = swz(wm * 64 + i * 32 + fr, 2 * s + fh);
+#pragma unroll
+        for (int j = 0; j < 2; ++j) b_off[j][s] = swz(wn * 64 + j * 32 + fr, 2 * s + fh);
+    }
+    struct Frag {
+        bf16x8_t a[2][3];
+        bf16x8_t b[2][3];
+    };
+    auto read_frag = [&](int g, int s, Frag &f) {
+        const uint8_t *SA = sh + CS_LDS_AP + (g & 1) * CS_STAGE;
+        const uint8_t *SB = sh + LDS_WB + (g & 1) * B_STAGE;
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int p = 0; p < 3; ++p)
+                f.a[i][p] = *reinterpret_cast<const bf16x8_t *>(SA + p * CS_PLANE + a_off[i][s]);
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int p = 0; p < 3; ++p)
+                f.b[j][p] = *reinterpret_cast<const bf16x8_t *>(SB + p * B_PLANE + b_off[j][s]);
+    };
+    f32x16_t acc_h[2][2], acc_l[2][2];
+    auto zero_acc = [&]() {
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                acc_h[i][j] = (f32x16_t){};
+                acc_l[i][j] = (f32x16_t){};
+            }
+    };
+    auto mfma_step = [&](const Frag &f) {
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                const bf16x8_t *w = f.b[j];
+                const bf16x8_t *fa = f.a[i];
+                acc_h[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w[0], fa[0], acc_h[i][j],
+                                                                      0, 0, 0);
+                f32x16_t t = acc_l[i][j];
+                t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w[1], fa[0], t, 0, 0, 0);
+                t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w[0], fa[1], t, 0, 0, 0);
+                t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w[2], fa[0], t, 0, 0, 0);
+                t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w[0], fa[2], t, 0, 0, 0);
+                t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w[1], fa[1], t, 0, 0, 0);
+                acc_l[i][j] = t;
+            }
+    };
+    auto epilogue = [&](int g) {
+        const int t = tile_of(g), b = net_of(t);
+        float *Cb = C + ((int64_t)b * m + (int64_t)(t - b * tiles_per_net) * XBM) * XN;
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                const f32x16_t v = acc_h[i][j] + acc_l[i][j];
+                float *c = Cb + (int64_t)(wm * 64 + i * 32 + fr) * XN + wn * 64 + j * 32 + 4 * fh;
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const float4 o = make_float4(v[4 * q], v[4 * q + 1], v[4 * q + 2],
+                                                 v[4 * q + 3]);
+                    if (nt)
+                        store_nt(reinterpret_cast<float4 *>(c + 8 * q), o);
+                    else
+                        *reinterpret_cast<float4 *>(c + 8 * q) = o;
+                }
+            }
+    };
+
+    // prologue: A(0), images 0 and 1; split stage 0; A(1); image 0 and
+    // planes 0 visible
+    issue_a(0);
+    issue_b(0);
+    issue_b(1);
+    asm volatile("s_waitcnt vmcnt(12)" ::: "memory");     // A(0): younger 2 x 6 image
+    split_stage(0);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");    // A32 read before A(1) lands
+    issue_a(1);
+    asm volatile("s_waitcnt vmcnt(8) lgkmcnt(0)\n\ts_barrier" ::: "memory");   // image 0
+    zero_acc();
+    Frag f0, f1;
+    read_frag(0, 0, f0);
+    for (int g = 0; g < G; ++g) {
+        // split first (only f0 live beside the accumulators).  This wave's
+        // A(g + 1) pieces were issued in iteration g - 1 right after its
+        // barrier, before image g + 1 (6) and that iteration's tile stores
+        // (16 after a tile's last stage); in the prologue after everything
+        if (g + 1 < G) {
+            const bool epi_prev = (g & 7) == 0 && g > 0;
+            __builtin_amdgcn_sched_barrier(0);
+            if (g == 0)
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            else if (epi_prev)
+                asm volatile("s_waitcnt vmcnt(22)" ::: "memory");
+            else
+                asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+            split_stage(g + 1);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        read_frag(g, 1, f1);
+        mfma_step(f0);
+        // image g + 1 (issued in iteration g - 1 after A(g + 1)); younger:
+        // that iteration's tile stores (16 after a tile's last stage).  The
+        // lgkmcnt(0) also retires this wave's A32 reads before its next DMA
+        const bool epi_prev = (g & 7) == 0 && g > 0;
+        __builtin_amdgcn_sched_barrier(0);
+        if (epi_prev)
+            asm volatile("s_waitcnt vmcnt(16) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        else
+            asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        if (g + 2 < G) issue_a(g + 2);
+        if (g + 2 < G) issue_b(g + 2);
+        read_frag(g + 1 < G ? g + 1 : g, 0, f0);
+        __builtin_amdgcn_sched_barrier(0);
+        mfma_step(f1);
+        if ((g & 7) == 7) {
+            epilogue(g);
+            zero_acc();
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
 // Half-width variant: 256-thread blocks own 128 rows x 128 columns (one
 // column half of the output), 80 KB of LDS, so TWO blocks share a CU and the
 // two waves on each SIMD come from different blocks: no common barrier keeps
@@ -1341,7 +1569,17 @@ int dr_gemm_x6(int64_t batch, int64_t m, const float *a, const void *img, float 
         const char *e = getenv("DRONERL_X6_PP");
         return e && e[0] == '1' ? 1 : 0;
     }();
-    if (pp)
+    // the cooperative-split form unless DRONERL_X6_CS=0 (A/B knob, read
+    // once): 117-121 vs 124-128 us at 65,536 rows (scripts/micro/gemm_x6_bench.py)
+    static const int cs = [] {
+        const char *e = getenv("DRONERL_X6_CS");
+        return e && e[0] == '0' ? 0 : 1;
+    }();
+    if (cs)
+        hipLaunchKernelGGL(gemm_x6_cs_kernel, dim3(grid), dim3(XTHREADS), 0,
+                           static_cast<hipStream_t>(stream), a,
+                           static_cast<const uint8_t *>(img), c, m, ntiles, nt);
+    else if (pp)
         hipLaunchKernelGGL(gemm_x6_pp_kernel, dim3(grid), dim3(XTHREADS), 0,
                            static_cast<hipStream_t>(stream), a,
                            static_cast<const uint8_t *>(img), c, m, ntiles, nt);
