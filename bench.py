@@ -481,7 +481,7 @@ def ppo_roofline(cfg, s_per_update, ktimes):
                     "the f32 matrix peak",
            "kernels_per_minibatch": kern}
     if x6 is not None:
-        out["dominant_kernel"] = {"kernel": "gemm_x6_kernel (forward)", "bound": "mfma",
+        out["dominant_kernel"] = {"kernel": "gemm_x6_cs_kernel (forward)", "bound": "mfma",
                                   "achieved": x6["bf16_mfma_tflops"],
                                   "peak": BF16_DENSE_PEAK_TFLOPS, "unit": "TFLOP/s",
                                   "frac": x6["frac"]}

@@ -14,19 +14,20 @@ for grp in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY 
   if [ $rc -ne 0 ]; then tail -5 "$OUT/p$i.log"; exit $rc; fi
 done
 python3 - "$OUT" <<'PY'
-import csv, glob, json, sys, collections
+import csv, glob, json, re, sys, collections
 out = sys.argv[1]
 acc = collections.defaultdict(list)
 for f in glob.glob(out + "/p*/run_counter_collection.csv"):
     for r in csv.DictReader(open(f)):
-        if "gemm_x6_kernel" in r["Kernel_Name"]:
+        if re.search(r"gemm_x6_(cs_)?kernel", r["Kernel_Name"]):
             acc[r["Counter_Name"]].append(float(r["Counter_Value"]))
 m = {k: sum(v) / len(v) for k, v in acc.items()}
 for k, v in sorted(m.items()):
     print(f"{k:28s} {v:.4g}  (n={len(acc[k])})")
 res = {"workload": "scripts/micro/gemm_x6_bench.py --reps 10 (both nets, 65,536 rows, forward "
                    "and input-gradient forms; cold inputs), rocprofv3 --pmc, two passes "
-                   "(scripts/micro/gemm_x6_pmc.sh); per-dispatch averages of gemm_x6_kernel",
+                   "(scripts/micro/gemm_x6_pmc.sh); per-dispatch averages of dr_gemm_x6's kernel "
+                   "(gemm_x6_cs_kernel, the cooperative-split form, since round 3)",
        "counters_per_dispatch": {k: round(v, 1) for k, v in sorted(m.items())}}
 w = m.get("SQ_WAVE_CYCLES")
 if w:
