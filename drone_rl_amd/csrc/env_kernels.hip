@@ -1204,7 +1204,8 @@ __global__ __launch_bounds__(kEnvBlock) void env_rollout_kernel(EnvView<S> v, Ro
 // ----------------------------------------------------------------------------
 // DR_WS_ABL (diagnostic builds, wrong by construction; timing only):
 // 1 = the memory waves store no outputs; 2 = the physics waves skip the
-// physics (the state only advances by the action's thrust)
+// physics (the state only advances by the action's thrust); 3 = no
+// auto-reset; 4 = no observation formed (zeros staged)
 #ifndef DR_WS_ABL
 #define DR_WS_ABL 0
 #endif
@@ -1441,7 +1442,7 @@ __global__ __launch_bounds__(kWsThreads) void env_rollout_ws_kernel(EnvView<S> v
         step += 1;
         const bool done = live && (crash || (step >= max_steps));
         if constexpr (GYMLIKE) {
-            if (done && io.auto_reset) {
+            if (done && io.auto_reset && DR_WS_ABL != 3) {
                 step = 0;
                 reset_any = true;
                 // a second reset within the group: draw its blocks here (the
@@ -1467,7 +1468,12 @@ __global__ __launch_bounds__(kWsThreads) void env_rollout_ws_kernel(EnvView<S> v
                 if (ep_num % 2000 == 0) eps += 0.1;
             }
         }
-        make_obs<S, OD>(st, ob, tvel);
+        if (DR_WS_ABL == 4) {
+#pragma unroll
+            for (int k = 0; k < OD; ++k) ob[k] = 0.f;
+        } else {
+            make_obs<S, OD>(st, ob, tvel);
+        }
         if (!live) {
 #pragma unroll
             for (int k = 0; k < OD; ++k) ob[k] = 0.f;
