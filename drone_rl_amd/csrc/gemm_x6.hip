@@ -1459,6 +1459,183 @@ __global__ __launch_bounds__(XTHREADS) void gemm_x6_wgrad_kernel(
         }
 }
 
+// ---------------------------------------------------------------------------
+// Cooperative-split form of gemm_x6_wgrad_kernel (A/B form, DRONERL_X6_WCS=1;
+// measured slower: 157 vs 137 us at 65,536 rows, 64 chunks -- the 16-row
+// stages need a barrier per k16 step, and each step's fragment reads wait
+// for that barrier).  The same blocks, output layout and per-output MFMA
+// order (the same six products of the same bf16 planes), so bitwise the
+// same workspace (tests/test_gemm_x6_gpu.py).
+//
+// gemm_x6_wgrad_kernel gathers each fragment with 8 ds_read_b32 and splits it
+// in registers: 32 reads and 176 split VALU per wave and k16 step, each G
+// value split by the four waves of its n half and each H value by two.  Here
+// the block splits every value once, per 16-row stage, into a transposed
+// plane image in the MFMA fragment order (per column: the 16 rows as two
+// 16-B chunks of 8 bf16, the chunks of columns 8-15 mod 16 swapped: reads
+// and writes free of bank conflicts); the waves read 12 ds_read_b128 of
+// planes per step.  A split unit is 8 rows x 1 column (one split8): 768 per
+// stage (128 G + 256 H columns x 2 row groups).  Wave w owns row group
+// w & 1 and 96 of the 384 columns (w >> 1): it moves exactly those f32 values
+// (8 rows x 96 columns, 3 KB: three LDS-DMA pieces) into its own slot of a
+// 2-deep staging ring and splits them (lane L: columns L and, below 32,
+// 64 + L), so no other wave reads its staging: its own vmcnt orders its
+// reads behind its DMA.  LDS: planes 2 x 36 KB + staging 2 x 24 KB = 120 KB.
+//
+// Iteration g (16-row stage g), per wave: fragments of stage g (planes
+// g & 1); split stage g + 1 (its DMA, issued in iteration g - 1, is the only
+// vector-memory op in flight: vmcnt(0)) into planes (g + 1) & 1, which held
+// stage g - 1, read before the barrier that ended iteration g - 1; MFMAs of
+// stage g; lgkmcnt(0) + barrier; LDS-DMA stage g + 2 into staging g & 1
+// (its stage-g values were split in iteration g - 1).
+// ---------------------------------------------------------------------------
+constexpr int WC_BM = 16;                            // rows per stage
+constexpr int WC_GP = 128 * WC_BM * 2;               // 4 KB: one G plane (128 n x 16 rows)
+constexpr int WC_HP = 256 * WC_BM * 2;               // 8 KB: one H plane (256 k x 16 rows)
+constexpr int WC_PSTAGE = 3 * WC_GP + 3 * WC_HP;     // 36 KB of planes per stage
+constexpr int WC_SSLOT = 8 * 96 * 4;                 // 3 KB: one wave's staging slot
+constexpr int WC_SSTAGE = XWAVES * WC_SSLOT;         // 24 KB
+constexpr int WC_LDS_S = 2 * WC_PSTAGE;              // staging ring after the plane ring
+constexpr int WC_LDS = 2 * WC_PSTAGE + 2 * WC_SSTAGE;  // 120 KB
+
+// byte offset of column c's row chunk q (0: rows 0-7, 1: rows 8-15) in a plane
+__device__ inline int wc_off(int c, int q) { return c * 32 + ((q ^ ((c >> 3) & 1)) << 4); }
+
+__global__ __launch_bounds__(XTHREADS) void gemm_x6_wgrad_cs_kernel(
+    const float *__restrict__ Gm, const float *__restrict__ Hm, float *__restrict__ ws,
+    int64_t m, int chunks) {
+    __shared__ __attribute__((aligned(16))) uint8_t sh[WC_LDS];
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wn = wid >> 2, wk = wid & 3;
+    const int chunk = (int)(blockIdx.x % chunks);
+    const int nh = (int)((blockIdx.x / chunks) & 1);
+    const int b = (int)(blockIdx.x / chunks / 2);
+    const int64_t rows = m / chunks;
+    const int G_ = (int)(rows / WC_BM);
+    const float *Gb = Gm + ((int64_t)b * m + (int64_t)chunk * rows) * 256 + nh * 128;
+    const float *Hb = Hm + ((int64_t)b * m + (int64_t)chunk * rows) * 256;
+
+    // this wave's split share: row group rg, global columns 96 q .. + 95
+    // (0-127: G column, 128-383: H column - 128)
+    const int rg = wid & 1, q0 = 96 * (wid >> 1);
+    // DMA: piece p moves the wave's local floats 256 p .. + 255 (8 rows x 96
+    // columns, row-major); lane L's 16 B = local row r, columns j .. j + 3
+    const float *src_p[3];
+#pragma unroll
+    for (int p = 0; p < 3; ++p) {
+        const int f = 256 * p + 4 * lane, r = f / 96, j = f % 96, cg = q0 + j;
+        src_p[p] = cg < 128 ? Gb + (int64_t)(8 * rg + r) * 256 + cg
+                            : Hb + (int64_t)(8 * rg + r) * 256 + (cg - 128);
+    }
+    auto issue = [&](int g) {
+        const int64_t off = (int64_t)g * WC_BM * 256;      // WC_BM rows of 256 floats
+        uint8_t *dst = sh + WC_LDS_S + (g & 1) * WC_SSTAGE + wid * WC_SSLOT;
+#pragma unroll
+        for (int p = 0; p < 3; ++p) glds16(src_p[p] + off, lds_addr(dst + p * 1024));
+    };
+    // split unit u (0: column q0 + lane; 1: column q0 + 64 + lane, lanes < 32)
+    auto split_unit = [&](int g, int jl) {
+        const float *S = reinterpret_cast<const float *>(sh + WC_LDS_S + (g & 1) * WC_SSTAGE +
+                                                         wid * WC_SSLOT);
+        float x[8];
+#pragma unroll
+        for (int r = 0; r < 8; ++r) x[r] = S[r * 96 + jl];
+        u32x4_t h, mm, l;
+        split8(x, h, mm, l);
+        const int cg = q0 + jl;
+        uint8_t *P = sh + (g & 1) * WC_PSTAGE;
+        uint8_t *dst = cg < 128 ? P + wc_off(cg, rg) : P + 3 * WC_GP + wc_off(cg - 128, rg);
+        const int pl = cg < 128 ? WC_GP : WC_HP;
+        *reinterpret_cast<u32x4_t *>(dst) = h;
+        *reinterpret_cast<u32x4_t *>(dst + pl) = mm;
+        *reinterpret_cast<u32x4_t *>(dst + 2 * pl) = l;
+    };
+    auto split_stage = [&](int g) {
+        split_unit(g, lane);
+        if (lane < 32) split_unit(g, 64 + lane);
+    };
+
+    const int fr = lane & 31, fh = lane >> 5;
+    int g_off[2], h_off[2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+        g_off[i] = wc_off(wn * 64 + i * 32 + fr, fh);
+        h_off[i] = 3 * WC_GP + wc_off(wk * 64 + i * 32 + fr, fh);
+    }
+    struct Frag {
+        bf16x8_t g[2][3];
+        bf16x8_t h[2][3];
+    };
+    auto read_frag = [&](int g, Frag &f) {
+        const uint8_t *P = sh + (g & 1) * WC_PSTAGE;
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int p = 0; p < 3; ++p) {
+                f.g[i][p] = *reinterpret_cast<const bf16x8_t *>(P + g_off[i] + p * WC_GP);
+                f.h[i][p] = *reinterpret_cast<const bf16x8_t *>(P + h_off[i] + p * WC_HP);
+            }
+    };
+    f32x16_t acc_h[2][2], acc_l[2][2];                    // [n tile i][k tile j]
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            acc_h[i][j] = (f32x16_t){};
+            acc_l[i][j] = (f32x16_t){};
+        }
+    // gemm_x6_wgrad_kernel's products, in its order
+    auto mfma_step = [&](const Frag &f) {
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                const bf16x8_t *a = f.g[i], *c = f.h[j];
+                acc_h[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], c[0], acc_h[i][j],
+                                                                      0, 0, 0);
+                f32x16_t t = acc_l[i][j];
+                t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], c[1], t, 0, 0, 0);
+                t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], c[0], t, 0, 0, 0);
+                t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], c[2], t, 0, 0, 0);
+                t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[2], c[0], t, 0, 0, 0);
+                t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], c[1], t, 0, 0, 0);
+                acc_l[i][j] = t;
+            }
+    };
+
+    issue(0);
+    issue(1);                                      // G_ >= 2 (checked by the host)
+    asm volatile("s_waitcnt vmcnt(3)" ::: "memory");  // this wave's stage-0 pieces
+    split_stage(0);
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    Frag f;
+    for (int g = 0; g < G_; ++g) {
+        read_frag(g, f);
+        if (g + 1 < G_) {
+            __builtin_amdgcn_sched_barrier(0);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // stage g + 1's pieces
+            split_stage(g + 1);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        mfma_step(f);
+        __builtin_amdgcn_sched_barrier(0);
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        if (g + 2 < G_) issue(g + 2);
+    }
+    // D[n][k]: column k = fr, row n = (r & 3) + 8 (r >> 2) + 4 fh
+    float *out = ws + ((int64_t)b * chunks + chunk) * 256 * 256 + (int64_t)(nh * 128) * 256;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const f32x16_t v = acc_h[i][j] + acc_l[i][j];
+            float *c = out + (int64_t)(wn * 64 + i * 32 + 4 * fh) * 256 + wk * 64 + j * 32 + fr;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) c[((r & 3) + 8 * (r >> 2)) * 256] = v[r];
+        }
+}
+
 // The L1 operands: w0p[b][k] = (W0[b][k][0..15), b0[b][k]) and, when obs is
 // given, obs16[r] = (obs[r][0..15), 0).  One thread per 16-float row.
 __global__ __launch_bounds__(256) void pack_first_kernel(int batch, const float *__restrict__ w0,
@@ -1640,9 +1817,20 @@ int dr_gemm_x6_wgrad(int64_t batch, int64_t m, int64_t chunks, const float *g, c
         return fail_g(DR_ERR_INVALID,
                       "dr_gemm_x6_wgrad: bad arguments (m / chunks a multiple of 32, >= 96; "
                       "pointers 16-byte aligned)");
-    hipLaunchKernelGGL(gemm_x6_wgrad_kernel, dim3((unsigned)(batch * 2 * chunks)),
-                       dim3(XTHREADS), 0, static_cast<hipStream_t>(stream), g, h, ws, m,
-                       (int)chunks);
+    // DRONERL_X6_WCS=1 (A/B knob, read once): the cooperative-split form
+    // (bitwise the same; measured slower, 157 vs 137 us)
+    static const int wcs = [] {
+        const char *e = getenv("DRONERL_X6_WCS");
+        return e && e[0] == '1' ? 1 : 0;
+    }();
+    if (wcs)
+        hipLaunchKernelGGL(gemm_x6_wgrad_cs_kernel, dim3((unsigned)(batch * 2 * chunks)),
+                           dim3(XTHREADS), 0, static_cast<hipStream_t>(stream), g, h, ws, m,
+                           (int)chunks);
+    else
+        hipLaunchKernelGGL(gemm_x6_wgrad_kernel, dim3((unsigned)(batch * 2 * chunks)),
+                           dim3(XTHREADS), 0, static_cast<hipStream_t>(stream), g, h, ws, m,
+                           (int)chunks);
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? DR_OK
                            : fail_g(DR_ERR_HIP, std::string("gemm_x6_wgrad_kernel: ") +

@@ -141,3 +141,27 @@ def test_first_layer_fused_forward_is_bitwise_the_two_launches(m):
     assert torch.equal(obs16[:, :15], obs) and (obs16[:, 15] == 0).all()
     assert torch.equal(h, h_ref)
     assert torch.equal(z, z_ref)
+
+
+@pytest.mark.parametrize("m,chunks", [(128 * 3, 1), (65536, 64)])
+def test_x6_kernel_forms_are_bitwise_equal(m, chunks):
+    """Every launch form of the x6 GEMMs -- the defaults (cooperative-split
+    forward / input-gradient kernel, gemm_x6_wgrad_kernel), gemm_x6_kernel
+    with the cooperative-split weight gradient (DRONERL_X6_CS=0,
+    DRONERL_X6_WCS=1) and the ping-pong form (DRONERL_X6_PP=1) -- gives the
+    same bytes: the same splits and MFMA products in the same order.  The
+    form is chosen once per process, hence one subprocess per form."""
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    digests = []
+    for extra in ({}, {"DRONERL_X6_CS": "0", "DRONERL_X6_WCS": "1"},
+                  {"DRONERL_X6_CS": "0", "DRONERL_X6_PP": "1"}):
+        env = dict(os.environ, PYTHONPATH=root, **extra)
+        r = subprocess.run([sys.executable, os.path.join(root, "tests", "x6_forms_worker.py"),
+                            str(m), str(chunks)], env=env, capture_output=True, text=True,
+                           timeout=100)
+        assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+        digests.append([l for l in r.stdout.splitlines() if l.startswith("sha")][0])
+    assert digests[0] == digests[1] == digests[2], digests
