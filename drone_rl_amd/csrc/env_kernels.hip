@@ -1205,7 +1205,8 @@ __global__ __launch_bounds__(kEnvBlock) void env_rollout_kernel(EnvView<S> v, Ro
 // DR_WS_ABL (diagnostic builds, wrong by construction; timing only):
 // 1 = the memory waves store no outputs; 2 = the physics waves skip the
 // physics (the state only advances by the action's thrust); 3 = no
-// auto-reset; 4 = no observation formed (zeros staged)
+// auto-reset; 4 = no observation formed (zeros staged); 5 = no reset
+// Philox draws (the reset takes zero words: the same branch, fewer VALU)
 #ifndef DR_WS_ABL
 #define DR_WS_ABL 0
 #endif
@@ -1418,7 +1419,7 @@ __global__ __launch_bounds__(kWsThreads) void env_rollout_ws_kernel(EnvView<S> v
         }
         const MotorMix mx = motor_mix(a_cur);
         if constexpr (GYMLIKE) {
-            if (t % kResetAhead == 0 && !nd_ok) {
+            if (t % kResetAhead == 0 && !nd_ok && DR_WS_ABL != 5) {
 #pragma unroll
                 for (int b = 0; b < NB; ++b)
                     nd[b] = philox4x32_10(u32x4{(uint32_t)(ep_num + 1), (uint32_t)gid,
@@ -1449,7 +1450,7 @@ __global__ __launch_bounds__(kWsThreads) void env_rollout_ws_kernel(EnvView<S> v
                 // same words the reset would draw; always passing the array
                 // keeps it in registers -- a pointer-or-null argument put it
                 // on the scratch stack)
-                if (!nd_ok) {
+                if (!nd_ok && DR_WS_ABL != 5) {
 #pragma unroll
                     for (int b = 0; b < NB; ++b)
                         nd[b] = philox4x32_10(u32x4{(uint32_t)(ep_num + 1), (uint32_t)gid,
