@@ -1246,12 +1246,24 @@ __device__ inline void ws_glds16(const void *gptr, uint32_t lds_base) {
 }
 #pragma clang diagnostic pop
 
+// DR_WS_MWR 1 (A/B knob, gym variant): the memory waves draw the physics
+// waves' reset Philox blocks (see the kernel).  Bitwise the same outputs but
+// slower (46.8-48.8 vs 45.8-46.3 us per 32-step launch; 51.7 vs 44.5 with
+// the in-kernel policy, whose actions the memory waves draw too): the two
+// waves of a SIMD share its VALU issue, so moving the draws across does not
+// take them off the physics wave's path (MI355X_MICROARCH.md, two waves per
+// SIMD, item 3)
+#ifndef DR_WS_MWR
+#define DR_WS_MWR 0
+#endif
+
 template <int OD>
 struct WsLds {
     float obs[2][kWsEnvs * OD];              // per slot: 4 waves x 64 rows x OD
     float rew[2][kWsEnvs];
     uint8_t done[2][kWsEnvs];
     float4 act[kWsNA][kWsEnvs];
+    u32x4 rnd[2][2][kWsEnvs];                // reset draw candidates [slot][ep + 1 | ep + 2]
 };
 
 template <typename S, int VAR, bool GEN>
@@ -1333,11 +1345,44 @@ __global__ __launch_bounds__(kWsThreads) void env_rollout_ws_kernel(EnvView<S> v
                 st_out(at(io.done + row, i_own), d);
             }
         };
+        // MWR: the reset draws of the partner's lanes.  A physics wave that
+        // resets at step t needs block 0 of Philox(ep + 1) for the episode
+        // number ep after step t - 1.  Here, at phase t - 1, the memory wave
+        // knows ep after step t - 2 (from the staged done flags) and
+        // publishes both candidates, Philox(ep + 1) and Philox(ep + 2), in
+        // slot t & 1; the physics wave picks by whether it reset at step
+        // t - 1.  After a reset the pair shifts and one new block is drawn.
+        constexpr bool MWR = DR_WS_MWR && VAR == DR_VARIANT_GYM && DR_WS_ABL != 5;
+        int32_t mw_ep = 0;
+        u32x4 c1{}, c2{};
+        auto draw = [&](int32_t e) {
+            return philox4x32_10(u32x4{(uint32_t)e, (uint32_t)gid, (uint32_t)(gid >> 32),
+                                       TAG_RESET},
+                                 v.seed_lo, v.seed_hi);
+        };
+        auto publish = [&](int slot) {
+            sh.rnd[slot][0][p * 64 + lane] = c1;
+            sh.rnd[slot][1][p * 64 + lane] = c2;
+        };
+        if constexpr (MWR) {
+            mw_ep = *at(fp.ep_num, i);
+            c1 = draw(mw_ep + 1);
+            c2 = draw(mw_ep + 2);
+            publish(0);                           // for step 0
+        }
         for (int t = 0; t <= kWsAhead && t < K; ++t) load_act(t);
-        if (!GEN) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // actions 0 .. D
+        if (!GEN || MWR) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // actions 0 .. D
         asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");   // B_(-1)
         for (int t = 0; t < K; ++t) {
             if (t + kWsAhead + 1 < K) load_act(t + kWsAhead + 1);
+            if constexpr (MWR) {
+                if (t >= 1 && io.auto_reset && sh.done[(t - 1) & 1][p * 64 + lane]) {
+                    mw_ep += 1;                   // the partner reset at step t - 1
+                    c1 = c2;
+                    c2 = draw(mw_ep + 2);
+                }
+                if (t + 1 < K) publish((t + 1) & 1);
+            }
             if (t >= 1) store_out(t - 1);
             // action a = t + 1 + PRE must have landed before B_t (actions
             // 0 .. D did before B_(-1)).  It was issued first in phase
@@ -1404,6 +1449,10 @@ __global__ __launch_bounds__(kWsThreads) void env_rollout_ws_kernel(EnvView<S> v
     constexpr int NB = VAR == DR_VARIANT_MOVING ? 4 : 1;
     u32x4 nd[NB] = {};
     bool nd_ok = false;
+    // MWR: the reset draw comes from the memory wave (prev_reset picks the
+    // candidate: did this lane reset at the previous step)
+    constexpr bool MWR = DR_WS_MWR && VAR == DR_VARIANT_GYM && DR_WS_ABL != 5;
+    bool prev_reset = false;
     int32_t max_steps;
     asm volatile("v_mov_b32 %0, %1" : "=v"(max_steps) : "s"(v.max_steps));
     asm volatile("s_barrier" ::: "memory");                          // B_(-1)
@@ -1418,7 +1467,9 @@ __global__ __launch_bounds__(kWsThreads) void env_rollout_ws_kernel(EnvView<S> v
             a_cur = sh.act[t % kWsNA][p * 64 + lane];
         }
         const MotorMix mx = motor_mix(a_cur);
-        if constexpr (GYMLIKE) {
+        u32x4 cand{};
+        if constexpr (MWR) cand = sh.rnd[t & 1][prev_reset ? 1 : 0][p * 64 + lane];
+        if constexpr (GYMLIKE && !MWR) {
             if (t % kResetAhead == 0 && !nd_ok && DR_WS_ABL != 5) {
 #pragma unroll
                 for (int b = 0; b < NB; ++b)
@@ -1443,14 +1494,17 @@ __global__ __launch_bounds__(kWsThreads) void env_rollout_ws_kernel(EnvView<S> v
         step += 1;
         const bool done = live && (crash || (step >= max_steps));
         if constexpr (GYMLIKE) {
-            if (done && io.auto_reset && DR_WS_ABL != 3) {
+            const bool rs = done && io.auto_reset && DR_WS_ABL != 3;
+            if (MWR) prev_reset = rs;
+            if (rs) {
                 step = 0;
                 reset_any = true;
+                if (MWR) nd[0] = cand;
                 // a second reset within the group: draw its blocks here (the
                 // same words the reset would draw; always passing the array
                 // keeps it in registers -- a pointer-or-null argument put it
                 // on the scratch stack)
-                if (!nd_ok && DR_WS_ABL != 5) {
+                if (!MWR && !nd_ok && DR_WS_ABL != 5) {
 #pragma unroll
                     for (int b = 0; b < NB; ++b)
                         nd[b] = philox4x32_10(u32x4{(uint32_t)(ep_num + 1), (uint32_t)gid,

@@ -7,7 +7,7 @@ OUT=scripts/micro/build
 V="${VARIANTS:-0 1 2}"
 # variant a: DR_WS_ABL=a; "prio": DR_WS_PRIO=1; "ra16" / "ra4": DR_WS_RA
 flags() { case $1 in prio) echo "-DDR_WS_PRIO=1";; ra16) echo "-DDR_WS_RA=16";;
-          5) echo "-DDR_WS_ABL=5 -DDR_ABLATE=5";;
+          5) echo "-DDR_WS_ABL=5 -DDR_ABLATE=5";; mwr0) echo "-DDR_WS_MWR=0";;
           ra4) echo "-DDR_WS_RA=4";; *) echo "-DDR_WS_ABL=$1";; esac; }
 if [ "$1" == "build" ]; then
   for a in $V; do
