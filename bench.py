@@ -317,8 +317,8 @@ def time_rollout(args, n_envs, device, k, reps, gen, variant="gym", state_dtype=
     """The K-step rollout kernel (dr_rollout; dr_rollout_random when gen):
     `reps` launches of k steps each over the same 65,536 envs, captured in
     one hipGraph; returns the per-launch GPU time (HIP events on the launch
-    stream) in seconds.  Reported beside the headline, never as `value`
-    (the headline stays on the single-step kernel PPO uses)."""
+    stream) in seconds.  Reported beside the headline (the `rollout_kernel`
+    block: fixed K, repeated launches, both action sources), never as `value`."""
     import torch
 
     from drone_rl_amd import DroneBatch, random_actions
