@@ -196,6 +196,11 @@ class PPOTrainer:
         # 1, faulted on the second replay of a captured graph at configs[2]
         # size).  DRONERL_TRAIN_GRAPH=0: always eager.
         self.train_graph = os.environ.get("DRONERL_TRAIN_GRAPH", "1") != "0"
+        # the next minibatch's gather on a side stream, beside this
+        # minibatch's step, into a second set of minibatch buffers
+        # (DRONERL_PPO_OVERLAP=1; same kernels and inputs, bitwise the same)
+        self.overlap_gather = os.environ.get("DRONERL_PPO_OVERLAP", "0") == "1"
+        self._slots, self._side = None, None
         self._tgraph, self._twarm, self._tstats, self._tkey = None, False, None, None
         self._ctr = torch.zeros(1, dtype=torch.int64, device=dev)
         # optional TrajectoryTensorboardCallback equivalent (trajectory.py)
@@ -314,6 +319,8 @@ class PPOTrainer:
         bias-correction schedule): the same kernels and numerics as train(),
         capturable into one hipGraph."""
         cfg, M = self.cfg, self.cfg.batch_size
+        if self.overlap_gather:
+            return self._train_body_overlap(obs_flat, act_flat, nmb)
         j = 0
         for epoch in range(cfg.n_epochs):
             perm = self.perm.dev(seed=cfg.seed * 104729 + self.rank, counter_base=self._pctr,
@@ -322,19 +329,74 @@ class PPOTrainer:
                 idx = perm[k * M:(k + 1) * M]
                 K.gather_minibatch(idx, obs_flat, act_flat, self.aux, self.mb_obs, self.mb_act,
                                    self.mb_aux, adv_part=self.head.adv_part)
-                grad, _ = self.fused.step(self.mb_obs, self.mb_act, self.mb_aux, self.head,
-                                          adv_ready=True, stats_out=self._tstats[j],
-                                          defer_finish=True)
-                if self.dp_step:
-                    # finish -> one all-reduce (sum) of the 564 KB flat
-                    # gradient -> clip+Adam on its mean
-                    self.fused.finish.run(self.device)
-                    if self.dp_collective:
-                        D.allreduce_flat_sum_(grad, group=self.pg)
-                    self.opt.step_sched(grad, self._sched[j], 1.0 / self.world)
-                else:
-                    self.opt.step_finish_sched(grad, self.fused.finish, self._sched[j])
+                self._train_minibatch(j, self.mb_obs, self.mb_act, self.mb_aux)
                 j += 1
+
+    def _train_minibatch(self, j, mb_obs, mb_act, mb_aux):
+        """Optimizer step j on one gathered minibatch (its advantage partials
+        in self.head.adv_part)."""
+        grad, _ = self.fused.step(mb_obs, mb_act, mb_aux, self.head, adv_ready=True,
+                                  stats_out=self._tstats[j], defer_finish=True)
+        if self.dp_step:
+            # finish -> one all-reduce (sum) of the 564 KB flat gradient ->
+            # clip+Adam on its mean (SURVEY.md 8e)
+            self.fused.finish.run(self.device)
+            if self.dp_collective:
+                D.allreduce_flat_sum_(grad, group=self.pg)
+            self.opt.step_sched(grad, self._sched[j], 1.0 / self.world)
+        else:
+            self.opt.step_finish_sched(grad, self.fused.finish, self._sched[j])
+
+    def _train_body_overlap(self, obs_flat, act_flat, nmb):
+        """_train_body with minibatch j + 1's gather on a side stream while
+        step j runs on the current one.  Two slots of minibatch buffers (obs,
+        actions, aux, the head workspace that holds the advantage partials):
+        gather j + 1 waits for everything issued before step j (step j - 1
+        read its slot), step j waits for gather j's event.  The permutation
+        of the next epoch is formed on the current stream after its last
+        gather was waited for."""
+        cfg, M = self.cfg, self.cfg.batch_size
+        S = cfg.n_epochs * nmb
+        if self._slots is None:
+            ws2 = torch.empty_like(self.head.ws)
+            self._slots = [(self.mb_obs, self.mb_act, self.mb_aux, self.head.ws),
+                           (torch.empty_like(self.mb_obs), torch.empty_like(self.mb_act),
+                            torch.empty_like(self.mb_aux), ws2)]
+            self._side = torch.cuda.Stream(self.device)
+            self._gev = [torch.cuda.Event(), torch.cuda.Event()]
+        cur = torch.cuda.current_stream(self.device)
+        side, slots, ev = self._side, self._slots, self._gev
+        perm = [None]
+
+        def make_perm(epoch):
+            perm[0] = self.perm.dev(seed=cfg.seed * 104729 + self.rank,
+                                    counter_base=self._pctr, counter_offset=epoch)
+
+        def gather(j):
+            k = j % nmb
+            o, a, x, ws = slots[j & 1]
+            K.gather_minibatch(perm[0][k * M:(k + 1) * M], obs_flat, act_flat, self.aux, o, a,
+                               x, adv_part=ws)
+
+        ws0 = self.head.ws
+        try:
+            make_perm(0)
+            gather(0)
+            for j in range(S):
+                if j > 0:
+                    cur.wait_event(ev[j & 1])
+                if j + 1 < S:
+                    if (j + 1) % nmb == 0:
+                        make_perm((j + 1) // nmb)
+                    side.wait_stream(cur)
+                    with torch.cuda.stream(side):
+                        gather(j + 1)
+                        ev[(j + 1) & 1].record(side)
+                o, a, x, ws = slots[j & 1]
+                self.head.ws = ws
+                self._train_minibatch(j, o, a, x)
+        finally:
+            self.head.ws = ws0
 
     def _train_graphed(self):
         cfg = self.cfg

@@ -12,10 +12,10 @@ from oracle import ppo_ref
 pytestmark = pytest.mark.gpu
 
 
-def _trainer(**kw):
+def _trainer(net_arch=(64, 64), **kw):
     from drone_rl_amd.ppo import PPOConfig, PPOTrainer
     cfg = PPOConfig(num_envs=2048, n_steps=8, batch_size=4096, n_epochs=2,
-                    net_arch=(64, 64), seed=5, **kw)
+                    net_arch=net_arch, seed=5, **kw)
     return PPOTrainer(cfg)
 
 
@@ -145,6 +145,27 @@ def test_sb3_zip_resume_continues_streams_and_schedule(tmp_path):
     c.load_sb3(path)
     c.learn_step()           # the update-0 entry must not fire again
     assert (c.env.get("eps").cpu().numpy() >= 0.1).all()
+    for t in (a, b, c):
+        t.close()
+
+
+@pytest.mark.parametrize("arch", [(64, 64), (256, 256)])
+def test_overlapped_gather_is_bitwise_the_serial_loop(arch):
+    """DRONERL_PPO_OVERLAP=1 (minibatch j + 1 gathered on a side stream
+    beside step j, two buffer slots) trains bitwise as the serial loop,
+    eager and graph-captured, across an epoch boundary (4 minibatches per
+    epoch, 2 epochs)."""
+    a, b, c = _trainer(net_arch=arch), _trainer(net_arch=arch), _trainer(net_arch=arch)
+    b.overlap_gather = c.overlap_gather = True
+    c.rollout_graph = c.train_graph = False
+    for it in range(3):
+        sa, sb, sc = a.learn_step(), b.learn_step(), c.learn_step()
+        assert torch.equal(sa, sb) and torch.equal(sa, sc), it
+        for t in (b, c):
+            assert torch.equal(a.policy.flat.detach(), t.policy.flat.detach()), it
+            assert torch.equal(a.opt.m, t.opt.m) and torch.equal(a.opt.v, t.opt.v), it
+    assert b._tgraph is not None and b._slots is not None and c._tgraph is None
+    assert b.head.ws.data_ptr() == b._slots[0][3].data_ptr()
     for t in (a, b, c):
         t.close()
 
