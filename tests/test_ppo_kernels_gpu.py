@@ -416,6 +416,24 @@ def test_gather_minibatch_equals_gathers_and_adv_pass(m, d):
     assert torch.equal(g1, g2) and torch.equal(s1, s2)
 
 
+@pytest.mark.parametrize("m,d", [(1, 7), (1025, 5), (4099, 15), (70001, 12)])
+def test_gather_minibatch_ragged_and_runtime_widths(m, d):
+    """dr_gather_minibatch at ragged row counts (partial last block of every
+    section) and at obs widths without a compiled-in constant (the runtime
+    divisor path): the rows of obs / actions / aux exactly."""
+    from drone_rl_amd import ppo_kernels as K
+    g = torch.Generator(device="cuda").manual_seed(m * 31 + d)
+    total = 3 * m + 2
+    obs = torch.randn(total, d, device="cuda", generator=g)
+    act = torch.randn(total, 4, device="cuda", generator=g)
+    aux = torch.randn(total, 3, device="cuda", generator=g)
+    idx = torch.randperm(total, device="cuda", generator=g)[:m].to(torch.int32)
+    o, a, x = (torch.full((m, w), float("nan"), device="cuda") for w in (d, 4, 3))
+    K.gather_minibatch(idx, obs, act, aux, o, a, x)
+    r = idx.long()
+    assert torch.equal(o, obs[r]) and torch.equal(a, act[r]) and torch.equal(x, aux[r])
+
+
 @pytest.mark.parametrize("arch,m", [((256, 256), 65536), ((64, 64), 1000), ((64, 128), 4096)])
 def test_deferred_finish_equals_separate_finishes(arch, m):
     """FusedTrainStep.step(defer_finish=True) + ClipAdam.step_finish (the
