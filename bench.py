@@ -523,8 +523,9 @@ def time_ppo(args, rank, world, device, force_dp=False, dp_graph=False, profile=
     es = tr.episode_stats()
     stats = dict(zip(("loss", "policy_loss", "value_loss", "entropy_loss", "clip_fraction",
                       "approx_kl"), [round(x, 5) for x in st.tolist()[:6]]))
-    path = ("data-parallel step (deferred finish -> " +
-            ("RCCL" if world > 1 or tr.dp_collective else "no") + " all-reduce -> clip+Adam)"
+    coll = {"nccl": "RCCL"}.get(dist.get_backend(), dist.get_backend()) if world > 1 else (
+        "RCCL" if tr.dp_collective else "no")
+    path = ("data-parallel step (deferred finish -> " + coll + " all-reduce -> clip+Adam)"
             if tr.dp_step else "single-GPU fused step (deferred finish + clip+Adam)"
             if tr._train_fast() else "per-kernel finishes")
     res = {"updates_per_s": round(K / el, 4),
