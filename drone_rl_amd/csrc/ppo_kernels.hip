@@ -861,6 +861,15 @@ struct LayerPair {
 #ifndef DR_LT_RPI
 #define DR_LT_RPI 1
 #endif
+// diagnostic builds of linear_tanh_kernel (wrong by construction; timing
+// only, scripts/micro/ab_ppo_kern.sh): 1 = no tanh, 2 = no per-row store
+#ifndef DR_LT_ABL
+#define DR_LT_ABL 0
+#endif
+// minimum rows per block (4 waves) of linear_tanh_kernel (A/B knob)
+#ifndef DR_LT_RPB
+#define DR_LT_RPB 64
+#endif
 // blocks per net of linear_tanh_kernel (A/B knob)
 #ifndef DR_LT_MAXB
 #define DR_LT_MAXB 1024
@@ -959,6 +968,9 @@ __global__ __launch_bounds__(kBlock) void linear_tanh_kernel(int64_t m, int n,
 #pragma unroll
         for (int k = 0; k < K; ++k) xn[k] = xr[k];
     }
+#if DR_LT_ABL == 2
+    float4 keep = make_float4(0.f, 0.f, 0.f, 0.f);
+#endif
     for (; r < m; r += stride) {
         float xv[K];
 #pragma unroll
@@ -975,11 +987,24 @@ __global__ __launch_bounds__(kBlock) void linear_tanh_kernel(int64_t m, int n,
 #pragma unroll
             for (int q = 0; q < 4; ++q) acc[q] = fmaf(xv[k], wr[q][k], acc[q]);
         }
+#if DR_LT_ABL == 1      // diagnostic: no tanh
+        if (act)
+            st4(h + r * n + c0, make_float4(acc[0] + bb[0], acc[1] + bb[1], acc[2] + bb[2],
+                                            acc[3] + bb[3]));
+#elif DR_LT_ABL == 2    // diagnostic: no per-row store (one store per wave at the end)
+        const float4 t4 = make_float4(tanh_fast(acc[0] + bb[0]), tanh_fast(acc[1] + bb[1]),
+                                      tanh_fast(acc[2] + bb[2]), tanh_fast(acc[3] + bb[3]));
+        keep = add4(keep, t4);
+#else
         if (act)
             st4(h + r * n + c0,
                 make_float4(tanh_fast(acc[0] + bb[0]), tanh_fast(acc[1] + bb[1]),
                             tanh_fast(acc[2] + bb[2]), tanh_fast(acc[3] + bb[3])));
+#endif
     }
+#if DR_LT_ABL == 2
+    if (act && keep.x == 12345.f) st4(h + c0, keep);
+#endif
 #else
     // rows are wave-strided; the next row's input is loaded before this
     // row's arithmetic (software pipelining hides the load latency)
@@ -2218,7 +2243,7 @@ static int launch_linear_tanh(const char *who, int nets, int64_t m, int64_t k, i
         if ((((uintptr_t)lp.h[j]) | ((uintptr_t)lp.w[j])) & 15)
             return fail0(DR_ERR_INVALID, std::string(who) + ": h and w must be 16-byte aligned");
     }
-    const int64_t nbl = (m + 63) / 64;    // >= 16 rows per wave
+    const int64_t nbl = (m + DR_LT_RPB - 1) / DR_LT_RPB;    // >= RPB / 4 rows per wave
     const int nb = (int)(nbl < DR_LT_MAXB ? nbl : DR_LT_MAXB);
     hipStream_t st = as_stream(stream);
     switch (k) {
