@@ -104,12 +104,70 @@ enum : uint32_t {
     TAG_PERM = 0x50000000u      // minibatch permutation keys
 };
 
-// Branch-free f32 tanh (<= 2 ulp): odd Taylor polynomial through x^15 for
+// The network's tanh (every kernel that applies it calls tanh_fast / tanh4,
+// so all paths agree bitwise).  DR_TANH_RAT 1 (default since round 3): the
+// rational form below, measured faster (linear_tanh 34.6 vs 37.9 us, the
+// head kernel 58.0 vs 61.5 us, PPO 5.84-5.85 vs 5.76-5.77 updates/s, same
+// box, scripts/micro/round3_y.sh); 0: the two-form evaluation (<= 2 ulp).
+#ifndef DR_TANH_RAT
+#define DR_TANH_RAT 1
+#endif
+// Rational f32 tanh: x P(x^2) / Q(x^2) on x clamped to +-7.905 (odd degree-13
+// / even degree-6 minimax set, as in Eigen's generic_fast_tanh_float), one
+// hardware rcp; <= 6 ulp from the correctly rounded tanh (4.6 ulp with an
+// exact quotient, scripts/micro/tanh_rat.py), half the VALU of the two-form
+// evaluation.  The clamp is NaN-propagating (IEEE maximum / minimum), so NaN
+// stays NaN; +-inf -> +-tanh(7.905) (1 - 3 ulp).
+__device__ inline float tanh_rat(float x) {
+    const float c = 7.90531110763549805f;
+    const float xc = __builtin_elementwise_minimum(__builtin_elementwise_maximum(x, -c), c);
+    const float s = xc * xc;
+    float p = fmaf(s, -2.76076847742355e-16f, 2.00018790482477e-13f);
+    p = fmaf(s, p, -8.60467152213735e-11f);
+    p = fmaf(s, p, 5.12229709037114e-08f);
+    p = fmaf(s, p, 1.48572235717979e-05f);
+    p = fmaf(s, p, 6.37261928875436e-04f);
+    p = fmaf(s, p, 4.89352455891786e-03f);
+    float q = fmaf(s, 1.19825839466702e-06f, 1.18534705686654e-04f);
+    q = fmaf(s, q, 2.26843463243900e-03f);
+    q = fmaf(s, q, 4.89352518554385e-03f);
+    return (xc * p) * __builtin_amdgcn_rcpf(q);
+}
+
+// tanh_rat on a pair, written on 2-wide vectors so that the polynomials and
+// products issue as packed f32 (v_pk_fma_f32 / v_pk_mul_f32); per component
+// bitwise tanh_rat.
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+__device__ inline f32x2 pk_fma(f32x2 a, f32x2 b, f32x2 c) {
+    return __builtin_elementwise_fma(a, b, c);
+}
+__device__ inline f32x2 tanh_rat2(f32x2 x) {
+    const f32x2 c = {7.90531110763549805f, 7.90531110763549805f};
+    const f32x2 xc = __builtin_elementwise_minimum(__builtin_elementwise_maximum(x, -c), c);
+    const f32x2 s = xc * xc;
+    auto k = [](float v) { return f32x2{v, v}; };
+    f32x2 p = pk_fma(s, k(-2.76076847742355e-16f), k(2.00018790482477e-13f));
+    p = pk_fma(s, p, k(-8.60467152213735e-11f));
+    p = pk_fma(s, p, k(5.12229709037114e-08f));
+    p = pk_fma(s, p, k(1.48572235717979e-05f));
+    p = pk_fma(s, p, k(6.37261928875436e-04f));
+    p = pk_fma(s, p, k(4.89352455891786e-03f));
+    f32x2 q = pk_fma(s, k(1.19825839466702e-06f), k(1.18534705686654e-04f));
+    q = pk_fma(s, q, k(2.26843463243900e-03f));
+    q = pk_fma(s, q, k(4.89352518554385e-03f));
+    const f32x2 r = {__builtin_amdgcn_rcpf(q.x), __builtin_amdgcn_rcpf(q.y)};
+    return (xc * p) * r;
+}
+
+// tanh_fast with DR_TANH_RAT 0: a branch-free f32 tanh (<= 2 ulp): odd Taylor polynomial through x^15 for
 // |x| < 0.55 (truncation < 0.5 ulp there), 1 - 2 / (e^{2|x|} + 1) above
 // (hardware exp2 / rcp, the cancellation costs <= 2 ulp at the switch),
 // sign restored; NaN propagates, +-inf -> +-1.  The device library's tanhf
 // branches per element, which costs ~3x the instructions in a wave.
 __device__ inline float tanh_fast(float x) {
+#if DR_TANH_RAT
+    return tanh_rat(x);
+#else
     const float ax = fabsf(x);
     const float z = ax * ax;
     float p = fmaf(z, -929569.0f / 638512875.0f, 21844.0f / 6081075.0f);
@@ -122,6 +180,7 @@ __device__ inline float tanh_fast(float x) {
     const float e = __builtin_amdgcn_exp2f(ax * 2.8853900817779268f);  // e^{2|x|}
     const float large = fmaf(-2.0f, __builtin_amdgcn_rcpf(e + 1.0f), 1.0f);
     return copysignf(ax < 0.55f ? small : large, x);
+#endif
 }
 
 constexpr int kBlock = 256;   // 4 waves of 64

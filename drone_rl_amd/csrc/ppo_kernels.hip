@@ -830,7 +830,12 @@ __device__ inline void st4(float *p, float4 x) {
     else *reinterpret_cast<float4 *>(p) = x;
 }
 __device__ inline float4 tanh4(float4 v) {
+#if DR_TANH_RAT
+    const f32x2 lo = tanh_rat2(f32x2{v.x, v.y}), hi = tanh_rat2(f32x2{v.z, v.w});
+    return make_float4(lo.x, lo.y, hi.x, hi.y);
+#else
     return make_float4(tanh_fast(v.x), tanh_fast(v.y), tanh_fast(v.z), tanh_fast(v.w));
+#endif
 }
 // z + b, as the GEMM epilogue would have added it (z already the full dot
 // product; b = 0 adds exactly nothing)
@@ -981,6 +986,23 @@ __global__ __launch_bounds__(kBlock) void linear_tanh_kernel(int64_t m, int n,
 #pragma unroll
             for (int k = 0; k < K; ++k) xn[k] = xr[k];
         }
+#if DR_TANH_RAT
+        // the same fmaf chain per column, written as packed pairs (columns
+        // 0-1, 2-3), and the pairs' rational tanh
+        f32x2 a01 = {0.f, 0.f}, a23 = {0.f, 0.f};
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            const f32x2 xk = {xv[k], xv[k]};
+            a01 = pk_fma(xk, f32x2{wr[0][k], wr[1][k]}, a01);
+            a23 = pk_fma(xk, f32x2{wr[2][k], wr[3][k]}, a23);
+        }
+        if (act) {
+            const f32x2 t01 = tanh_rat2(a01 + f32x2{bb[0], bb[1]});
+            const f32x2 t23 = tanh_rat2(a23 + f32x2{bb[2], bb[3]});
+            st4(h + r * n + c0, make_float4(t01.x, t01.y, t23.x, t23.y));
+        }
+        continue;
+#endif
         float acc[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int k = 0; k < K; ++k) {
