@@ -1400,8 +1400,10 @@ constexpr int kFirstTile = DR_FL_TILE;
 #ifndef DR_FL_LDS2
 #define DR_FL_LDS2 1
 #endif
+// 256 blocks per net (round 3): 52.5-53.2 vs 54.2-54.7 us per minibatch at
+// 512 (scripts/micro/round3_z.sh), fewer partials for the deferred finish
 #ifndef DR_FL_MAXB
-#define DR_FL_MAXB 512
+#define DR_FL_MAXB 256
 #endif
 
 // With gridDim.y == 2 the launch covers both MLPs (blockIdx.y = net); block
