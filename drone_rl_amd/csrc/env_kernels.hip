@@ -1231,7 +1231,13 @@ constexpr int kWsThreads = 2 * kWsEnvs;
 #ifndef DR_WS_PRE
 #define DR_WS_PRE 0
 #endif
-constexpr int kWsAhead = DR_WS_PRE ? 3 : 2;  // D
+// DR_WS_AHEAD (A/B knob): D, how many steps ahead of the physics the memory
+// waves issue an action load (the hand-counted waits below are generic in D;
+// vmcnt holds at most 63, so S_OPS + D * (S_OPS + 1) must stay below it)
+#ifndef DR_WS_AHEAD
+#define DR_WS_AHEAD (DR_WS_PRE ? 3 : 2)
+#endif
+constexpr int kWsAhead = DR_WS_AHEAD;  // D
 constexpr int kWsNA = kWsAhead + 2;          // action ring slots
 
 // global_load_lds_dwordx4: lane l's 16 bytes land at LDS byte lds_base + 16 l
@@ -1274,6 +1280,8 @@ __global__ __launch_bounds__(kWsThreads) void env_rollout_ws_kernel(EnvView<S> v
     constexpr int NQ = (64 * OD / 4 + 63) / 64;  // float4 rows-stores per lane and step
     // the hand-counted wait assumes NQ obs + 1 reward + 1 done store per phase
     constexpr int S_OPS = NQ + 2;
+    static_assert(S_OPS + (kWsAhead - DR_WS_PRE) * (S_OPS + 1) <= 63,
+                  "the action-load wait count must fit vmcnt");
     __shared__ __attribute__((aligned(16))) WsLds<OD> sh;
     const int64_t n_ = v.n;
     const int K = io.k;
