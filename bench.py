@@ -622,7 +622,7 @@ def main():
         roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                 "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": tr,
                 "traffic_GBs": round(tr / per_launch_s / 1e9, 1) if tr else None,
-                "kernel": "env_rollout_ws_kernel", "steps_per_launch": kh, "launches": launches,
+                "kernel": "env_rollout_ab_kernel", "steps_per_launch": kh, "launches": launches,
                 "bytes_per_env_step": round(bpe, 2),
                 "bytes_basis": "per env-step 16 action + 60 obs + 4 reward + 1 done; per "
                                "launch and env the f64 state read (124 B) and written (100 B) "
@@ -633,9 +633,10 @@ def main():
                 # kernel alone, without the event records' queue time
                 "avg_launch_us_packet": (round(packet_ms / launches * 1e3, 3)
                                          if packet_ms else None),
-                "limiter": "the physics waves' f64 step at one physics wave per SIMD "
-                           "(memory waves stream the outputs beside them; with no physics "
-                           "the stream alone takes ~31 us per 32 steps, DESIGN.md section 3)"}
+                "limiter": "the f64 step, split by data over two waves per SIMD "
+                           "(translation / rotation; memory waves stream the outputs beside "
+                           "them; with no physics the stream alone takes ~30 us per 32 "
+                           "steps, DESIGN.md section 3)"}
     else:
         elapsed, gpu_ms, ep = el_s, gm_s, ep_s
         roof = single["roofline"]
@@ -694,12 +695,15 @@ def main():
         # (bitwise the K single steps; tests/test_rollout_gpu.py)
         k, sb = args.rollout_k, (8 if args.state_dtype == "f64" else 4)
         state_b = (15 * sb + 4) + (12 * sb + 4)   # state in + out once per launch
-        ro = {"kernel": "env_rollout_ws_kernel", "k": k, "envs": N, "launches": 10}
+        ro = {"k": k, "envs": N, "launches": 10}
         for gen in (False, True):
             pl = time_rollout(args, N, device, k, 10, gen)
             bpe = (65 if gen else 81) + state_b / k
             ach = N * k * bpe / pl / 1e9
             ro["random_policy_in_kernel" if gen else "actions_from_hbm"] = {
+                # dr_rollout's default form per action source (env_kernels.hip
+                # launch_rollout)
+                "kernel": "env_rollout_ws_kernel" if gen else "env_rollout_ab_kernel",
                 "env_steps_per_s": round(N * k / pl, 1),
                 "avg_launch_us": round(pl * 1e6, 3), "us_per_step": round(pl * 1e6 / k, 3),
                 "bytes_per_env_step": round(bpe, 2),

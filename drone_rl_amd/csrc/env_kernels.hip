@@ -1206,7 +1206,9 @@ __global__ __launch_bounds__(kEnvBlock) void env_rollout_kernel(EnvView<S> v, Ro
 // 1 = the memory waves store no outputs; 2 = the physics waves skip the
 // physics (the state only advances by the action's thrust); 3 = no
 // auto-reset; 4 = no observation formed (zeros staged); 5 = no reset
-// Philox draws (the reset takes zero words: the same branch, fewer VALU)
+// Philox draws (the reset takes zero words: the same branch, fewer VALU);
+// 6 = no per-step barrier: the memory waves end after the prologue, the
+// physics waves step on the first action slot with no synchronisation
 #ifndef DR_WS_ABL
 #define DR_WS_ABL 0
 #endif
@@ -1381,6 +1383,7 @@ __global__ __launch_bounds__(kWsThreads) void env_rollout_ws_kernel(EnvView<S> v
         for (int t = 0; t <= kWsAhead && t < K; ++t) load_act(t);
         if (!GEN || MWR) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // actions 0 .. D
         asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");   // B_(-1)
+        if (DR_WS_ABL == 6) return;
         for (int t = 0; t < K; ++t) {
             if (t + kWsAhead + 1 < K) load_act(t + kWsAhead + 1);
             if constexpr (MWR) {
@@ -1472,7 +1475,7 @@ __global__ __launch_bounds__(kWsThreads) void env_rollout_ws_kernel(EnvView<S> v
             a_cur = a_next;
             if (t + 1 < K) a_next = sh.act[(t + 1) % kWsNA][p * 64 + lane];
         } else {
-            a_cur = sh.act[t % kWsNA][p * 64 + lane];
+            a_cur = sh.act[DR_WS_ABL == 6 ? 0 : t % kWsNA][p * 64 + lane];
         }
         const MotorMix mx = motor_mix(a_cur);
         u32x4 cand{};
@@ -1548,7 +1551,10 @@ __global__ __launch_bounds__(kWsThreads) void env_rollout_ws_kernel(EnvView<S> v
         sh.rew[so][p * 64 + lane] = (float)r;
         sh.done[so][p * 64 + lane] = (uint8_t)done;
         __builtin_amdgcn_sched_barrier(0);
-        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");   // B_t
+        if (DR_WS_ABL == 6)
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        else
+            asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");   // B_t
     }
     if (live) {
 #pragma unroll
@@ -1564,6 +1570,336 @@ __global__ __launch_bounds__(kWsThreads) void env_rollout_ws_kernel(EnvView<S> v
 #pragma unroll
                 for (int k = 0; k < 9; ++k) *at(v.mot + k * v.stride, i) = mp[k];
             }
+        }
+    }
+}
+
+// ----------------------------------------------------------------------------
+// Split-physics K-step rollout (gym variant; DRONERL_ROLLOUT_AB).  The
+// warp-specialised kernel's physics wave, split by DATA into two waves on the
+// same SIMD, so that two dependent f64 chains interleave where one wave per
+// SIMD left the VALU idle about half of its cycles (two physics waves per
+// SIMD were measured to hide 24 % per env):
+//   * the TRANSLATION wave (waves 0-3) owns pos / vel / target, the step
+//     counter, the curriculum and the reset draws: R's column 2 from the
+//     step's Euler sincos, acceleration, velocity, position, reward, crash,
+//     done, the reset, and the obs fields pos / vel / target - pos;
+//   * the ROTATION wave (waves 4-7) owns the Euler angles and body rates:
+//     their sincos, the Euler rates and the angular update, and the obs
+//     fields euler / omega;
+//   * the MEMORY waves (8-11) load actions and stream outputs as in the
+//     warp-specialised kernel.
+// Wave p, p + 4 and p + 8 share SIMD p.  The two halves of a step touch
+// disjoint state; what crosses is the sincos of the step's angles (rotation ->
+// translation, computed one step ahead from the updated angles, through a
+// double-buffered LDS slot) and the done flag (translation -> rotation, read
+// one phase later: a reset zeroes the angles and rates before the next step,
+// and their sincos is then exactly (+0, 1), which both waves substitute).  The
+// rotation wave therefore writes step t's euler / omega obs fields in phase
+// t + 1, and the memory waves store step t's outputs in phase t + 2 from
+// three output slots.  Every expression is physics_step_mixed's, in its
+// order: outputs bitwise those of the other kernels (tests/test_rollout_gpu.py).
+// ----------------------------------------------------------------------------
+constexpr int kAbThreads = 3 * kWsEnvs;   // 4 translation + 4 rotation + 4 memory waves
+constexpr int kAbOut = 3;                 // output slots
+
+template <typename S, int OD>
+struct AbLds {
+    float obs[kAbOut][kWsEnvs * OD];
+    float rew[kAbOut][kWsEnvs];
+    uint8_t done[kAbOut][kWsEnvs];
+    float4 act[kWsNA][kWsEnvs];
+    S sc[2][6][kWsEnvs];                  // sin phi, theta, psi, cos phi, theta, psi
+};
+
+template <typename S, bool GEN>
+__global__ __launch_bounds__(kAbThreads) void env_rollout_ab_kernel(EnvView<S> v, RolloutIO io,
+                                                                    FieldPtrs<S> fp) {
+    constexpr int OD = 15;
+    constexpr int NQ = (64 * OD / 4 + 63) / 64;
+    constexpr int S_OPS = NQ + 2;
+    static_assert(DR_WS_PRE == 0, "the split kernel reads action t at the top of step t");
+    static_assert(S_OPS + kWsAhead * (S_OPS + 1) <= 63, "the action-load wait count must fit vmcnt");
+    __shared__ __attribute__((aligned(16))) AbLds<S, OD> sh;
+    const int64_t n_ = v.n;
+    const int K = io.k;
+    const int lane = threadIdx.x & 63;
+    const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int p = wid & 3;
+    const int role = wid >> 2;                    // 0 translation, 1 rotation, 2 memory
+    const int ps = p * 64 + lane;                 // this lane's env within the block
+    const int64_t wbase = (int64_t)blockIdx.x * kWsEnvs + p * 64;
+    const int64_t i_own = wbase + lane;
+    const bool live = i_own < n_;
+    const int64_t i = live ? i_own : n_ - 1;
+
+    if (role == 2) {
+        // ---------------- memory wave (env_rollout_ws_kernel's, stores two
+        // phases behind the translation wave, three output slots) ----------
+        const int64_t nvalid = (n_ - wbase) < 64 ? (n_ - wbase) : 64;
+        const bool full = nvalid == 64 && (((uintptr_t)io.obs) & 15) == 0 &&
+                          ((n_ * OD) & 3) == 0;
+        const float4 *acts = reinterpret_cast<const float4 *>(io.actions);
+        const uint64_t gid = (uint64_t)(v.env_id_offset + i);
+        auto load_act = [&](int t) {
+            if constexpr (GEN) {
+                const uint64_t s = io.a_step0 + (uint64_t)t;
+                uint32_t ak0 = io.a_k0, ak1 = io.a_k1;
+                asm volatile("" : "+s"(ak0), "+s"(ak1));
+                const u32x4 r = philox4x32_10(
+                    u32x4{(uint32_t)s, (uint32_t)(s >> 32), (uint32_t)gid,
+                          TAG_ACTION ^ (uint32_t)(gid >> 32)},
+                    ak0, ak1);
+                const float4 act = make_float4(io.a_lo + io.a_span * u01_f32(r.x),
+                                               io.a_lo + io.a_span * u01_f32(r.y),
+                                               io.a_lo + io.a_span * u01_f32(r.z),
+                                               io.a_lo + io.a_span * u01_f32(r.w));
+                sh.act[t % kWsNA][ps] = act;
+                if (io.act_out && live)
+                    st_out(at(reinterpret_cast<float4 *>(io.act_out) + (int64_t)t * n_, i), act);
+            } else if (nvalid > 0) {
+                ws_glds16(at(acts + (int64_t)t * n_, i),
+                          (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void *)
+                              &sh.act[t % kWsNA][p * 64]);
+            }
+        };
+        auto store_out = [&](int t) {
+            if (nvalid <= 0) return;
+            const int so = t % kAbOut;
+            const int64_t row = (int64_t)t * n_;
+            const float *src = &sh.obs[so][p * 64 * OD];
+            float *dst = io.obs + (row + wbase) * OD;
+            const float r = sh.rew[so][ps];
+            const uint8_t d = sh.done[so][ps];
+            if (full) {
+                float4 q[NQ];
+#pragma unroll
+                for (int j = 0; j < NQ; ++j)
+                    if (j * 64 + lane < 64 * OD / 4)
+                        q[j] = reinterpret_cast<const float4 *>(src)[j * 64 + lane];
+#pragma unroll
+                for (int j = 0; j < NQ; ++j)
+                    if (j * 64 + lane < 64 * OD / 4)
+                        st_out(reinterpret_cast<float4 *>(dst) + j * 64 + lane, q[j]);
+            } else {
+                for (int q = lane; q < (int)nvalid * OD; q += 64) st_out(dst + q, src[q]);
+            }
+            if (live) {
+                st_out(at(io.rew + row, i_own), r);
+                st_out(at(io.done + row, i_own), d);
+            }
+        };
+        for (int t = 0; t <= kWsAhead && t < K; ++t) load_act(t);
+        if (!GEN) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");        // actions 0 .. D
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");   // B_(-1)
+        for (int t = 0; t < K; ++t) {
+            if (t + kWsAhead + 1 < K) load_act(t + kWsAhead + 1);
+            if (t >= 2) store_out(t - 2);
+            // action t + 1 lands before B_t.  Issued in phase q = t - D;
+            // younger in the steady state (q >= 2, loads through phase t):
+            // q's S_OPS stores and D phases of one load and S_OPS stores;
+            // otherwise at least this phase's S_OPS stores (t >= D >= 2).
+            if (!GEN && t + 1 < K && t + 1 > kWsAhead) {
+                __builtin_amdgcn_sched_barrier(0);
+                if (!full)
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                else if (t >= kWsAhead + 2 && t + kWsAhead + 1 < K)
+                    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(S_OPS + kWsAhead * (S_OPS + 1))
+                                 : "memory");
+                else
+                    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(S_OPS) : "memory");
+            }
+            asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");   // B_t
+        }
+        asm volatile("s_barrier" ::: "memory");   // B_K: step K - 1's euler / omega staged
+        if (K >= 2) store_out(K - 2);
+        if (K >= 1) store_out(K - 1);
+        return;
+    }
+
+    if (role == 1) {
+        // ---------------- rotation wave ----------------
+        S eul[3], omg[3];
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            eul[k] = *at(fp.p[F_EUL + k], i);
+            omg[k] = *at(fp.p[F_OMG + k], i);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        S sn[3], cs[3];
+        m_sincos3(eul, sn, cs);
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            sh.sc[0][k][ps] = sn[k];
+            sh.sc[0][3 + k][ps] = cs[k];
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");   // B_(-1)
+        // the reset of step t - 1 (done flag staged by the translation wave
+        // before B_(t-1)) and the obs fields of step t - 1
+        auto after_step = [&](int tp) {
+            const bool rs = io.auto_reset && sh.done[tp % kAbOut][ps];
+            if (rs) {
+#pragma unroll
+                for (int k = 0; k < 3; ++k) {
+                    eul[k] = (S)0;
+                    omg[k] = (S)0;
+                    sn[k] = (S)0;      // sincos(+0) = (+0, 1) exactly
+                    cs[k] = (S)1;
+                }
+            }
+            float *srow = &sh.obs[tp % kAbOut][ps * OD];
+#pragma unroll
+            for (int k = 0; k < 3; ++k) {
+                srow[F_EUL + k] = live ? (float)eul[k] : 0.f;
+                srow[F_OMG + k] = live ? (float)omg[k] : 0.f;
+            }
+        };
+        for (int t = 0; t < K; ++t) {
+            const float4 a_cur = sh.act[t % kWsNA][ps];
+            if (t >= 1) after_step(t - 1);
+            const MotorMix mx = motor_mix(a_cur);
+            // physics_step_mixed's angular part, in its order
+            const S tau_phi = (S)kFactor * (S)mx.phi;
+            const S tau_theta = (S)kFactor * (S)mx.theta;
+            const float tau_psi = kKyaw32 * mx.psi;
+            const S sph = sn[0], cph = cs[0], sth = sn[1], cth = cs[1];
+            const S w0 = omg[0], w1 = omg[1], w2 = omg[2];
+            const S sec = (S)1 / cth;
+            const S tth = div_rcp(sth, cth, sec);
+            const S ed2 = ((S)0 * w0 + div_rcp(sph, cth, sec) * w1) + div_rcp(cph, cth, sec) * w2;
+            const S ed0 = ((S)1 * w0 + (sph * tth) * w1) + (cph * tth) * w2;
+            const S ed1 = ((S)0 * w0 + cph * w1) + (-sph) * w2;
+            eul[0] += ed0 * v.dt;
+            eul[1] += ed1 * v.dt;
+            eul[2] += ed2 * v.dt;
+            const S wd0 = div_rcp(tau_phi - (S)(kIyy - kIzz) * w1 * w2, (S)kIxx, (S)(1.0 / kIxx));
+            const S wd1 = div_rcp(tau_theta - (S)(kIzz - kIxx) * w0 * w2, (S)kIyy, (S)(1.0 / kIyy));
+            const S wd2 = div_rcp((S)tau_psi - (S)(kIxx - kIyy) * w0 * w1, (S)kIzz, (S)(1.0 / kIzz));
+            omg[0] += wd0 * v.dt;
+            omg[1] += wd1 * v.dt;
+            omg[2] += wd2 * v.dt;
+            // the next step's sincos (of the angles before any reset of this
+            // step: the translation wave substitutes (+0, 1) after one)
+            m_sincos3(eul, sn, cs);
+            if (t + 1 < K) {
+#pragma unroll
+                for (int k = 0; k < 3; ++k) {
+                    sh.sc[(t + 1) & 1][k][ps] = sn[k];
+                    sh.sc[(t + 1) & 1][3 + k][ps] = cs[k];
+                }
+            }
+            __builtin_amdgcn_sched_barrier(0);
+            asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");   // B_t
+        }
+        if (K >= 1) after_step(K - 1);
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");   // B_K
+        if (live) {
+#pragma unroll
+            for (int k = 0; k < 3; ++k) {
+                st_out(at(fp.p[F_EUL + k], i), eul[k]);
+                st_out(at(fp.p[F_OMG + k], i), omg[k]);
+            }
+        }
+        return;
+    }
+
+    // ---------------- translation wave ----------------
+    const uint64_t gid = (uint64_t)(v.env_id_offset + i);
+    S st[F_N];                // euler / omega entries unused here
+#pragma unroll
+    for (int k = 0; k < F_EUL; ++k) st[k] = *at(fp.p[k], i);
+#pragma unroll
+    for (int k = F_TGT; k < F_N; ++k) st[k] = *at(fp.p[k], i);
+#pragma unroll
+    for (int k = F_EUL; k < F_TGT; ++k) st[k] = (S)0;
+    int32_t step = *at(fp.step, i);
+    int32_t ep_num = *at(fp.ep_num, i);
+    double eps = *at(fp.eps, i);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    bool reset_any = false, prev_rs = false;
+    EnvView<S> vk = v;
+    constexpr int kResetAhead = DR_WS_RA;
+    u32x4 nd[1] = {};
+    bool nd_ok = false;
+    int32_t max_steps;
+    asm volatile("v_mov_b32 %0, %1" : "=v"(max_steps) : "s"(v.max_steps));
+    asm volatile("s_barrier" ::: "memory");                          // B_(-1)
+    for (int t = 0; t < K; ++t) {
+        asm volatile("" : "+s"(vk.seed_lo), "+s"(vk.seed_hi));
+        const float4 a_cur = sh.act[t % kWsNA][ps];
+        S sn[3], cs[3];
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            sn[k] = prev_rs ? (S)0 : sh.sc[t & 1][k][ps];
+            cs[k] = prev_rs ? (S)1 : sh.sc[t & 1][3 + k][ps];
+        }
+        const MotorMix mx = motor_mix(a_cur);
+        if (t % kResetAhead == 0 && !nd_ok) {
+            nd[0] = philox4x32_10(u32x4{(uint32_t)(ep_num + 1), (uint32_t)gid,
+                                        (uint32_t)(gid >> 32), TAG_RESET},
+                                  vk.seed_lo, vk.seed_hi);
+            nd_ok = true;
+        }
+        // physics_step_mixed's translational part, in its order
+        const float thr = mx.thr;
+        const S sph = sn[0], cph = cs[0], sth = sn[1], cth = cs[1], sps = sn[2], cps = cs[2];
+        const S r02 = cps * sth * cph + sps * sph;
+        const S r12 = sps * sth * cph - cps * sph;
+        const S r22 = cth * cph;
+        const S T = (S)thr;
+        const S acc0 = (S)0 + (r02 * T) / (S)kMass;
+        const S acc1 = (S)0 + (r12 * T) / (S)kMass;
+        const S acc2 = (S)(-kG) + (r22 * T) / (S)kMass;
+        st[F_VEL + 0] += acc0 * v.dt;
+        st[F_VEL + 1] += acc1 * v.dt;
+        st[F_VEL + 2] += acc2 * v.dt;
+#pragma unroll
+        for (int k = 0; k < 3; ++k) st[F_POS + k] += st[F_VEL + k] * v.dt;
+        const S dx = st[F_POS + 0] - st[F_TGT + 0];
+        const S dy = st[F_POS + 1] - st[F_TGT + 1];
+        const S dz = st[F_POS + 2] - st[F_TGT + 2];
+        const S d = m_sqrt((dx * dx + dy * dy) + dz * dz);
+        S r = (S)0.01 * -d;
+        if (d < (S)0.05) r += (S)1;
+        const S px = st[F_POS + 0], py = st[F_POS + 1], pz = st[F_POS + 2];
+        const S pn2 = (px * px + py * py) + pz * pz;
+        const bool crash = (pz < (S)0) || (pn2 > (S)2500);
+        step += 1;
+        const bool done = live && (crash || (step >= max_steps));
+        const bool rs = done && io.auto_reset;
+        if (rs) {
+            step = 0;
+            reset_any = true;
+            if (!nd_ok)
+                nd[0] = philox4x32_10(u32x4{(uint32_t)(ep_num + 1), (uint32_t)gid,
+                                            (uint32_t)(gid >> 32), TAG_RESET},
+                                      vk.seed_lo, vk.seed_hi);
+            gym_reset_regs(vk, i, 0, st, ep_num, eps, &nd[0]);
+            nd_ok = false;
+            ep_num += 1;
+            if (ep_num % 2000 == 0) eps += 0.1;
+        }
+        prev_rs = rs;
+        const int so = t % kAbOut;
+        float *srow = &sh.obs[so][ps * OD];
+#pragma unroll
+        for (int k = 0; k < F_EUL; ++k) srow[k] = live ? (float)st[k] : 0.f;
+#pragma unroll
+        for (int k = 0; k < 3; ++k)
+            srow[12 + k] = live ? (float)(st[F_TGT + k] - st[F_POS + k]) : 0.f;
+        sh.rew[so][ps] = (float)r;
+        sh.done[so][ps] = (uint8_t)done;
+        __builtin_amdgcn_sched_barrier(0);
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");   // B_t
+    }
+    asm volatile("s_barrier" ::: "memory");                          // B_K
+    if (live) {
+#pragma unroll
+        for (int k = 0; k < F_EUL; ++k) st_out(at(fp.p[k], i), st[k]);
+        st_out(at(fp.step, i), step);
+        if (reset_any) {
+#pragma unroll
+            for (int k = F_TGT; k < F_N; ++k) *at(fp.p[k], i) = st[k];
         }
     }
 }
@@ -2142,9 +2478,27 @@ int launch_rollout(dr_handle *h, const RolloutIO &io, hipStream_t st, hipEvent_t
         return c;
     }();
     const bool ws = ws_env >= 0 ? ws_env == 1 : h->n <= (int64_t)kWsEnvs * n_cu;
+    // the split-physics form of the warp-specialised kernel (gym variant,
+    // actions read from HBM; with the in-kernel policy its memory waves' Philox
+    // draws share the SIMD with two physics waves and it measured slower):
+    // DRONERL_ROLLOUT_AB=1 / 0 forces it on / off (A/B)
+    static const int ab_env = [] {
+        const char *r = std::getenv("DRONERL_ROLLOUT_AB");
+        return r ? (std::atoi(r) != 0 ? 1 : 0) : -1;
+    }();
+    bool ab = false;
+    if constexpr (VAR == DR_VARIANT_GYM)
+        ab = ws && rpw == 64 && (ab_env >= 0 ? ab_env == 1 : !GEN);
     // with events: hipExtLaunchKernelGGL binds them to the dispatch packet's
     // own start / end timestamps (no extra packets in the queue)
-    if (ws && rpw == 64) {
+    if (ab) {
+        const dim3 grid(grid_for(h->n, kWsEnvs)), block(kAbThreads);
+        if (e0 || e1)
+            hipExtLaunchKernelGGL((env_rollout_ab_kernel<S, GEN>), grid, block, 0, st, e0, e1, 0,
+                                  v, io, fp);
+        else
+            hipLaunchKernelGGL((env_rollout_ab_kernel<S, GEN>), grid, block, 0, st, v, io, fp);
+    } else if (ws && rpw == 64) {
         const dim3 grid(grid_for(h->n, kWsEnvs)), block(kWsThreads);
         if (e0 || e1)
             hipExtLaunchKernelGGL((env_rollout_ws_kernel<S, VAR, GEN>), grid, block, 0, st, e0,

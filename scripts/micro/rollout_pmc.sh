@@ -25,19 +25,21 @@ res = {"workload": "scripts/micro/rollout_bench.py --envs 65536 --ks 32 --reps 5
                    "one action set), rocprofv3 --pmc, two passes (scripts/micro/rollout_pmc.sh)"}
 for tag in ("false", "true"):   # actions from HBM / in-kernel random policy
     acc = collections.defaultdict(list)
-    ws = False
-    pat = re.compile(r"env_rollout(_ws)?_kernel<double, 0, (64, )?" + tag + ">")
+    ws = ""
+    pat = re.compile(r"env_rollout(_ws|_ab)?_kernel<double, (0, )?(64, )?" + tag + ">")
     for f in glob.glob(out + "/p*/run_counter_collection.csv"):
         for r in csv.DictReader(open(f)):
             mt = pat.search(r["Kernel_Name"])
             if mt:
-                ws = ws or bool(mt.group(1))
+                ws = ws or mt.group(1) or ""
                 acc[r["Counter_Name"]].append(float(r["Counter_Value"]))
     m = {k: sum(v) / len(v) for k, v in acc.items()}
     w, K = m["SQ_WAVES"], 32
-    pw = w / 2 if ws else w                 # physics waves
+    # physics waves: half of the warp-specialised kernel's, two thirds of the
+    # split kernel's (translation + rotation)
+    pw = w / 2 if ws == "_ws" else (2 * w / 3 if ws == "_ab" else w)
     res["random_policy_in_kernel" if tag == "true" else "actions_from_hbm"] = {
-        "kernel": "env_rollout_ws_kernel" if ws else "env_rollout_kernel",
+        "kernel": "env_rollout%s_kernel" % ws,
         "counters_per_launch": {k: round(v, 1) for k, v in sorted(m.items())},
         "valu_insts_per_wave_step": round(m["SQ_INSTS_VALU"] / pw / K, 1),
         "salu_insts_per_wave_step": round(m["SQ_INSTS_SALU"] / pw / K, 1),
