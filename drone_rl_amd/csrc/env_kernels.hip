@@ -1600,6 +1600,14 @@ __global__ __launch_bounds__(kWsThreads) void env_rollout_ws_kernel(EnvView<S> v
 // three output slots.  Every expression is physics_step_mixed's, in its
 // order: outputs bitwise those of the other kernels (tests/test_rollout_gpu.py).
 // ----------------------------------------------------------------------------
+// DR_AB_MREW 1 (default): the translation wave stages the squared target
+// distance and the memory wave forms the reward from it (the same sqrt and
+// reward arithmetic, off the translation wave's instruction stream): 41.3-41.9
+// vs 43.0-44.2 us per 32-step launch, 27.4 vs 28.0 per 20-step launch
+// (scripts/micro/round3_af.sh, bitwise through tests/test_rollout_gpu.py)
+#ifndef DR_AB_MREW
+#define DR_AB_MREW 1
+#endif
 constexpr int kAbThreads = 3 * kWsEnvs;   // 4 translation + 4 rotation + 4 memory waves
 constexpr int kAbOut = 3;                 // output slots
 
@@ -1607,6 +1615,7 @@ template <typename S, int OD>
 struct AbLds {
     float obs[kAbOut][kWsEnvs * OD];
     float rew[kAbOut][kWsEnvs];
+    S d2[DR_AB_MREW ? kAbOut : 1][kWsEnvs];   // MREW: squared target distance
     uint8_t done[kAbOut][kWsEnvs];
     float4 act[kWsNA][kWsEnvs];
     S sc[2][6][kWsEnvs];                  // sin phi, theta, psi, cos phi, theta, psi
@@ -1669,7 +1678,16 @@ __global__ __launch_bounds__(kAbThreads) void env_rollout_ab_kernel(EnvView<S> v
             const int64_t row = (int64_t)t * n_;
             const float *src = &sh.obs[so][p * 64 * OD];
             float *dst = io.obs + (row + wbase) * OD;
-            const float r = sh.rew[so][ps];
+            float r;
+            if constexpr (DR_AB_MREW) {
+                // physics_step_mixed's reward (gym variant) from the staged d^2
+                const S dd = m_sqrt(sh.d2[so][ps]);
+                S rr = (S)0.01 * -dd;
+                if (dd < (S)0.05) rr += (S)1;
+                r = (float)rr;
+            } else {
+                r = sh.rew[so][ps];
+            }
             const uint8_t d = sh.done[so][ps];
             if (full) {
                 float4 q[NQ];
@@ -1858,9 +1876,13 @@ __global__ __launch_bounds__(kAbThreads) void env_rollout_ab_kernel(EnvView<S> v
         const S dx = st[F_POS + 0] - st[F_TGT + 0];
         const S dy = st[F_POS + 1] - st[F_TGT + 1];
         const S dz = st[F_POS + 2] - st[F_TGT + 2];
-        const S d = m_sqrt((dx * dx + dy * dy) + dz * dz);
-        S r = (S)0.01 * -d;
-        if (d < (S)0.05) r += (S)1;
+        const S dist2 = (dx * dx + dy * dy) + dz * dz;
+        S r = (S)0;
+        if constexpr (!DR_AB_MREW) {
+            const S d = m_sqrt(dist2);
+            r = (S)0.01 * -d;
+            if (d < (S)0.05) r += (S)1;
+        }
         const S px = st[F_POS + 0], py = st[F_POS + 1], pz = st[F_POS + 2];
         const S pn2 = (px * px + py * py) + pz * pz;
         const bool crash = (pz < (S)0) || (pn2 > (S)2500);
@@ -1887,7 +1909,10 @@ __global__ __launch_bounds__(kAbThreads) void env_rollout_ab_kernel(EnvView<S> v
 #pragma unroll
         for (int k = 0; k < 3; ++k)
             srow[12 + k] = live ? (float)(st[F_TGT + k] - st[F_POS + k]) : 0.f;
-        sh.rew[so][ps] = (float)r;
+        if constexpr (DR_AB_MREW)
+            sh.d2[so][ps] = dist2;
+        else
+            sh.rew[so][ps] = (float)r;
         sh.done[so][ps] = (uint8_t)done;
         __builtin_amdgcn_sched_barrier(0);
         asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");   // B_t
