@@ -53,10 +53,10 @@ HBM_PEAK_GBS = 8000.0      # MI355X HBM3E spec (MI355X_MICROARCH.md)
 # SQ_ACTIVE_INST_VALU over the physics waves' share of SQ_WAVE_CYCLES of the
 # K = 32 rollout kernel at 65,536 envs (profiles/r03_pmc_rollout.json; an
 # upper bound, the memory waves' VALU included): per physics wave of the
-# split kernel (two per SIMD: 0.65 of the SIMD's cycles together) with actions
+# split kernel (two per SIMD: 0.67 of the SIMD's cycles together) with actions
 # from HBM, of the warp-specialised kernel (one per SIMD) with the in-kernel
 # policy
-PMC_ROLLOUT_VALU_ACTIVE = {"actions_from_hbm": 0.323, "random_policy_in_kernel": 0.628}
+PMC_ROLLOUT_VALU_ACTIVE = {"actions_from_hbm": 0.335, "random_policy_in_kernel": 0.637}
 
 
 def parse():
