@@ -1608,6 +1608,11 @@ __global__ __launch_bounds__(kWsThreads) void env_rollout_ws_kernel(EnvView<S> v
 #ifndef DR_AB_MREW
 #define DR_AB_MREW 1
 #endif
+// DR_AB_PRIO (A/B knob): s_setprio for the translation waves (1) or the
+// rotation waves (2), so that they win the SIMD's issue arbitration
+#ifndef DR_AB_PRIO
+#define DR_AB_PRIO 0
+#endif
 constexpr int kAbThreads = 3 * kWsEnvs;   // 4 translation + 4 rotation + 4 memory waves
 constexpr int kAbOut = 3;                 // output slots
 
@@ -1752,6 +1757,7 @@ __global__ __launch_bounds__(kAbThreads) void env_rollout_ab_kernel(EnvView<S> v
             sh.sc[0][3 + k][ps] = cs[k];
         }
         asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");   // B_(-1)
+        if (DR_AB_PRIO == 2) __builtin_amdgcn_s_setprio(1);
         // the reset of step t - 1 (done flag staged by the translation wave
         // before B_(t-1)) and the obs fields of step t - 1
         auto after_step = [&](int tp) {
@@ -1842,6 +1848,7 @@ __global__ __launch_bounds__(kAbThreads) void env_rollout_ab_kernel(EnvView<S> v
     int32_t max_steps;
     asm volatile("v_mov_b32 %0, %1" : "=v"(max_steps) : "s"(v.max_steps));
     asm volatile("s_barrier" ::: "memory");                          // B_(-1)
+    if (DR_AB_PRIO == 1) __builtin_amdgcn_s_setprio(1);
     for (int t = 0; t < K; ++t) {
         asm volatile("" : "+s"(vk.seed_lo), "+s"(vk.seed_hi));
         const float4 a_cur = sh.act[t % kWsNA][ps];
