@@ -334,7 +334,9 @@ __device__ inline void reset_uniforms(const EnvView<S> &v, int64_t i,
 
 // DroneEnv.reset (drone.py:48-75) on registers st[F_N]; updates ep_num/eps
 // in memory, returns the new step counter (0).
-template <typename S>
+// MEM false: ep_num / eps stay in the caller's registers (a K-step kernel
+// stores their final values once at the end) instead of being written here.
+template <typename S, bool MEM = true>
 __device__ inline void gym_reset_regs(const EnvView<S> &v, int64_t i, int mode,
                                       S st[F_N], int32_t ep_old, double eps,
                                       const u32x4 *pre0 = nullptr) {
@@ -342,7 +344,7 @@ __device__ inline void gym_reset_regs(const EnvView<S> &v, int64_t i, int mode,
     if (!DR_PREFETCH_EPS) eps = v.eps[i];
     if (ep_new % 2000 == 0) {                 // curriculum bump      (68-70)
         eps += 0.1;
-        v.eps[i] = eps;
+        if (MEM) v.eps[i] = eps;
     }
     double u[5];
     if (mode == 0 && DR_ABLATE != 5) {
@@ -371,7 +373,7 @@ __device__ inline void gym_reset_regs(const EnvView<S> &v, int64_t i, int mode,
         reset_uniforms<5>(v, i, ep_new, mode, u);
     }
     DR_STAMP(6);
-    v.ep_num[i] = ep_new;
+    if (MEM) v.ep_num[i] = ep_new;
     st[F_POS + 0] = (S)(u[0] - 0.5);          // (57)
     st[F_POS + 1] = (S)(u[1] - 0.5);
     st[F_POS + 2] = (S)1.0;
@@ -1613,6 +1615,11 @@ __global__ __launch_bounds__(kWsThreads) void env_rollout_ws_kernel(EnvView<S> v
 #ifndef DR_AB_PRIO
 #define DR_AB_PRIO 0
 #endif
+// DR_AB_EPREG 1: the translation wave keeps ep_num / eps in registers through
+// the launch and stores them once at the end (no global store per reset)
+#ifndef DR_AB_EPREG
+#define DR_AB_EPREG 0
+#endif
 constexpr int kAbThreads = 3 * kWsEnvs;   // 4 translation + 4 rotation + 4 memory waves
 constexpr int kAbOut = 3;                 // output slots
 
@@ -1903,7 +1910,7 @@ __global__ __launch_bounds__(kAbThreads) void env_rollout_ab_kernel(EnvView<S> v
                 nd[0] = philox4x32_10(u32x4{(uint32_t)(ep_num + 1), (uint32_t)gid,
                                             (uint32_t)(gid >> 32), TAG_RESET},
                                       vk.seed_lo, vk.seed_hi);
-            gym_reset_regs(vk, i, 0, st, ep_num, eps, &nd[0]);
+            gym_reset_regs<S, !DR_AB_EPREG>(vk, i, 0, st, ep_num, eps, &nd[0]);
             nd_ok = false;
             ep_num += 1;
             if (ep_num % 2000 == 0) eps += 0.1;
@@ -1932,6 +1939,10 @@ __global__ __launch_bounds__(kAbThreads) void env_rollout_ab_kernel(EnvView<S> v
         if (reset_any) {
 #pragma unroll
             for (int k = F_TGT; k < F_N; ++k) *at(fp.p[k], i) = st[k];
+            if (DR_AB_EPREG) {
+                *at(fp.ep_num, i) = ep_num;
+                *at(fp.eps, i) = eps;
+            }
         }
     }
 }
