@@ -56,6 +56,10 @@ HBM_PEAK_GBS = 8000.0      # MI355X HBM3E spec (MI355X_MICROARCH.md)
 # split kernel (two per SIMD: 0.67 of the SIMD's cycles together) with actions
 # from HBM, of the warp-specialised kernel (one per SIMD) with the in-kernel
 # policy
+# dr_rollout's form with actions read at 65,536 envs (DRONERL_ROLLOUT_AB=0
+# restores the one-physics-wave form; env_kernels.hip launch_rollout)
+AB_KERNEL = ("env_rollout_ws_kernel" if os.environ.get("DRONERL_ROLLOUT_AB", "") == "0"
+             else "env_rollout_ab_kernel")
 PMC_ROLLOUT_VALU_ACTIVE = {"actions_from_hbm": 0.335, "random_policy_in_kernel": 0.637}
 
 
@@ -625,7 +629,7 @@ def main():
         roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                 "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": tr,
                 "traffic_GBs": round(tr / per_launch_s / 1e9, 1) if tr else None,
-                "kernel": "env_rollout_ab_kernel", "steps_per_launch": kh, "launches": launches,
+                "kernel": AB_KERNEL, "steps_per_launch": kh, "launches": launches,
                 "bytes_per_env_step": round(bpe, 2),
                 "bytes_basis": "per env-step 16 action + 60 obs + 4 reward + 1 done; per "
                                "launch and env the f64 state read (124 B) and written (100 B) "
@@ -706,7 +710,7 @@ def main():
             ro["random_policy_in_kernel" if gen else "actions_from_hbm"] = {
                 # dr_rollout's default form per action source (env_kernels.hip
                 # launch_rollout)
-                "kernel": "env_rollout_ws_kernel" if gen else "env_rollout_ab_kernel",
+                "kernel": "env_rollout_ws_kernel" if gen else AB_KERNEL,
                 "env_steps_per_s": round(N * k / pl, 1),
                 "avg_launch_us": round(pl * 1e6, 3), "us_per_step": round(pl * 1e6 / k, 3),
                 "bytes_per_env_step": round(bpe, 2),
