@@ -13,8 +13,11 @@ synchronize on both sides; the max over ranks is taken.  `--headline step`
 times one dr_step launch per step instead (the kernel PPO's rollout uses;
 always reported as `single_step`).
 
-Multi-GPU: one process per GPU (torchrun), independent env shards (global
-env ids rank*N+i), no data-path collective -> "scaling": "weak".
+Multi-GPU: one process per GPU, independent env shards (global env ids
+rank*N+i), no data-path collective -> "scaling": "weak".  Two launch forms:
+under torchrun (WORLD_SIZE set; it must equal --gpus), or directly as
+`python bench.py --gpus N`, where this process starts the N ranks itself
+(spawn_ranks; it never touches the GPU) and rank 0 prints the line.
 
 The JSON line also carries
   roofline      the headline kernel: algorithmic bytes per launch (per env-
@@ -568,10 +571,64 @@ def time_ppo(args, rank, world, device, force_dp=False, dp_graph=False, profile=
     return res
 
 
+def _free_port():
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def spawn_ranks(n):
+    """`--gpus N` (N > 1) with no WORLD_SIZE in the environment: start N
+    fresh child processes of this script, one per GPU (RANK = LOCAL_RANK = i,
+    WORLD_SIZE = N, MASTER_ADDR 127.0.0.1 and a free MASTER_PORT), the same
+    environment torchrun gives each rank.  This parent imports neither torch
+    nor HIP: it only waits.  Rank 0 prints the JSON line itself (stdout is
+    inherited); any rank failing ends the others (their exact PIDs) and the
+    parent exits with that rank's status.  Returns the exit status."""
+    import signal
+    import subprocess
+    env0 = dict(os.environ, WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()),
+                DRONERL_BENCH_SPAWNED="1")
+    procs = []
+    for r in range(n):
+        env = dict(env0, RANK=str(r), LOCAL_RANK=str(r))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:],
+                                      env=env))
+    rc = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            r = p.poll()
+            if r is None:
+                continue
+            live.remove(p)
+            if r != 0 and rc == 0:
+                rc = r if r > 0 else 128 - r
+                sys.stderr.write(f"bench.py: rank {procs.index(p)} exited with {r}; "
+                                 f"stopping the other ranks\n")
+                for q in live:
+                    q.send_signal(signal.SIGTERM)
+        time.sleep(0.05)
+    return rc
+
+
 def main():
     args = parse()
     rank = int(os.environ.get("RANK", "0"))
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+    ws_env = os.environ.get("WORLD_SIZE")
+    if ws_env is None and args.gpus > 1:
+        # the direct form `python bench.py --gpus N`: this process becomes the
+        # launcher of N ranks (the torchrun form sets WORLD_SIZE itself)
+        sys.exit(spawn_ranks(args.gpus))
+    world = int(ws_env or "1")
+    if world != args.gpus:
+        sys.stderr.write(f"bench.py: WORLD_SIZE={world} but --gpus {args.gpus}; launch one rank "
+                         f"per GPU with matching counts\n")
+        sys.exit(2)
     local = int(os.environ.get("LOCAL_RANK", "0"))
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
