@@ -53,16 +53,28 @@ BYTES_PER_ENV_STEP = {"f64": 305, "f32": 197}
 # moving-target variant: + 9 f32 motion params read, + 3 f32 obs written
 BYTES_PER_ENV_STEP_MOVING = {"f64": 353, "f32": 245}
 HBM_PEAK_GBS = 8000.0      # MI355X HBM3E spec (MI355X_MICROARCH.md)
+
+
+def rollout_kernel_name(n_envs, n_cu, gen, variant="gym"):
+    """The kernel dr_rollout launches for n_envs envs on a device with n_cu
+    CUs -- the rule of launch_rollout (csrc/env_kernels.hip): the
+    warp-specialised forms while the grid is at most one 256-env block per CU
+    (DRONERL_ROLLOUT_WS=0/1 forces), of which the split-physics form for the
+    gym variant with actions read from HBM; the one-role rollout kernel above
+    that."""
+    ws_env = os.environ.get("DRONERL_ROLLOUT_WS")
+    ws = (ws_env != "0") if ws_env is not None else n_envs <= 256 * n_cu
+    if variant == "gym" and ws and not gen:
+        return "env_rollout_ab_kernel"
+    return "env_rollout_ws_kernel" if ws else "env_rollout_kernel"
+
+
 # SQ_ACTIVE_INST_VALU over the physics waves' share of SQ_WAVE_CYCLES of the
 # K = 32 rollout kernel at 65,536 envs (profiles/r03_pmc_rollout.json; an
 # upper bound, the memory waves' VALU included): per physics wave of the
 # split kernel (two per SIMD: 0.67 of the SIMD's cycles together) with actions
 # from HBM, of the warp-specialised kernel (one per SIMD) with the in-kernel
 # policy
-# dr_rollout's form with actions read at 65,536 envs (DRONERL_ROLLOUT_AB=0
-# restores the one-physics-wave form; env_kernels.hip launch_rollout)
-AB_KERNEL = ("env_rollout_ws_kernel" if os.environ.get("DRONERL_ROLLOUT_AB", "") == "0"
-             else "env_rollout_ab_kernel")
 PMC_ROLLOUT_VALU_ACTIVE = {"actions_from_hbm": 0.335, "random_policy_in_kernel": 0.637}
 
 
@@ -287,17 +299,23 @@ def time_headline(args, n_envs, rank, world, device, steps, warmup, kmax):
         dist.barrier()
     packet_ms = None
     if g is None:
-        # the last untimed repetition right before the timed one, through
-        # dr_rollout_timed: its events ride on the dispatch packets
+        # untimed repetitions right before the timed one, through
+        # dr_rollout_timed: their events ride on the dispatch packets
         # (hipExtLaunchKernel), i.e. the kernels' own start / end timestamps,
         # the durations rocprofv3 reports (the timed launches below stay plain
         # dr_rollout calls: the extended launch costs ~3 us more host wall,
-        # scripts/micro/launch_paths.py)
-        for i, c in enumerate(calls):
-            rcs.append(b.L.dr_rollout_timed(*c, pk0.cuda_event if i == 0 else None,
-                                            pk1.cuda_event if i == len(calls) - 1 else None))
-        torch.cuda.synchronize(device)
-        packet_ms = pk0.elapsed_time(pk1)
+        # scripts/micro/launch_paths.py).  The first extended launch of a
+        # process is a warm-up (BENCH_r03 read 95.9 us from a single one
+        # against 28.6 us by events); the median of 5 after it is reported.
+        reps = []
+        for rep in range(6):
+            for i, c in enumerate(calls):
+                rcs.append(b.L.dr_rollout_timed(*c, pk0.cuda_event if i == 0 else None,
+                                                pk1.cuda_event if i == len(calls) - 1 else None))
+            torch.cuda.synchronize(device)
+            if rep > 0:
+                reps.append(pk0.elapsed_time(pk1))
+        packet_ms = sorted(reps)[len(reps) // 2]
     gc.disable()
     torch.cuda.synchronize(device)
     t0 = time.perf_counter()
@@ -319,8 +337,9 @@ def time_headline(args, n_envs, rank, world, device, steps, warmup, kmax):
         elapsed, gpu_ms = float(t[0]), float(t[1])
     ep = b.get("ep_num").float().mean().item()
     b.close()
+    graphed = g is not None
     del g
-    return elapsed, gpu_ms, launches, ep, packet_ms
+    return elapsed, gpu_ms, launches, ep, packet_ms, graphed
 
 
 def time_rollout(args, n_envs, device, k, reps, gen, variant="gym", state_dtype=None):
@@ -651,6 +670,7 @@ def main():
             dist.init_process_group(backend)
 
     K, N = args.steps, args.envs
+    n_cu = torch.cuda.get_device_properties(device).multi_processor_count
     sb = 8 if args.state_dtype == "f64" else 4
     state_b = (15 * sb + 4) + (12 * sb + 4)      # rollout kernel: state in + out per launch
     tj = {}
@@ -676,7 +696,7 @@ def main():
     el_s, gm_s, ep_s = time_env(args, args.state_dtype, N, rank, world, device, K, args.warmup)
     single = step_block(el_s, gm_s, K, N)
     if args.headline == "rollout":
-        elapsed, gpu_ms, launches, ep, packet_ms = time_headline(
+        elapsed, gpu_ms, launches, ep, packet_ms, graphed = time_headline(
             args, N, rank, world, device, K, args.warmup, args.headline_k)
         per_launch_s = gpu_ms / 1e3 / launches
         bpe = 81 + state_b * launches / K
@@ -686,15 +706,17 @@ def main():
         roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                 "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": tr,
                 "traffic_GBs": round(tr / per_launch_s / 1e9, 1) if tr else None,
-                "kernel": AB_KERNEL, "steps_per_launch": kh, "launches": launches,
+                "kernel": rollout_kernel_name(N, n_cu, False), "steps_per_launch": kh,
+                "launches": launches,
                 "bytes_per_env_step": round(bpe, 2),
                 "bytes_basis": "per env-step 16 action + 60 obs + 4 reward + 1 done; per "
                                "launch and env the f64 state read (124 B) and written (100 B) "
                                "once",
                 "avg_launch_us": round(per_launch_s * 1e6, 3),
-                # the same launches (the untimed repetition right before the
-                # timed one) by their dispatch packets' own timestamps: the
-                # kernel alone, without the event records' queue time
+                # the same launches (median of 5 untimed repetitions right
+                # before the timed one, after a warm-up) by their dispatch
+                # packets' own timestamps: the kernel alone, without the
+                # event records' queue time
                 "avg_launch_us_packet": (round(packet_ms / launches * 1e3, 3)
                                          if packet_ms else None),
                 "limiter": "the f64 step, split by data over two waves per SIMD "
@@ -704,6 +726,7 @@ def main():
     else:
         elapsed, gpu_ms, ep = el_s, gm_s, ep_s
         roof = single["roofline"]
+        graphed = not args.no_graph
     value = N * world * K / elapsed
     out = {
         "metric": "env-steps/s (whole node) + PPO updates/s, 65 536 envs/GPU, 2x256 MLP",
@@ -723,7 +746,7 @@ def main():
                                "random policy, dynamics-kernel throughput (auto-reset in step, "
                                "every step's obs / reward / done written)",
                    "envs_per_gpu": N, "global_envs": N * world,
-                   "state_dtype": args.state_dtype, "hipgraph": True,
+                   "state_dtype": args.state_dtype, "hipgraph": graphed,
                    "kernel": ("dr_rollout (K-step rollout kernel, <= %d steps per launch)"
                               % args.headline_k if args.headline == "rollout"
                               else "dr_step (one launch per step)"),
@@ -746,13 +769,29 @@ def main():
                 "hbm_bytes_per_launch"]
         except (OSError, ValueError, KeyError):
             pass
-        out["companion"] = {"envs": n4, "steps": k4,
+        out["companion"] = {"envs": n4, "steps": k4, "kernel": "env_step_kernel (dr_step)",
                             "env_steps_per_s": round(n4 * k4 / el4, 1),
                             "avg_launch_us": round(pl4 * 1e6, 3),
                             "roofline": {"bound": "hbm", "achieved": round(ach4, 1),
                                          "peak": HBM_PEAK_GBS, "unit": "GB/s",
                                          "frac": round(ach4 / HBM_PEAK_GBS, 4),
                                          "traffic": tr4}}
+        # the headline's own kernel past the 256-MB Infinity Cache: dr_rollout
+        # at 4,194,304 envs, K = 32 steps per launch, actions read from HBM
+        # (one launch writes ~11 GB of obs / reward / done)
+        kr, reps = 32, 4
+        plr = time_rollout(args, n4, device, kr, reps, False)
+        bper = 81 + state_b / kr
+        achr = n4 * kr * bper / plr / 1e9
+        trr = tj.get(f"rollout_{args.state_dtype}_{n4}_k{kr}", {}).get("hbm_bytes_per_launch")
+        out["companion_rollout"] = {
+            "envs": n4, "steps_per_launch": kr, "launches": reps,
+            "kernel": rollout_kernel_name(n4, n_cu, False),
+            "env_steps_per_s": round(n4 * kr / plr, 1), "avg_launch_us": round(plr * 1e6, 3),
+            "bytes_per_env_step": round(bper, 2),
+            "roofline": {"bound": "hbm", "achieved": round(achr, 1), "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": round(achr / HBM_PEAK_GBS, 4), "traffic": trr,
+                         "traffic_GBs": round(trr / plr / 1e9, 1) if trr else None}}
     if world == 1 and args.rollout_k > 0:
         # SURVEY 7 "hard parts" (a): the K-step random-policy rollout kernel,
         # same envs and action stream, every step's obs / rew / done written
@@ -767,7 +806,7 @@ def main():
             ro["random_policy_in_kernel" if gen else "actions_from_hbm"] = {
                 # dr_rollout's default form per action source (env_kernels.hip
                 # launch_rollout)
-                "kernel": "env_rollout_ws_kernel" if gen else AB_KERNEL,
+                "kernel": rollout_kernel_name(N, n_cu, gen),
                 "env_steps_per_s": round(N * k / pl, 1),
                 "avg_launch_us": round(pl * 1e6, 3), "us_per_step": round(pl * 1e6 / k, 3),
                 "bytes_per_env_step": round(bpe, 2),
@@ -805,18 +844,14 @@ def main():
             finally:
                 if dist.is_initialized():
                     dist.destroy_process_group()
-        saved = os.environ.get("DRONERL_STEP_KERNEL")
-        for kern in ("quad", "lane"):
-            os.environ["DRONERL_STEP_KERNEL"] = kern
-            for dn, n in (("f64", N), ("f32", N), ("f64", 1 << 22), ("f32", 1 << 22)):
-                k = 200 if n > N else args.steps
-                el, gm, _ = time_env(args, dn, n, 0, 1, device, k, 20)
-                pl = gm / 1e3 / k
-                ex[f"{kern}_{dn}_{n}"] = {
-                    "env_steps_per_s": round(n * k / el, 1),
-                    "avg_launch_us": round(pl * 1e6, 3),
-                    "achieved_GBs": round(n * BYTES_PER_ENV_STEP[dn] / pl / 1e9, 1)}
-        os.environ["DRONERL_STEP_KERNEL"] = "lane"
+        for dn, n in (("f64", N), ("f32", N), ("f64", 1 << 22), ("f32", 1 << 22)):
+            k = 200 if n > N else args.steps
+            el, gm, _ = time_env(args, dn, n, 0, 1, device, k, 20)
+            pl = gm / 1e3 / k
+            ex[f"step_{dn}_{n}"] = {
+                "env_steps_per_s": round(n * k / el, 1),
+                "avg_launch_us": round(pl * 1e6, 3),
+                "achieved_GBs": round(n * BYTES_PER_ENV_STEP[dn] / pl / 1e9, 1)}
         # configs[4]: the moving-target curriculum, 1M envs over 8 GPUs
         for dn, n in (("f64", 1 << 17), ("f64", 1 << 20)):
             k = 200 if n > N else args.steps
@@ -838,10 +873,6 @@ def main():
             ex[f"rollout_moving_f64_{n}"] = {"env_steps_per_s": round(n * 32 / pl, 1),
                                              "avg_launch_us": round(pl * 1e6, 3),
                                              "us_per_step": round(pl * 1e6 / 32, 3)}
-        if saved is None:
-            os.environ.pop("DRONERL_STEP_KERNEL", None)
-        else:
-            os.environ["DRONERL_STEP_KERNEL"] = saved
         out["extra"] = ex
     if rank == 0:
         print(json.dumps(out), flush=True)

@@ -140,8 +140,6 @@ SIGNATURES = {
     "dr_gemm_x6_split_weights": (c_int, [c_int64, _P, c_int, _P, _P]),
     "dr_gemm_x6": (c_int, [c_int64, c_int64, _P, _P, _P, _P]),
     "dr_gemm_x6_wgrad": (c_int, [c_int64, c_int64, c_int64, _P, _P, _P, _P]),
-    "dr_gemm_x6_l1_pack": (c_int, [c_int64, _P, _P, _P, c_int64, _P, _P, _P]),
-    "dr_gemm_x6_l1": (c_int, [c_int64, c_int64, _P, _P, _P, _P, _P, _P]),
 }
 
 _lib = None

@@ -183,6 +183,22 @@ __device__ inline float tanh_fast(float x) {
 #endif
 }
 
+// Compute units of the current device, looked up once per device index (a
+// process may drive handles on several GPUs).
+inline int device_cu_count() {
+    static int cache[64] = {0};
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) dev = 0;
+    if (cache[dev] == 0) {
+        int n = 0;
+        if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+            n < 1)
+            n = 256;
+        cache[dev] = n;
+    }
+    return cache[dev];
+}
+
 constexpr int kBlock = 256;   // 4 waves of 64
 
 inline unsigned grid_for(int64_t n, int per_block = kBlock) {

@@ -42,23 +42,6 @@ constexpr double kFactor = kArm / 1.4142135623730951;  // L / np.sqrt(2)
 constexpr float kKyaw32 = 0.01f;  // python float * np.float32 -> f32 (NEP 50)
 constexpr double kDt = 0.02;
 
-// Rollout kernel (A/B knobs): DR_RO_PIPE 1 = a full wave's obs rows of step
-// t are read back from the LDS staging buffer at the top of step t + 1 and
-// stored after its physics (two staging buffers per wave), so the LDS round
-// trip hides behind the physics; DR_RO_VM13 1 = the action-load wait counts
-// every younger store of a full wave (vmcnt(13)) instead of vmcnt(4), which
-// also waited for the previous step's reward / done stores.
-#ifndef DR_RO_PIPE
-#define DR_RO_PIPE 0
-#endif
-#ifndef DR_RO_VM13
-#define DR_RO_VM13 0
-#endif
-// DR_RO_PRESC 1 = the next step's Euler sincos formed inside the current
-// step's physics block (physics_step_mixed<PRE>)
-#ifndef DR_RO_PRESC
-#define DR_RO_PRESC 0
-#endif
 // DR_ABLATE (diagnostic builds only, scripts/micro/ablate.sh; never set in
 // the product build): 1 = f32 trig, 2 = no auto-reset, 3 = no LDS obs
 // staging, 4 = divides by reciprocal multiplies, 5 = constant reset draws,
@@ -114,6 +97,8 @@ __device__ unsigned long long g_stamps[16384 * 8];
 #define DR_ENV_WPB 4
 #endif
 constexpr int kEnvBlock = 64 * DR_ENV_WPB;
+// steps per group of the rollout kernels' next-reset Philox draw-ahead
+constexpr int kResetAhead = 8;
 
 // 1: the observation is formed once, after the auto-reset (the terminal
 // obs only when requested); 0: formed before the reset and again for the
@@ -145,45 +130,15 @@ __device__ inline void st_out(T *p, T x) {
     if (DR_NT_STORES) store_nt(p, x);
     else *p = x;
 }
-// 1 (A/B builds only): the device library's sincos(double) instead of trig.h
-#ifndef DR_LIB_TRIG
-#define DR_LIB_TRIG 0
-#endif
-#if DR_ABLATE == 1
-__device__ inline void m_sincos(double x, double *s, double *c) {
-    float fs, fc;
-    __sincosf((float)x, &fs, &fc);
-    *s = fs;
-    *c = fc;
-}
-#elif DR_LIB_TRIG
-__device__ inline void m_sincos(double x, double *s, double *c) { sincos(x, s, c); }
-#else
-// trig.h: 3-FMA reduction + shared polynomials (<= 1 ulp); the library
-// sincos only for |x| >= 2^19 rad, inf and NaN (a branch no lane usually takes)
-__device__ inline void m_sincos(double x, double *s, double *c) {
-    if (sincos_fast_range(x)) {
-        const SinCos t = sincos_medium(x);
-        *s = t.s;
-        *c = t.c;
-    } else {
-        sincos(x, s, c);
-    }
-}
-#define DR_SINCOS3 1
-#endif
-#ifndef DR_SINCOS3
-#define DR_SINCOS3 0
-#endif
-
-__device__ inline void m_sincos(float x, float *s, float *c) { sincosf(x, s, c); }
-
 // The three Euler angles at once: the fast path runs unconditionally for
 // all three (independent chains interleave; the polynomial constants are
 // materialised once), the library path only for out-of-range lanes.
 template <typename S>
 __device__ inline void m_sincos3(const S x[3], S s[3], S c[3]) {
-    if constexpr (DR_SINCOS3 && sizeof(S) == 8) {
+    if constexpr (sizeof(S) == 8) {
+        // trig.h: 3-FMA reduction + shared polynomials (<= 1 ulp); the
+        // library sincos only for |x| >= 2^19 rad, inf and NaN (a branch no
+        // lane usually takes)
 #pragma unroll
         for (int k = 0; k < 3; ++k) {
             const SinCos t = sincos_medium(x[k]);
@@ -197,7 +152,7 @@ __device__ inline void m_sincos3(const S x[3], S s[3], S c[3]) {
             for (int k = 0; k < 3; ++k)
                 if (!sincos_fast_range(x[k])) sincos(x[k], &s[k], &c[k]);
         }
-    } else if constexpr (DR_SINCOS3 && sizeof(S) == 4) {
+    } else {
         // f32 state mode: trig.h's sincosf_medium (f64 reduction, f32
         // polynomials, <= 2 ulp); the library sincosf only out of range
 #pragma unroll
@@ -213,9 +168,6 @@ __device__ inline void m_sincos3(const S x[3], S s[3], S c[3]) {
             for (int k = 0; k < 3; ++k)
                 if (!sincosf_fast_range(x[k])) sincosf(x[k], &s[k], &c[k]);
         }
-    } else {
-#pragma unroll
-        for (int k = 0; k < 3; ++k) m_sincos(x[k], &s[k], &c[k]);
     }
 }
 __device__ inline double m_sqrt(double x) { return sqrt(x); }
@@ -334,9 +286,7 @@ __device__ inline void reset_uniforms(const EnvView<S> &v, int64_t i,
 
 // DroneEnv.reset (drone.py:48-75) on registers st[F_N]; updates ep_num/eps
 // in memory, returns the new step counter (0).
-// MEM false: ep_num / eps stay in the caller's registers (a K-step kernel
-// stores their final values once at the end) instead of being written here.
-template <typename S, bool MEM = true>
+template <typename S>
 __device__ inline void gym_reset_regs(const EnvView<S> &v, int64_t i, int mode,
                                       S st[F_N], int32_t ep_old, double eps,
                                       const u32x4 *pre0 = nullptr) {
@@ -344,7 +294,7 @@ __device__ inline void gym_reset_regs(const EnvView<S> &v, int64_t i, int mode,
     if (!DR_PREFETCH_EPS) eps = v.eps[i];
     if (ep_new % 2000 == 0) {                 // curriculum bump      (68-70)
         eps += 0.1;
-        if (MEM) v.eps[i] = eps;
+        v.eps[i] = eps;
     }
     double u[5];
     if (mode == 0 && DR_ABLATE != 5) {
@@ -373,7 +323,7 @@ __device__ inline void gym_reset_regs(const EnvView<S> &v, int64_t i, int mode,
         reset_uniforms<5>(v, i, ep_new, mode, u);
     }
     DR_STAMP(6);
-    if (MEM) v.ep_num[i] = ep_new;
+    v.ep_num[i] = ep_new;
     st[F_POS + 0] = (S)(u[0] - 0.5);          // (57)
     st[F_POS + 1] = (S)(u[1] - 0.5);
     st[F_POS + 2] = (S)1.0;
@@ -477,14 +427,8 @@ __device__ inline MotorMix motor_mix(float4 act) {
                     ((-a0 + a1) + a2) - a3, ((a0 - a1) + a2) - a3};
 }
 
-// PRE (the K-step rollout kernel): the Euler sincos of this step arrives in
-// sc_in (computed at the end of the previous step) and the next step's is
-// returned in sc_out, formed from the updated angles in the same basic block
-// as the position / reward chain, so it leaves the step's critical path.
-// The same m_sincos3 on the same angles: bitwise the non-PRE step.
-template <typename S, int VAR, bool PRE = false>
-__device__ inline S physics_step_mixed(S st[F_N], MotorMix mx, S dt, bool &crash,
-                                       const S *sc_in = nullptr, S *sc_out = nullptr) {
+template <typename S, int VAR>
+__device__ inline S physics_step_mixed(S st[F_N], MotorMix mx, S dt, bool &crash) {
 #if DR_ABLATE == 6
     // diagnostic: no physics (loads / stores / reset / obs as built)
 #pragma unroll
@@ -502,15 +446,7 @@ __device__ inline S physics_step_mixed(S st[F_N], MotorMix mx, S dt, bool &crash
     // One sincos per angle: a shared range reduction yields exactly the
     // separate sin() and cos() results at half the instructions.
     S sn[3], cs[3];
-    if constexpr (PRE) {
-#pragma unroll
-        for (int k = 0; k < 3; ++k) {
-            sn[k] = sc_in[k];
-            cs[k] = sc_in[3 + k];
-        }
-    } else {
-        m_sincos3(&st[F_EUL], sn, cs);
-    }
+    m_sincos3(&st[F_EUL], sn, cs);
     DR_STAMP(1);
     const S sph = sn[0], cph = cs[0], sth = sn[1], cth = cs[1], sps = sn[2], cps = cs[2];
     // R(old euler) column 2 (drone.py:169-173): thrust is body-z only.
@@ -545,7 +481,6 @@ __device__ inline S physics_step_mixed(S st[F_N], MotorMix mx, S dt, bool &crash
     st[F_EUL + 0] += ed0 * dt;
     st[F_EUL + 1] += ed1 * dt;
     st[F_EUL + 2] += ed2 * dt;
-    if constexpr (PRE) m_sincos3(&st[F_EUL], sc_out, sc_out + 3);
 
     // Angular dynamics, diagonal inertia, old omega (135-139).
 #if DR_ABLATE == 4
@@ -902,7 +837,7 @@ __global__ __launch_bounds__(kEnvBlock) void env_rollout_kernel(EnvView<S> v, Ro
                                                                 FieldPtrs<S> fp) {
     constexpr int OD = VAR == DR_VARIANT_GYM ? 15 : (VAR == DR_VARIANT_MOVING ? 18 : 12);
     constexpr bool GYMLIKE = VAR != DR_VARIANT_VECTORIZED;
-    __shared__ float4 sh4[(DR_RO_PIPE ? 2 : 1) * kEnvBlock * OD / 4];
+    __shared__ float4 sh4[kEnvBlock * OD / 4];
     const int64_t n_ = v.n;
     const int64_t base = (int64_t)blockIdx.x * (DR_ENV_WPB * RPW);
     const int lane_ = threadIdx.x & 63;
@@ -910,31 +845,6 @@ __global__ __launch_bounds__(kEnvBlock) void env_rollout_kernel(EnvView<S> v, Ro
     const bool live = i_own < n_;
     const int64_t i = live ? i_own : n_ - 1;
     const uint64_t gid = (uint64_t)(v.env_id_offset + i);
-    // DR_RO_PIPE: this wave's rows are all live and every step's obs rows
-    // start 16-byte aligned (wave-uniform; else the unpipelined staging)
-    const int64_t wbase_ = base + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) * RPW;
-    const bool pipe = DR_RO_PIPE && !GEN && RPW == 64 && wbase_ + RPW <= n_ &&
-                      (((uintptr_t)io.obs) & 15) == 0 && ((n_ * OD) & 3) == 0 &&
-                      ((wbase_ * OD) & 3) == 0;
-    constexpr int NQ = (64 * OD + 255) / 256;     // float4 stores per lane and step
-    float4 *const stg0 = sh4 + (threadIdx.x >> 6) * (64 * OD / 4);
-    float4 *const stg1 = stg0 + kEnvBlock * OD / 4;
-    float4 pend[NQ];                               // step t - 1's rows, read back
-    (void)pend;
-    // read back step t's staged rows (issued early), then store them
-    auto pipe_read = [&](int t) {
-        const float4 *src = (t & 1) ? stg1 : stg0;
-#pragma unroll
-        for (int q = 0; q < NQ; ++q)
-            if (q * 64 + lane_ < 64 * OD / 4) pend[q] = src[q * 64 + lane_];
-    };
-    auto pipe_store = [&](int t) {
-        float4 *dst = reinterpret_cast<float4 *>(io.obs + ((int64_t)t * n_ + wbase_) * OD);
-#pragma unroll
-        for (int q = 0; q < NQ; ++q)
-            if (q * 64 + lane_ < 64 * OD / 4) st_out(&dst[q * 64 + lane_], pend[q]);
-    };
-
     S st[F_N];
 #pragma unroll
     for (int k = F_EUL; k < F_N - 3; ++k) st[k] = *at(fp.p[k], i);
@@ -978,7 +888,6 @@ __global__ __launch_bounds__(kEnvBlock) void env_rollout_kernel(EnvView<S> v, Ro
     // waves hold a resetting env at each step under the random policy).  A
     // lane resetting twice within one group draws in the branch as before;
     // the draws are the same Philox words either way.
-    constexpr int kResetAhead = 8;
     constexpr int NB = VAR == DR_VARIANT_MOVING ? 4 : 1;   // Philox blocks per reset
     u32x4 nd[NB] = {};
     bool nd_ok = false;
@@ -987,10 +896,6 @@ __global__ __launch_bounds__(kEnvBlock) void env_rollout_kernel(EnvView<S> v, Ro
     // step (a scalar load and its wait on the critical path)
     int32_t max_steps;
     asm volatile("v_mov_b32 %0, %1" : "=v"(max_steps) : "s"(v.max_steps));
-    // DR_RO_PRESC: this step's Euler sincos, formed at the end of the
-    // previous step (physics_step_mixed<PRE>); (0, 1) after a reset
-    S sc[6];
-    if (DR_RO_PRESC) m_sincos3(&st[F_EUL], sc, sc + 3);
     // one step from the action's motor mixes: the body of env_step_kernel
     // on registers
     auto step_one = [&](const MotorMix mx, const int t) {
@@ -1005,19 +910,10 @@ __global__ __launch_bounds__(kEnvBlock) void env_rollout_kernel(EnvView<S> v, Ro
                 nd_ok = true;
             }
         }
-        if (DR_RO_PIPE && pipe && t > 0) pipe_read(t - 1);
         if constexpr (VAR == DR_VARIANT_MOVING)
             moving_target(cen, mp, step + 1, (float)v.dt, &st[F_TGT], tvel);
         bool crash;
-        S sc_next[6];
-        const S r = DR_RO_PRESC
-                        ? physics_step_mixed<S, VAR, true>(st, mx, v.dt, crash, sc, sc_next)
-                        : physics_step_mixed<S, VAR>(st, mx, v.dt, crash);
-        if (DR_RO_PRESC) {
-#pragma unroll
-            for (int k = 0; k < 6; ++k) sc[k] = sc_next[k];
-        }
-        if (DR_RO_PIPE && pipe && t > 0) pipe_store(t - 1);
+        const S r = physics_step_mixed<S, VAR>(st, mx, v.dt, crash);
         step += 1;
         const bool done = live && (crash || (step >= max_steps));
         const int64_t row = (int64_t)t * n_;
@@ -1041,15 +937,6 @@ __global__ __launch_bounds__(kEnvBlock) void env_rollout_kernel(EnvView<S> v, Ro
                 // (drone.py:61, 68-70), carried on in registers
                 ep_num += 1;
                 if (ep_num % 2000 == 0) eps += 0.1;
-                // the reset's Euler angles are +0: sincos(+0) = (+0, 1)
-                // exactly (m_sincos3: k = 0, r = +0)
-                if (DR_RO_PRESC) {
-#pragma unroll
-                    for (int k = 0; k < 3; ++k) {
-                        sc[k] = (S)0;
-                        sc[3 + k] = (S)1;
-                    }
-                }
             }
         }
         make_obs<S, OD>(st, ob, tvel);
@@ -1061,10 +948,6 @@ __global__ __launch_bounds__(kEnvBlock) void env_rollout_kernel(EnvView<S> v, Ro
         // per 32-step launch at 65,536 envs)
         if (DR_ABLATE == 7) {
             asm volatile("" ::"v"(ob[0]), "v"(ob[5]), "v"(ob[14 % OD]));
-        } else if (pipe) {
-            float *sw = reinterpret_cast<float *>((t & 1) ? stg1 : stg0);
-#pragma unroll
-            for (int k = 0; k < OD; ++k) sw[lane_ * OD + k] = ob[k];
         } else {
             store_obs_wave<OD, RPW>(reinterpret_cast<float *>(sh4), ob, io.obs + row * OD, n_);
         }
@@ -1129,10 +1012,7 @@ __global__ __launch_bounds__(kEnvBlock) void env_rollout_kernel(EnvView<S> v, Ro
                 // younger than step t's action load (issued at the top of step
                 // t - 2): each of steps t - 2 and t - 1 issues its reward,
                 // done and NQ obs-row stores, step t - 1 the next load
-                if (DR_RO_VM13 && pipe && NQ == 4)
-                    asm volatile("s_waitcnt vmcnt(13)" ::: "memory");
-                else
-                    asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+                asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
             }
             const MotorMix mx = motor_mix(make_float4(r.x, r.y, r.z, r.w));
             asm volatile("" ::"v"(mx.thr), "v"(mx.phi), "v"(mx.theta), "v"(mx.psi));
@@ -1151,10 +1031,6 @@ __global__ __launch_bounds__(kEnvBlock) void env_rollout_kernel(EnvView<S> v, Ro
         // a wave with no live lane never waited for its loads: none may
         // still be writing registers the code below reuses
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    if (DR_RO_PIPE && pipe && io.k > 0) {          // the last step's rows
-        pipe_read(io.k - 1);
-        pipe_store(io.k - 1);
     }
     if (live) {
 #pragma unroll
@@ -1214,35 +1090,15 @@ __global__ __launch_bounds__(kEnvBlock) void env_rollout_kernel(EnvView<S> v, Ro
 #ifndef DR_WS_ABL
 #define DR_WS_ABL 0
 #endif
-// A/B knobs: DR_WS_PRIO 1 = the physics waves at s_setprio 1 (they win issue
-// arbitration against their memory-wave partner); DR_WS_RA = steps per
-// group of the next-reset Philox draw-ahead
-#ifndef DR_WS_PRIO
-#define DR_WS_PRIO 0
-#endif
-#ifndef DR_WS_RA
-#define DR_WS_RA 8
-#endif
 constexpr int kWsEnvs = 256;                 // envs per block: 4 physics waves
 constexpr int kWsThreads = 2 * kWsEnvs;
-// DR_WS_PRE (A/B knob; measured 1-2 us slower per 32-step launch, so 0):
-// 1: the physics wave reads action t + 1 from LDS at the top of
-// step t (its LDS latency hidden behind the step), so the memory waves land
-// it one barrier earlier: loads D = 3 steps ahead; 0: action t read at the
-// top of step t, D = 2.  Ring slots: D + 2 (PRE: action 0 is read after
-// B_(-1), in phase 0, when action D + 1 is issued; so slot 0 must not be its
-// slot).
-#ifndef DR_WS_PRE
-#define DR_WS_PRE 0
-#endif
-// DR_WS_AHEAD (A/B knob): D, how many steps ahead of the physics the memory
-// waves issue an action load (the hand-counted waits below are generic in D;
-// vmcnt holds at most 63, so S_OPS + D * (S_OPS + 1) must stay below it)
-#ifndef DR_WS_AHEAD
-#define DR_WS_AHEAD (DR_WS_PRE ? 3 : 2)
-#endif
-constexpr int kWsAhead = DR_WS_AHEAD;  // D
+// D: how many steps ahead of the physics the memory waves issue an action
+// load (the physics wave reads action t at the top of step t; the
+// hand-counted waits below are generic in D; vmcnt holds at most 63, so
+// S_OPS + D * (S_OPS + 1) must stay below it).  Ring slots: D + 2.
+constexpr int kWsAhead = 2;                  // D
 constexpr int kWsNA = kWsAhead + 2;          // action ring slots
+
 
 // global_load_lds_dwordx4: lane l's 16 bytes land at LDS byte lds_base + 16 l
 // (the wave's 64 actions as one 1-KB slot).  It clobbers m0, which the
@@ -1256,16 +1112,6 @@ __device__ inline void ws_glds16(const void *gptr, uint32_t lds_base) {
 }
 #pragma clang diagnostic pop
 
-// DR_WS_MWR 1 (A/B knob, gym variant): the memory waves draw the physics
-// waves' reset Philox blocks (see the kernel).  Bitwise the same outputs but
-// slower (46.8-48.8 vs 45.8-46.3 us per 32-step launch; 51.7 vs 44.5 with
-// the in-kernel policy, whose actions the memory waves draw too): the two
-// waves of a SIMD share its VALU issue, so moving the draws across does not
-// take them off the physics wave's path (MI355X_MICROARCH.md, two waves per
-// SIMD, item 3)
-#ifndef DR_WS_MWR
-#define DR_WS_MWR 0
-#endif
 
 template <int OD>
 struct WsLds {
@@ -1273,7 +1119,6 @@ struct WsLds {
     float rew[2][kWsEnvs];
     uint8_t done[2][kWsEnvs];
     float4 act[kWsNA][kWsEnvs];
-    u32x4 rnd[2][2][kWsEnvs];                // reset draw candidates [slot][ep + 1 | ep + 2]
 };
 
 template <typename S, int VAR, bool GEN>
@@ -1284,7 +1129,7 @@ __global__ __launch_bounds__(kWsThreads) void env_rollout_ws_kernel(EnvView<S> v
     constexpr int NQ = (64 * OD / 4 + 63) / 64;  // float4 rows-stores per lane and step
     // the hand-counted wait assumes NQ obs + 1 reward + 1 done store per phase
     constexpr int S_OPS = NQ + 2;
-    static_assert(S_OPS + (kWsAhead - DR_WS_PRE) * (S_OPS + 1) <= 63,
+    static_assert(S_OPS + kWsAhead * (S_OPS + 1) <= 63,
                   "the action-load wait count must fit vmcnt");
     __shared__ __attribute__((aligned(16))) WsLds<OD> sh;
     const int64_t n_ = v.n;
@@ -1357,54 +1202,21 @@ __global__ __launch_bounds__(kWsThreads) void env_rollout_ws_kernel(EnvView<S> v
                 st_out(at(io.done + row, i_own), d);
             }
         };
-        // MWR: the reset draws of the partner's lanes.  A physics wave that
-        // resets at step t needs block 0 of Philox(ep + 1) for the episode
-        // number ep after step t - 1.  Here, at phase t - 1, the memory wave
-        // knows ep after step t - 2 (from the staged done flags) and
-        // publishes both candidates, Philox(ep + 1) and Philox(ep + 2), in
-        // slot t & 1; the physics wave picks by whether it reset at step
-        // t - 1.  After a reset the pair shifts and one new block is drawn.
-        constexpr bool MWR = DR_WS_MWR && VAR == DR_VARIANT_GYM && DR_WS_ABL != 5;
-        int32_t mw_ep = 0;
-        u32x4 c1{}, c2{};
-        auto draw = [&](int32_t e) {
-            return philox4x32_10(u32x4{(uint32_t)e, (uint32_t)gid, (uint32_t)(gid >> 32),
-                                       TAG_RESET},
-                                 v.seed_lo, v.seed_hi);
-        };
-        auto publish = [&](int slot) {
-            sh.rnd[slot][0][p * 64 + lane] = c1;
-            sh.rnd[slot][1][p * 64 + lane] = c2;
-        };
-        if constexpr (MWR) {
-            mw_ep = *at(fp.ep_num, i);
-            c1 = draw(mw_ep + 1);
-            c2 = draw(mw_ep + 2);
-            publish(0);                           // for step 0
-        }
         for (int t = 0; t <= kWsAhead && t < K; ++t) load_act(t);
-        if (!GEN || MWR) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // actions 0 .. D
+        if (!GEN) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // actions 0 .. D
         asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");   // B_(-1)
         if (DR_WS_ABL == 6) return;
         for (int t = 0; t < K; ++t) {
             if (t + kWsAhead + 1 < K) load_act(t + kWsAhead + 1);
-            if constexpr (MWR) {
-                if (t >= 1 && io.auto_reset && sh.done[(t - 1) & 1][p * 64 + lane]) {
-                    mw_ep += 1;                   // the partner reset at step t - 1
-                    c1 = c2;
-                    c2 = draw(mw_ep + 2);
-                }
-                if (t + 1 < K) publish((t + 1) & 1);
-            }
             if (t >= 1) store_out(t - 1);
-            // action a = t + 1 + PRE must have landed before B_t (actions
-            // 0 .. D did before B_(-1)).  It was issued first in phase
-            // q = a - D - 1 = t - (D - PRE); younger in the steady state: q's
-            // S_OPS stores and D - PRE phases of one load and S_OPS stores;
-            // elsewhere at least this phase's S_OPS stores (t >= 1 here).  A
-            // ragged wave waits for every op.
-            constexpr int AH = kWsAhead - DR_WS_PRE;
-            if (!GEN && t + 1 + DR_WS_PRE < K && t + 1 + DR_WS_PRE > kWsAhead) {
+            // action a = t + 1 must have landed before B_t (actions 0 .. D
+            // did before B_(-1)).  It was issued first in phase q = a - D - 1
+            // = t - D; younger in the steady state: q's S_OPS stores and D
+            // phases of one load and S_OPS stores; elsewhere at least this
+            // phase's S_OPS stores (t >= 1 here).  A ragged wave waits for
+            // every op.
+            constexpr int AH = kWsAhead;
+            if (!GEN && t + 1 < K && t + 1 > kWsAhead) {
                 __builtin_amdgcn_sched_barrier(0);
                 if (!full)
                     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1455,34 +1267,19 @@ __global__ __launch_bounds__(kWsThreads) void env_rollout_ws_kernel(EnvView<S> v
     bool reset_any = false;
     float ob[OD];
     EnvView<S> vk = v;
-    // the next reset's Philox blocks drawn ahead, once per group of steps
-    // (env_rollout_kernel)
-    constexpr int kResetAhead = DR_WS_RA;
-    if (DR_WS_PRIO) __builtin_amdgcn_s_setprio(1);
+    // the next reset's Philox blocks drawn ahead, once per group of
+    // kResetAhead steps (env_rollout_kernel)
     constexpr int NB = VAR == DR_VARIANT_MOVING ? 4 : 1;
     u32x4 nd[NB] = {};
     bool nd_ok = false;
-    // MWR: the reset draw comes from the memory wave (prev_reset picks the
-    // candidate: did this lane reset at the previous step)
-    constexpr bool MWR = DR_WS_MWR && VAR == DR_VARIANT_GYM && DR_WS_ABL != 5;
-    bool prev_reset = false;
     int32_t max_steps;
     asm volatile("v_mov_b32 %0, %1" : "=v"(max_steps) : "s"(v.max_steps));
     asm volatile("s_barrier" ::: "memory");                          // B_(-1)
-    float4 a_next = sh.act[0][p * 64 + lane];
     for (int t = 0; t < K; ++t) {
         asm volatile("" : "+s"(vk.seed_lo), "+s"(vk.seed_hi));
-        float4 a_cur;
-        if (DR_WS_PRE) {
-            a_cur = a_next;
-            if (t + 1 < K) a_next = sh.act[(t + 1) % kWsNA][p * 64 + lane];
-        } else {
-            a_cur = sh.act[DR_WS_ABL == 6 ? 0 : t % kWsNA][p * 64 + lane];
-        }
+        const float4 a_cur = sh.act[DR_WS_ABL == 6 ? 0 : t % kWsNA][p * 64 + lane];
         const MotorMix mx = motor_mix(a_cur);
-        u32x4 cand{};
-        if constexpr (MWR) cand = sh.rnd[t & 1][prev_reset ? 1 : 0][p * 64 + lane];
-        if constexpr (GYMLIKE && !MWR) {
+        if constexpr (GYMLIKE) {
             if (t % kResetAhead == 0 && !nd_ok && DR_WS_ABL != 5) {
 #pragma unroll
                 for (int b = 0; b < NB; ++b)
@@ -1508,16 +1305,14 @@ __global__ __launch_bounds__(kWsThreads) void env_rollout_ws_kernel(EnvView<S> v
         const bool done = live && (crash || (step >= max_steps));
         if constexpr (GYMLIKE) {
             const bool rs = done && io.auto_reset && DR_WS_ABL != 3;
-            if (MWR) prev_reset = rs;
             if (rs) {
                 step = 0;
                 reset_any = true;
-                if (MWR) nd[0] = cand;
                 // a second reset within the group: draw its blocks here (the
                 // same words the reset would draw; always passing the array
                 // keeps it in registers -- a pointer-or-null argument put it
                 // on the scratch stack)
-                if (!MWR && !nd_ok && DR_WS_ABL != 5) {
+                if (!nd_ok && DR_WS_ABL != 5) {
 #pragma unroll
                     for (int b = 0; b < NB; ++b)
                         nd[b] = philox4x32_10(u32x4{(uint32_t)(ep_num + 1), (uint32_t)gid,
@@ -1602,32 +1397,17 @@ __global__ __launch_bounds__(kWsThreads) void env_rollout_ws_kernel(EnvView<S> v
 // three output slots.  Every expression is physics_step_mixed's, in its
 // order: outputs bitwise those of the other kernels (tests/test_rollout_gpu.py).
 // ----------------------------------------------------------------------------
-// DR_AB_MREW 1 (default): the translation wave stages the squared target
-// distance and the memory wave forms the reward from it (the same sqrt and
-// reward arithmetic, off the translation wave's instruction stream): 41.3-41.9
-// vs 43.0-44.2 us per 32-step launch, 27.4 vs 28.0 per 20-step launch
-// (scripts/micro/round3_af.sh, bitwise through tests/test_rollout_gpu.py)
-#ifndef DR_AB_MREW
-#define DR_AB_MREW 1
-#endif
-// DR_AB_PRIO (A/B knob): s_setprio for the translation waves (1) or the
-// rotation waves (2), so that they win the SIMD's issue arbitration
-#ifndef DR_AB_PRIO
-#define DR_AB_PRIO 0
-#endif
-// DR_AB_EPREG 1: the translation wave keeps ep_num / eps in registers through
-// the launch and stores them once at the end (no global store per reset)
-#ifndef DR_AB_EPREG
-#define DR_AB_EPREG 0
-#endif
+// The translation wave stages the squared target distance and the memory
+// wave forms the reward from it (the same sqrt and reward arithmetic, off the
+// translation wave's instruction stream): 41.3-41.9 vs 43.0-44.2 us per
+// 32-step launch against the translation wave forming it (round 3).
 constexpr int kAbThreads = 3 * kWsEnvs;   // 4 translation + 4 rotation + 4 memory waves
 constexpr int kAbOut = 3;                 // output slots
 
 template <typename S, int OD>
 struct AbLds {
     float obs[kAbOut][kWsEnvs * OD];
-    float rew[kAbOut][kWsEnvs];
-    S d2[DR_AB_MREW ? kAbOut : 1][kWsEnvs];   // MREW: squared target distance
+    S d2[kAbOut][kWsEnvs];                // squared target distance
     uint8_t done[kAbOut][kWsEnvs];
     float4 act[kWsNA][kWsEnvs];
     S sc[2][6][kWsEnvs];                  // sin phi, theta, psi, cos phi, theta, psi
@@ -1639,7 +1419,6 @@ __global__ __launch_bounds__(kAbThreads) void env_rollout_ab_kernel(EnvView<S> v
     constexpr int OD = 15;
     constexpr int NQ = (64 * OD / 4 + 63) / 64;
     constexpr int S_OPS = NQ + 2;
-    static_assert(DR_WS_PRE == 0, "the split kernel reads action t at the top of step t");
     static_assert(S_OPS + kWsAhead * (S_OPS + 1) <= 63, "the action-load wait count must fit vmcnt");
     __shared__ __attribute__((aligned(16))) AbLds<S, OD> sh;
     const int64_t n_ = v.n;
@@ -1690,16 +1469,11 @@ __global__ __launch_bounds__(kAbThreads) void env_rollout_ab_kernel(EnvView<S> v
             const int64_t row = (int64_t)t * n_;
             const float *src = &sh.obs[so][p * 64 * OD];
             float *dst = io.obs + (row + wbase) * OD;
-            float r;
-            if constexpr (DR_AB_MREW) {
-                // physics_step_mixed's reward (gym variant) from the staged d^2
-                const S dd = m_sqrt(sh.d2[so][ps]);
-                S rr = (S)0.01 * -dd;
-                if (dd < (S)0.05) rr += (S)1;
-                r = (float)rr;
-            } else {
-                r = sh.rew[so][ps];
-            }
+            // physics_step_mixed's reward (gym variant) from the staged d^2
+            const S dd = m_sqrt(sh.d2[so][ps]);
+            S rr = (S)0.01 * -dd;
+            if (dd < (S)0.05) rr += (S)1;
+            const float r = (float)rr;
             const uint8_t d = sh.done[so][ps];
             if (full) {
                 float4 q[NQ];
@@ -1764,7 +1538,6 @@ __global__ __launch_bounds__(kAbThreads) void env_rollout_ab_kernel(EnvView<S> v
             sh.sc[0][3 + k][ps] = cs[k];
         }
         asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");   // B_(-1)
-        if (DR_AB_PRIO == 2) __builtin_amdgcn_s_setprio(1);
         // the reset of step t - 1 (done flag staged by the translation wave
         // before B_(t-1)) and the obs fields of step t - 1
         auto after_step = [&](int tp) {
@@ -1849,13 +1622,11 @@ __global__ __launch_bounds__(kAbThreads) void env_rollout_ab_kernel(EnvView<S> v
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     bool reset_any = false, prev_rs = false;
     EnvView<S> vk = v;
-    constexpr int kResetAhead = DR_WS_RA;
     u32x4 nd[1] = {};
     bool nd_ok = false;
     int32_t max_steps;
     asm volatile("v_mov_b32 %0, %1" : "=v"(max_steps) : "s"(v.max_steps));
     asm volatile("s_barrier" ::: "memory");                          // B_(-1)
-    if (DR_AB_PRIO == 1) __builtin_amdgcn_s_setprio(1);
     for (int t = 0; t < K; ++t) {
         asm volatile("" : "+s"(vk.seed_lo), "+s"(vk.seed_hi));
         const float4 a_cur = sh.act[t % kWsNA][ps];
@@ -1891,12 +1662,6 @@ __global__ __launch_bounds__(kAbThreads) void env_rollout_ab_kernel(EnvView<S> v
         const S dy = st[F_POS + 1] - st[F_TGT + 1];
         const S dz = st[F_POS + 2] - st[F_TGT + 2];
         const S dist2 = (dx * dx + dy * dy) + dz * dz;
-        S r = (S)0;
-        if constexpr (!DR_AB_MREW) {
-            const S d = m_sqrt(dist2);
-            r = (S)0.01 * -d;
-            if (d < (S)0.05) r += (S)1;
-        }
         const S px = st[F_POS + 0], py = st[F_POS + 1], pz = st[F_POS + 2];
         const S pn2 = (px * px + py * py) + pz * pz;
         const bool crash = (pz < (S)0) || (pn2 > (S)2500);
@@ -1910,7 +1675,7 @@ __global__ __launch_bounds__(kAbThreads) void env_rollout_ab_kernel(EnvView<S> v
                 nd[0] = philox4x32_10(u32x4{(uint32_t)(ep_num + 1), (uint32_t)gid,
                                             (uint32_t)(gid >> 32), TAG_RESET},
                                       vk.seed_lo, vk.seed_hi);
-            gym_reset_regs<S, !DR_AB_EPREG>(vk, i, 0, st, ep_num, eps, &nd[0]);
+            gym_reset_regs(vk, i, 0, st, ep_num, eps, &nd[0]);
             nd_ok = false;
             ep_num += 1;
             if (ep_num % 2000 == 0) eps += 0.1;
@@ -1923,10 +1688,7 @@ __global__ __launch_bounds__(kAbThreads) void env_rollout_ab_kernel(EnvView<S> v
 #pragma unroll
         for (int k = 0; k < 3; ++k)
             srow[12 + k] = live ? (float)(st[F_TGT + k] - st[F_POS + k]) : 0.f;
-        if constexpr (DR_AB_MREW)
-            sh.d2[so][ps] = dist2;
-        else
-            sh.rew[so][ps] = (float)r;
+        sh.d2[so][ps] = dist2;
         sh.done[so][ps] = (uint8_t)done;
         __builtin_amdgcn_sched_barrier(0);
         asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");   // B_t
@@ -1939,245 +1701,10 @@ __global__ __launch_bounds__(kAbThreads) void env_rollout_ab_kernel(EnvView<S> v
         if (reset_any) {
 #pragma unroll
             for (int k = F_TGT; k < F_N; ++k) *at(fp.p[k], i) = st[k];
-            if (DR_AB_EPREG) {
-                *at(fp.ep_num, i) = ep_num;
-                *at(fp.eps, i) = eps;
-            }
         }
     }
 }
 
-// ----------------------------------------------------------------------------
-// Quad kernel: 4 lanes per env (one DPP quad), lane k < 3 owns component k of
-// pos / vel / euler / omega / target.  Every lane runs the SAME instruction
-// stream on its own component (SIMD-uniform: selects, never lane-divergent
-// branches), so one env's serial f64 chain -- three sincos range reductions,
-// the divides -- is split three ways and a launch of N envs has 4N lanes of
-// latency-hiding parallelism.  Lane 3 mirrors lane 2's data and its results
-// are discarded.  Values cross lanes with DPP quad_perm broadcasts.
-//
-// Exactness: each component is computed with the reference's own operation
-// order (the selects only pick operands; (-x) and 0*x+y forms are exact), so
-// the quad kernel and the one-lane kernel agree except tan(theta), formed
-// here as sin/cos from the shared sincos (<= 2 ulp from np.tan).
-// ----------------------------------------------------------------------------
-template <int J>
-__device__ inline uint32_t qb(uint32_t x) {
-    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, J * 0x55, 0xF, 0xF, false);
-}
-template <int J>
-__device__ inline float qb(float x) {
-    return __int_as_float((int)qb<J>((uint32_t)__float_as_int(x)));
-}
-template <int J>
-__device__ inline double qb(double x) {
-    const uint32_t lo = qb<J>((uint32_t)__double2loint(x));
-    const uint32_t hi = qb<J>((uint32_t)__double2hiint(x));
-    return __hiloint2double((int)hi, (int)lo);
-}
-
-template <typename T>
-__device__ inline T sel3(int k, T a0, T a1, T a2) {
-    return k == 0 ? a0 : (k == 1 ? a1 : a2);
-}
-
-template <typename S, int VAR, bool MON>
-__global__ __launch_bounds__(kBlock) void env_step_quad_kernel(EnvView<S> v,
-                                                               StepIO io) {
-    constexpr int OD = (VAR == DR_VARIANT_GYM) ? 15 : 12;
-    constexpr int EPB = kBlock / 4;                    // envs per block
-    __shared__ float4 sh4[EPB * OD / 4];
-    float *sh = reinterpret_cast<float *>(sh4);
-    const int q = threadIdx.x & 3;                     // lane in the quad
-    const int k = q < 3 ? q : 2;                       // component owned
-    const int el = threadIdx.x >> 2;                   // env within block
-    const int64_t base = (int64_t)blockIdx.x * EPB;
-    const int64_t e = base + el;
-    const bool live = e < v.n;
-    float ob[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
-    if (live) {
-        // ---- loads: component k of each 3-vector, the action row, counter
-        S p = v.field(F_POS + k)[e];
-        S vel = v.field(F_VEL + k)[e];
-        S ang = v.field(F_EUL + (q < 3 ? q : 1))[e];   // lane 3: theta again
-        S w = v.field(F_OMG + k)[e];
-        S tg;
-        if constexpr (VAR == DR_VARIANT_GYM) {
-            tg = v.field(F_TGT + k)[e];
-        } else {
-            tg = k == 2 ? (S)10.0 : (S)0;
-        }
-        const float4 act = reinterpret_cast<const float4 *>(io.actions)[e];
-        int32_t step = v.step[e];
-
-        // ---- thrust / torque component k (drone.py:106, 113-117)
-        const float a0 = act.x, a1 = act.y, a2 = act.z, a3 = act.w;
-        const float thr = ((a0 + a1) + a2) + a3;
-        const float x0 = k == 1 ? -a0 : a0;
-        const float x1 = k == 2 ? -a1 : a1;
-        const float x2 = k == 0 ? -a2 : a2;
-        const float tsum = ((x0 + x1) + x2) + (-a3);
-        const S tau = k == 2 ? (S)(kKyaw32 * tsum) : (S)kFactor * (S)tsum;
-
-        // ---- one sincos per lane, then share (phi, theta, psi)
-        S sn, cs;
-        m_sincos(ang, &sn, &cs);
-        const S sph = qb<0>(sn), cph = qb<0>(cs);
-        const S sth = qb<1>(sn), cth = qb<1>(cs);
-        const S sps = qb<2>(sn), cps = qb<2>(cs);
-        const S w0 = qb<0>(w), w1 = qb<1>(w), w2 = qb<2>(w);
-
-        // ---- linear: R(old euler) row k, column 2 (drone.py:120-128)
-        const S A = (k == 0 ? cps : sps) * sth;
-        const S t1 = A * cph;
-        const S Bp = (k == 0 ? sps : cps) * sph;
-        const S r = k == 0 ? t1 + Bp : (k == 1 ? t1 - Bp : cth * cph);
-        const S T = (S)thr;
-        const S acc = (k == 2 ? (S)(-kG) : (S)0) + (r * T) / (S)kMass;
-        vel += acc * v.dt;
-        p += vel * v.dt;
-
-        // ---- Euler-angle rates, row k of W(old phi, theta) (131-132, 176-186)
-        S c1, c2;
-        const S sec = (S)1 / cth;                          // also vd:116
-        const S tth = div_rcp(sth, cth, sec);
-        if constexpr (VAR == DR_VARIANT_GYM) {
-            c1 = sel3(k, sph * tth, cph, div_rcp(sph, cth, sec));
-            c2 = sel3(k, cph * tth, -sph, div_rcp(cph, cth, sec));
-        } else {
-            c1 = sel3(k, sph * tth, cph, sph * sec);
-            c2 = sel3(k, cph * tth, -sph, cph * sec);
-        }
-        const S c0 = k == 0 ? (S)1 : (S)0;
-        const S ed = (c0 * w0 + c1 * w1) + c2 * w2;
-        const S ang_new = ang + ed * v.dt;                 // lane 3's is unused
-
-        // ---- angular: omega component k from the old omega (135-139)
-        const S dI = (S)sel3(k, kIyy - kIzz, kIzz - kIxx, kIxx - kIyy);
-        const S Ik = (S)sel3(k, kIxx, kIyy, kIzz);
-        const S wa = k == 0 ? w1 : w0;
-        const S wb = k == 2 ? w1 : w2;
-        const S rIk = (S)sel3(k, 1.0 / kIxx, 1.0 / kIyy, 1.0 / kIzz);
-        const S wd = div_rcp(tau - dI * wa * wb, Ik, rIk);
-        w += wd * v.dt;
-
-        // ---- reward / termination on the new position (142-157)
-        const S dx = p - tg;
-        const S dsq = dx * dx, psq = p * p;
-        const S d = m_sqrt((qb<0>(dsq) + qb<1>(dsq)) + qb<2>(dsq));
-        const S pn = m_sqrt((qb<0>(psq) + qb<1>(psq)) + qb<2>(psq));
-        const S pz = qb<2>(p);
-        S rw;
-        if constexpr (VAR == DR_VARIANT_GYM) {
-            rw = (S)0.01 * -d;
-            if (d < (S)0.05) rw += (S)1;
-        } else {
-            rw = (S)(-0.01) * d;
-            if (d < (S)1) rw += (S)1;
-        }
-        step += 1;
-        const bool crash = (pz < (S)0) || (pn > (S)50);
-        const bool done = crash || (step >= v.max_steps);
-        const float rf = (float)rw;
-        ob[0] = (float)p;
-        ob[1] = (float)vel;
-        ob[2] = (float)ang_new;
-        ob[3] = (float)w;
-        ob[4] = (float)(tg - p);
-
-        float ret = 0.f;
-        int32_t len = 0;
-        if constexpr (MON) {
-            ret = v.ep_ret[e] + rf;
-            len = v.ep_len[e] + 1;
-        }
-        S ang_out = ang_new;
-        if constexpr (VAR == DR_VARIANT_GYM) {
-            if (done && io.auto_reset) {          // quad-uniform branch
-                if (io.term_obs && q < 3) {
-                    float *to = io.term_obs + e * OD;
-#pragma unroll
-                    for (int j = 0; j < 5; ++j) to[j * 3 + k] = ob[j];
-                }
-                // DroneEnv.reset (drone.py:48-75): lane k draws Philox block k
-                const int32_t ep_new = v.ep_num[e] + 1;
-                double u0, u1, u2, u3, u4;
-                if (v.host_u) {
-                    const double *hu = v.host_u + e * 5;
-                    u0 = hu[0]; u1 = hu[1]; u2 = hu[2]; u3 = hu[3]; u4 = hu[4];
-                } else {
-                    const uint64_t gid = (uint64_t)(v.env_id_offset + e);
-                    const u32x4 rr = philox4x32_10(
-                        u32x4{(uint32_t)ep_new, (uint32_t)gid, (uint32_t)(gid >> 32),
-                              TAG_RESET | (uint32_t)(q & 1)},
-                        v.seed_lo, v.seed_hi);
-                    u0 = u01_w32(qb<0>(rr.x));
-                    u1 = u01_w32(qb<0>(rr.y));
-                    u2 = u01_w32(qb<0>(rr.z));
-                    u3 = u01_w32(qb<0>(rr.w));
-                    u4 = u01_w32(qb<1>(rr.x));
-                }
-                double eps = v.eps[e];
-                const bool bump = (ep_new % 2000) == 0;
-                if (bump) eps += 0.1;
-                if (q == 0) {
-                    v.ep_num[e] = ep_new;
-                    if (bump) v.eps[e] = eps;
-                }
-                p = (S)sel3(k, u0 - 0.5, u1 - 0.5, 1.0);
-                tg = (S)sel3(k, eps * u2, eps * u3, eps * u4 + 1.0 + 0.0);
-                vel = (S)0;
-                ang_out = (S)0;
-                w = (S)0;
-                step = 0;
-                if (q < 3) v.field(F_TGT + k)[e] = tg;
-                ob[0] = (float)p;
-                ob[1] = 0.f;
-                ob[2] = 0.f;
-                ob[3] = 0.f;
-                ob[4] = (float)(tg - p);
-            }
-        }
-        if (q < 3) {
-            v.field(F_POS + k)[e] = p;
-            v.field(F_VEL + k)[e] = vel;
-            v.field(F_EUL + k)[e] = ang_out;
-            v.field(F_OMG + k)[e] = w;
-        }
-        if (q == 0) {
-            v.step[e] = step;
-            io.rew[e] = rf;
-            io.done[e] = (uint8_t)done;
-            if constexpr (MON) {
-                if (io.trunc_out) io.trunc_out[e] = (uint8_t)(done && !crash);
-                if (done) {
-                    io.ep_ret_out[e] = ret;
-                    io.ep_len_out[e] = len;
-                    ret = 0.f;
-                    len = 0;
-                }
-                v.ep_ret[e] = ret;
-                v.ep_len[e] = len;
-            }
-        }
-    }
-    // ---- obs rows through LDS, out as contiguous float4 (64 envs/block)
-    if (q < 3) {
-        constexpr int NJ = OD / 3;
-#pragma unroll
-        for (int j = 0; j < NJ; ++j) sh[el * OD + j * 3 + k] = ob[j];
-    }
-    __syncthreads();
-    const int64_t nvalid = (v.n - base) < EPB ? (v.n - base) : EPB;
-    float *dst = io.obs + base * OD;
-    if (nvalid == EPB && (((uintptr_t)dst) & 15) == 0) {
-        float4 *d4 = reinterpret_cast<float4 *>(dst);
-        for (int t = threadIdx.x; t < EPB * OD / 4; t += kBlock) d4[t] = sh4[t];
-    } else {
-        const int total = (int)nvalid * OD;
-        for (int t = threadIdx.x; t < total; t += kBlock) dst[t] = sh[t];
-    }
-}
 
 // Reset (all envs, or those with mask[i] != 0) and write every env's obs.
 // mode: 0 Philox, 1 host uniforms, 2 constant 0.5.  `init` additionally
@@ -2338,7 +1865,6 @@ struct dr_handle {
     int64_t n = 0;
     int64_t stride = 0;
     int obs_dim = 15;
-    bool quad = false;  // true: 4 lanes per env (env_step_quad_kernel)
     // envs per wave of env_step_kernel: 64, or 32 (half-populated waves:
     // twice the waves in flight); chosen by batch size in dr_create
     int rpw = 64;
@@ -2430,13 +1956,6 @@ int launch_step(dr_handle *h, const StepIO &io, hipStream_t st) {
     fp.ep_num = v.ep_num;
     fp.eps = v.eps;
     bool launched = false;
-    if constexpr (VAR != DR_VARIANT_MOVING) {  // the quad A/B kernel has no moving form
-        if (h->quad) {
-            hipLaunchKernelGGL((env_step_quad_kernel<S, VAR, MON>),
-                               dim3(grid_for(h->n, kBlock / 4)), dim3(kBlock), 0, st, v, io);
-            launched = true;
-        }
-    }
     if (!launched && VAR != DR_VARIANT_VECTORIZED && v.host_u) {   // parity mode
         if (h->rpw == 32)
             hipLaunchKernelGGL((env_step_kernel<S, VAR, MON, 32, true, false>),
@@ -2496,11 +2015,6 @@ int launch_rollout(dr_handle *h, const RolloutIO &io, hipStream_t st, hipEvent_t
     fp.step = v.step;
     fp.ep_num = v.ep_num;
     fp.eps = v.eps;
-    // rows per wave: 64 unless DRONERL_ROLLOUT_RPW=32 (A/B; read once)
-    static const int rpw = [] {
-        const char *r = std::getenv("DRONERL_ROLLOUT_RPW");
-        return r && std::atoi(r) == 32 ? 32 : 64;
-    }();
     // The warp-specialised form while its grid is at most one block per CU
     // (n <= 256 x CUs: 65,536 envs on MI355X), where one physics wave per
     // SIMD has nothing else to overlap with; above that the one-role kernel
@@ -2512,51 +2026,32 @@ int launch_rollout(dr_handle *h, const RolloutIO &io, hipStream_t st, hipEvent_t
         const char *r = std::getenv("DRONERL_ROLLOUT_WS");
         return r ? (std::atoi(r) != 0 ? 1 : 0) : -1;
     }();
-    static const int n_cu = [] {
-        int dev = 0, c = 0;
-        if (hipGetDevice(&dev) != hipSuccess ||
-            hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-            c < 1)
-            c = 256;
-        return c;
-    }();
-    const bool ws = ws_env >= 0 ? ws_env == 1 : h->n <= (int64_t)kWsEnvs * n_cu;
-    // the split-physics form of the warp-specialised kernel (gym variant,
-    // actions read from HBM; with the in-kernel policy its memory waves' Philox
-    // draws share the SIMD with two physics waves and it measured slower):
-    // DRONERL_ROLLOUT_AB=1 / 0 forces it on / off (A/B)
-    static const int ab_env = [] {
-        const char *r = std::getenv("DRONERL_ROLLOUT_AB");
-        return r ? (std::atoi(r) != 0 ? 1 : 0) : -1;
-    }();
-    bool ab = false;
-    if constexpr (VAR == DR_VARIANT_GYM)
-        ab = ws && rpw == 64 && (ab_env >= 0 ? ab_env == 1 : !GEN);
+    const bool ws = ws_env >= 0 ? ws_env == 1 : h->n <= (int64_t)kWsEnvs * device_cu_count();
     // with events: hipExtLaunchKernelGGL binds them to the dispatch packet's
     // own start / end timestamps (no extra packets in the queue)
-    if (ab) {
-        const dim3 grid(grid_for(h->n, kWsEnvs)), block(kAbThreads);
-        if (e0 || e1)
-            hipExtLaunchKernelGGL((env_rollout_ab_kernel<S, GEN>), grid, block, 0, st, e0, e1, 0,
-                                  v, io, fp);
-        else
-            hipLaunchKernelGGL((env_rollout_ab_kernel<S, GEN>), grid, block, 0, st, v, io, fp);
-    } else if (ws && rpw == 64) {
-        const dim3 grid(grid_for(h->n, kWsEnvs)), block(kWsThreads);
-        if (e0 || e1)
-            hipExtLaunchKernelGGL((env_rollout_ws_kernel<S, VAR, GEN>), grid, block, 0, st, e0,
-                                  e1, 0, v, io, fp);
-        else
-            hipLaunchKernelGGL((env_rollout_ws_kernel<S, VAR, GEN>), grid, block, 0, st, v, io,
-                               fp);
-    } else if (rpw == 32) {
-        const dim3 grid(grid_for(h->n, DR_ENV_WPB * 32)), block(kEnvBlock);
-        if (e0 || e1)
-            hipExtLaunchKernelGGL((env_rollout_kernel<S, VAR, 32, GEN>), grid, block, 0, st, e0,
-                                  e1, 0, v, io, fp);
-        else
-            hipLaunchKernelGGL((env_rollout_kernel<S, VAR, 32, GEN>), grid, block, 0, st, v, io,
-                               fp);
+    if (ws) {
+        if constexpr (VAR == DR_VARIANT_GYM && !GEN) {
+            // the split-physics form of the warp-specialised kernel (gym
+            // variant, actions read from HBM; with the in-kernel policy its
+            // memory waves' Philox draws share the SIMD with two physics
+            // waves and it measured slower, so GEN keeps the one-physics-wave
+            // form)
+            const dim3 grid(grid_for(h->n, kWsEnvs)), block(kAbThreads);
+            if (e0 || e1)
+                hipExtLaunchKernelGGL((env_rollout_ab_kernel<S, GEN>), grid, block, 0, st, e0,
+                                      e1, 0, v, io, fp);
+            else
+                hipLaunchKernelGGL((env_rollout_ab_kernel<S, GEN>), grid, block, 0, st, v, io,
+                                   fp);
+        } else {
+            const dim3 grid(grid_for(h->n, kWsEnvs)), block(kWsThreads);
+            if (e0 || e1)
+                hipExtLaunchKernelGGL((env_rollout_ws_kernel<S, VAR, GEN>), grid, block, 0, st,
+                                      e0, e1, 0, v, io, fp);
+            else
+                hipLaunchKernelGGL((env_rollout_ws_kernel<S, VAR, GEN>), grid, block, 0, st, v,
+                                   io, fp);
+        }
     } else {
         const dim3 grid(grid_for(h->n, DR_ENV_WPB * 64)), block(kEnvBlock);
         if (e0 || e1)
@@ -2636,11 +2131,6 @@ int dr_create(const dr_config *cfg_in, dr_handle **out) {
     // (same HBM channel bits); DR_STRIDE_PAD elements of skew break that.
     h->stride = (cfg.num_envs + 63) / 64 * 64 + DR_STRIDE_PAD;
     h->obs_dim = cfg.variant == DR_VARIANT_GYM ? 15 : (cfg.variant == DR_VARIANT_MOVING ? 18 : 12);
-    // Step kernel choice: one lane per env unless DRONERL_STEP_KERNEL=quad
-    // (4 lanes per env; fewer serial f64 ops per lane, more total VALU work:
-    // slower on MI355X at every measured size, kept for A/B measurement).
-    if (const char *kk = std::getenv("DRONERL_STEP_KERNEL"))
-        h->quad = std::strcmp(kk, "quad") == 0;
     // Launch form by batch size, from the measured sweep
     // (scripts/micro/ab_sweep.sh, profiles/r01_env_launch_sweep.txt):
     // [0, 384k) 64 rows/wave; [384k, 1.5M) 32 + nontemporal state loads;

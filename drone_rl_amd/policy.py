@@ -220,8 +220,6 @@ class X6Weights:
         self.pol = pol
         self.img = torch.empty(2 * nb, dtype=torch.uint8, device=pol.device)
         self.fwd, self.bwd = self.img[:nb], self.img[nb:]
-        # first-layer-fused forward (dr_gemm_x6_l1): W0 rows + bias, 16 floats
-        self.w0p = torch.empty(2, pol.net_arch[0], 16, dtype=torch.float32, device=pol.device)
 
     def refresh(self):
         from . import _lib
@@ -241,34 +239,6 @@ def x6_weights(pol: "ActorCritic", m: int):
     if pol._x6 is None:
         pol._x6 = X6Weights(pol)
     return pol._x6
-
-
-def x6_l1_enabled(pol: "ActorCritic") -> bool:
-    """The training forward's first two layers in one launch
-    (dr_gemm_x6_l1, the first layer fused into the 256x256 GEMM's prologue;
-    bitwise dr_linear_tanh2 + dr_gemm_x6) when DRONERL_X6_L1=1, for 2x256
-    nets on 15-d observations with the x6 GEMMs.  Off by default: measured
-    slower (176-177 us for the fused launch against
-    122-130 + 38-39 us for the two launches; 5.91 vs 6.01 updates/s on one
-    box) -- the first layer's VALU and scalar loads cannot hide beside the
-    GEMM's MFMAs with its register file full."""
-    return (pol.gemm_x6 and pol.net_arch == (256, 256) and pol.obs_dim == 15 and
-            os.environ.get("DRONERL_X6_L1", "0") == "1")
-
-
-def gemm_x6_l1(pol: "ActorCritic", obs, obs16, xw: "X6Weights", h1, z, mark=None):
-    """h1 (2, m, 256) = tanh(obs W0^T + b0) and z (2, m, 256) = h1 W1^T for
-    both nets: one pack launch (W0 + bias rows, obs padded to 16) and one
-    dr_gemm_x6_l1 launch; bitwise dr_linear_tanh2 + dr_gemm_x6."""
-    from . import _lib
-    L, st = _lib.lib(), torch.cuda.current_stream(obs.device).cuda_stream
-    m = obs.shape[0]
-    _lib.check(L.dr_gemm_x6_l1_pack(2, pol.p2(0, "w").data_ptr(), pol.p2(0, "b").data_ptr(),
-                                    xw.w0p.data_ptr(), m, obs.data_ptr(), obs16.data_ptr(), st))
-    if mark:
-        mark("pack_first")
-    _lib.check(L.dr_gemm_x6_l1(2, m, obs16.data_ptr(), xw.w0p.data_ptr(), xw.fwd.data_ptr(),
-                               z.data_ptr(), h1.data_ptr(), st))
 
 
 def gemm_x6(a, img, out):
@@ -347,8 +317,6 @@ class FusedTrainStep:
         self._g2 = torch.empty(2, M, max(pol.net_arch), **f32)
         self._ws2 = torch.empty(2 * self.C * max(pol.net_arch) ** 2, **f32) if self.C > 1 else None
         self._first = self.K.FirstLayerBackward2(M, pol.obs_dim, pol.net_arch[0], pol.device)
-        # the first-layer-fused forward's padded observation rows
-        self._obs16 = torch.zeros(M, 16, **f32) if x6_l1_enabled(pol) else None
 
     def first_layer_end(self) -> int:
         """Flat offset where the first layer's parameters end (they come
@@ -419,7 +387,7 @@ class FusedTrainStep:
             raise ValueError("defer_finish needs a 2-hidden-layer net and no on_ready")
         mark = self.mark or _no_mark
         hs = hidden_forward(pol, obs, self._acts, self._acts2, rows, top_preact=preact,
-                            mark=self.mark, obs16=self._obs16)
+                            mark=self.mark)
         gz = self._gz2[top]
         stats = head(hs["pi"][top], hs["vf"][top], pol.p("action.w"), pol.p("action.b"),
                      pol.p("value.w"), pol.p("value.b"), pol.log_std, actions, aux,
@@ -555,7 +523,7 @@ def fusable(pol: ActorCritic) -> bool:
 
 @torch.no_grad()
 def hidden_forward(pol: ActorCritic, obs, acts, acts2=None, rows=None, top_preact=False,
-                   mark=None, obs16=None):
+                   mark=None):
     """Hidden activations of the pi and vf MLPs into preallocated buffers
     acts[pre][k] (M, net_arch[k]); with acts2 (the (2, M, n) buffers that
     acts views) each layer's tanh runs once over both MLPs; with rows the
@@ -564,22 +532,10 @@ def hidden_forward(pol: ActorCritic, obs, acts, acts2=None, rows=None, top_preac
     the head kernel, adds the bias and applies tanh on load (top_bias(pol)
     gives the pointers), so the (M, n) tanh pass is skipped and both MLPs'
     top GEMMs run as ONE batched GEMM (no bias epilogue; 125 us against
-    2 x 74 us for two addmm at M = 65,536, MI355X-tuned solutions).
-    With obs16 (an (M, 16) buffer) and the 2x256 x6 path, the first layer is
-    formed inside the 256x256 GEMM's prologue instead (dr_gemm_x6_l1:
-    bitwise the same h1 and z, one launch and 134 MB of HBM traffic less)."""
+    2 x 74 us for two addmm at M = 65,536, MI355X-tuned solutions)."""
     from . import ppo_kernels as K
     mark = mark or _no_mark
     top = len(pol.net_arch) - 1
-    if obs16 is not None and rows is None and top_preact and acts2 is not None:
-        xw = x6_weights(pol, acts2[0].shape[1])
-        if xw is not None and x6_l1_enabled(pol) and obs.is_contiguous():
-            # the first two layers in one GEMM launch (h1 written on the way)
-            xw.refresh()
-            mark("split_weights")
-            gemm_x6_l1(pol, obs, obs16, xw, acts2[0], acts2[1], mark)
-            mark("gemm_x6_fwd")
-            return acts
     K.linear_tanh2(obs, pol.p("pi0.w"), pol.p("pi0.b"), acts["pi"][0],
                    pol.p("vf0.w"), pol.p("vf0.b"), acts["vf"][0], rows)
     mark("linear_tanh")

@@ -545,21 +545,6 @@ int dr_gemm_x6_split_weights(int64_t batch, const float *w, int transpose, void 
 int dr_gemm_x6(int64_t batch, int64_t m, const float *a, const void *img, float *c,
                void *stream);
 
-/* The MLP's first two layers in one launch for the training forward
-   (dr_gemm_x6 with the first layer fused into its prologue; ABI v12):
-   c[b] = h1[b] . W[b]^T for h1[b] = tanh(obs W0[b]^T + b0[b]), formed in the
-   kernel with dr_linear_tanh2's exact arithmetic, so h1 and c are bitwise
-   dr_linear_tanh2 followed by dr_gemm_x6 (obs_dim 15, hidden 256).
-   obs16 (m, 16) f32: the observation rows padded with a 0; w0p (batch, 256,
-   16): W0 row k then b0[k]; both formed by dr_gemm_x6_l1_pack (obs16 only
-   when obs is non-null).  h1 (batch, m, 256) receives the first layer's
-   activations when non-null.  m a positive multiple of 128, pointers 16-byte
-   aligned. */
-int dr_gemm_x6_l1_pack(int64_t batch, const float *w0, const float *b0, float *w0p, int64_t m,
-                       const float *obs, float *obs16, void *stream);
-int dr_gemm_x6_l1(int64_t batch, int64_t m, const float *obs16, const float *w0p,
-                  const void *img, float *c, float *h1, void *stream);
-
 /* The layer's weight gradient on the same arithmetic, split over `chunks`
    row chunks: ws[b][c] (256 x 256) = G[b][rows of chunk c]^T H[b][rows of
    chunk c] for G (batch, m, 256) = grad_z and H (batch, m, 256) = the layer

@@ -6,7 +6,7 @@ mkdir -p "$OUT"
 export TMPDIR=/tmp
 i=0
 for grp in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_WAIT_INST_LDS" \
-           "SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_LDS SQ_ACTIVE_INST_LDS SQ_INSTS_MFMA GRBM_GUI_ACTIVE GRBM_COUNT"; do
+           "SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_LDS SQ_ACTIVE_INST_LDS SQ_INSTS_MFMA SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_INSTS_SALU GRBM_GUI_ACTIVE GRBM_COUNT"; do
   i=$((i+1))
   timeout -s KILL 90 rocprofv3 --pmc $grp --output-format csv -d "$OUT/p$i" -o run \
       -- python3 "$PWD/scripts/micro/gemm_x6_bench.py" --reps 10 "$@" > "$OUT/p$i.log" 2>&1
@@ -19,7 +19,7 @@ out = sys.argv[1]
 acc = collections.defaultdict(list)
 for f in glob.glob(out + "/p*/run_counter_collection.csv"):
     for r in csv.DictReader(open(f)):
-        if re.search(r"gemm_x6_(cs_)?kernel", r["Kernel_Name"]):
+        if re.search(r"gemm_x6_(cs_|ws_)?kernel", r["Kernel_Name"]):
             acc[r["Counter_Name"]].append(float(r["Counter_Value"]))
 m = {k: sum(v) / len(v) for k, v in acc.items()}
 for k, v in sorted(m.items()):
@@ -27,7 +27,7 @@ for k, v in sorted(m.items()):
 res = {"workload": "scripts/micro/gemm_x6_bench.py --reps 10 (both nets, 65,536 rows, forward "
                    "and input-gradient forms; cold inputs), rocprofv3 --pmc, two passes "
                    "(scripts/micro/gemm_x6_pmc.sh); per-dispatch averages of dr_gemm_x6's kernel "
-                   "(gemm_x6_cs_kernel, the cooperative-split form, since round 3)",
+                   "(gemm_x6_ws_kernel, the weight-stationary form, since round 4)",
        "counters_per_dispatch": {k: round(v, 1) for k, v in sorted(m.items())}}
 w = m.get("SQ_WAVE_CYCLES")
 if w:

@@ -13,12 +13,6 @@ pytestmark = pytest.mark.gpu
 VEC = ("pos", "vel", "euler", "omega", "target")
 
 
-@pytest.fixture(autouse=True, params=["lane", "quad"])
-def step_kernel(request, monkeypatch):
-    monkeypatch.setenv("DRONERL_STEP_KERNEL", request.param)
-    return request.param
-
-
 def _close(a, b, tol=1e-5):
     a, b = np.asarray(a, np.float64), np.asarray(b, np.float64)
     err = np.abs(a - b) / np.maximum(np.abs(b), 1.0)

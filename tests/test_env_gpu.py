@@ -15,15 +15,6 @@ from oracle import cref
 
 pytestmark = pytest.mark.gpu
 
-
-@pytest.fixture(autouse=True, params=["quad", "lane"])
-def step_kernel(request, monkeypatch):
-    """Run every test with both step kernels: one lane per env (the default,
-    DRONERL_STEP_KERNEL=lane) and 4 lanes per env (DRONERL_STEP_KERNEL=quad,
-    kept for A/B), read at dr_create."""
-    monkeypatch.setenv("DRONERL_STEP_KERNEL", request.param)
-    return request.param
-
 TOL = 1e-5
 VEC = ("pos", "vel", "euler", "omega")
 

@@ -110,58 +110,23 @@ def test_gemm_x6_wgrad_as_accurate_as_fp32(m, chunks):
         _lib.DR_ERR_INVALID
 
 
-@pytest.mark.parametrize("m", [128, 4096, 65536])
-def test_first_layer_fused_forward_is_bitwise_the_two_launches(m):
-    """dr_gemm_x6_l1 (the first layer formed in the 256x256 GEMM's prologue)
-    against dr_linear_tanh2 + dr_gemm_x6: h1 and z bitwise equal (the fused
-    kernel repeats linear_tanh's fmaf order and tanh; the MFMA stream is the
-    same), so the rollout forward (two launches) and the training forward
-    (fused, DRONERL_X6_L1=1) see identical network outputs."""
-    from drone_rl_amd import ppo_kernels as K
-    from drone_rl_amd.policy import ActorCritic, gemm_x6, gemm_x6_l1, x6_weights
-    dev = torch.device("cuda", 0)
-    pol = ActorCritic(15, 4, (256, 256), dev, 0.0, 3)
-    with torch.no_grad():
-        pol.flat.add_(torch.randn_like(pol.flat) * 0.05)      # non-zero biases too
-    g = torch.Generator(device=dev).manual_seed(m)
-    obs = torch.randn(m, 15, generator=g, device=dev) * 2.0
-    obs[0, 3] = 0.0
-    xw = x6_weights(pol, m)
-    xw.refresh()
-    h_ref = torch.empty(2, m, 256, device=dev)
-    K.linear_tanh2(obs, pol.p("pi0.w"), pol.p("pi0.b"), h_ref[0], pol.p("vf0.w"),
-                   pol.p("vf0.b"), h_ref[1])
-    z_ref = torch.empty(2, m, 256, device=dev)
-    gemm_x6(h_ref, xw.fwd, z_ref)
-    obs16 = torch.full((m, 16), float("nan"), device=dev)
-    h = torch.full((2, m, 256), float("nan"), device=dev)
-    z = torch.full((2, m, 256), float("nan"), device=dev)
-    gemm_x6_l1(pol, obs, obs16, xw, h, z)
-    torch.cuda.synchronize()
-    assert torch.equal(obs16[:, :15], obs) and (obs16[:, 15] == 0).all()
-    assert torch.equal(h, h_ref)
-    assert torch.equal(z, z_ref)
-
-
 @pytest.mark.parametrize("m,chunks", [(128 * 3, 1), (65536, 64)])
-def test_x6_kernel_forms_are_bitwise_equal(m, chunks):
-    """Every launch form of the x6 GEMMs -- the defaults (cooperative-split
-    forward / input-gradient kernel, gemm_x6_wgrad_kernel), gemm_x6_kernel
-    with the cooperative-split weight gradient (DRONERL_X6_CS=0,
-    DRONERL_X6_WCS=1) and the ping-pong form (DRONERL_X6_PP=1) -- gives the
-    same bytes: the same splits and MFMA products in the same order.  The
-    form is chosen once per process, hence one subprocess per form."""
+def test_x6_outputs_are_the_same_bytes_in_two_processes(m, chunks):
+    """dr_gemm_x6 (both image forms) and dr_gemm_x6_wgrad on fixed seeded
+    inputs give the same bytes in two fresh processes (deterministic: fixed
+    block -> row and chunk assignment, no atomics; the weight-stationary
+    kernel was bitwise round 3's cooperative-split kernel while both
+    existed)."""
     import os
     import subprocess
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     digests = []
-    for extra in ({}, {"DRONERL_X6_CS": "0", "DRONERL_X6_WCS": "1"},
-                  {"DRONERL_X6_CS": "0", "DRONERL_X6_PP": "1"}):
-        env = dict(os.environ, PYTHONPATH=root, **extra)
+    for _ in range(2):
+        env = dict(os.environ, PYTHONPATH=root)
         r = subprocess.run([sys.executable, os.path.join(root, "tests", "x6_forms_worker.py"),
                             str(m), str(chunks)], env=env, capture_output=True, text=True,
                            timeout=100)
         assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
         digests.append([l for l in r.stdout.splitlines() if l.startswith("sha")][0])
-    assert digests[0] == digests[1] == digests[2], digests
+    assert digests[0] == digests[1], digests

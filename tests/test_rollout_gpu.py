@@ -201,7 +201,7 @@ def test_rollout_timed_same_outputs_and_packet_events():
 
 
 @pytest.mark.parametrize("ws,variant,n", [
-    ("1", "gym", 131072 + 320),     # warp-specialised form at two blocks per CU, ragged
+    ("1", "gym", 131072 + 320),     # split-physics form at two blocks per CU, ragged
     ("1", "moving", 70000),         # warp-specialised moving variant above one block per CU
     ("0", "gym", 65536),            # the one-role kernel where the default is warp-specialised
 ])

@@ -1,8 +1,7 @@
-"""Subprocess body of tests/test_gemm_x6_gpu.py::test_x6_kernel_forms_are_bitwise_equal:
-dr_gemm_x6 (both transposes) and dr_gemm_x6_wgrad on fixed seeded inputs; the
-kernel forms are chosen once per process (DRONERL_X6_CS / DRONERL_X6_WCS /
-DRONERL_X6_PP), so the test runs this once per form and compares the
-printed SHA-256 of the raw output bytes.  argv: m chunks."""
+"""Subprocess body of
+tests/test_gemm_x6_gpu.py::test_x6_outputs_are_the_same_bytes_in_two_processes:
+dr_gemm_x6 (both transposes) and dr_gemm_x6_wgrad on fixed seeded inputs;
+prints the SHA-256 of the raw output bytes.  argv: m chunks."""
 import hashlib
 import sys
 
