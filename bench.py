@@ -342,6 +342,42 @@ def time_headline(args, n_envs, rank, world, device, steps, warmup, kmax):
     return elapsed, gpu_ms, launches, ep, packet_ms, graphed
 
 
+def time_host_floor(device, reps=60):
+    """The host side of one launch + synchronize on the headline's own path
+    (a direct dr_rollout C-ABI call with prebuilt arguments, then
+    torch.cuda.synchronize), measured on a launch whose kernel does almost no
+    work: 64 envs, one step.  Returns median wall and median dispatch-packet
+    duration (dr_rollout_timed) in us; their difference is the launch +
+    completion cost that any single timed launch pays."""
+    import torch
+
+    from drone_rl_amd import DroneBatch, random_actions
+    b = DroneBatch(64, "gym", dtype=torch.float64, device=device, seed=5, auto_reset=True)
+    b.reset()
+    acts = random_actions(64, seed=1, step=0).reshape(1, 64, 4).to(device)
+    obs = torch.empty(1, 64, b.obs_dim, device=device)
+    rew = torch.empty(1, 64, device=device)
+    done = torch.empty(1, 64, dtype=torch.uint8, device=device)
+    stream = torch.cuda.current_stream(device)
+    c = (b.handle, 1, acts.data_ptr(), obs.data_ptr(), rew.data_ptr(), done.data_ptr(),
+         stream.cuda_stream)
+    fn = b.L.dr_rollout
+    walls, pkts = [], []
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    for r in range(reps):
+        torch.cuda.synchronize(device)
+        t0 = time.perf_counter()
+        fn(*c)
+        torch.cuda.synchronize(device)
+        walls.append((time.perf_counter() - t0) * 1e6)
+        b.L.dr_rollout_timed(*c, e0.cuda_event, e1.cuda_event)
+        torch.cuda.synchronize(device)
+        pkts.append(e0.elapsed_time(e1) * 1e3)
+    b.close()
+    walls, pkts = sorted(walls[5:]), sorted(pkts[5:])
+    return walls[len(walls) // 2], pkts[len(pkts) // 2]
+
+
 def time_rollout(args, n_envs, device, k, reps, gen, variant="gym", state_dtype=None):
     """The K-step rollout kernel (dr_rollout; dr_rollout_random when gen):
     `reps` launches of k steps each over the same 65,536 envs, captured in
@@ -727,6 +763,15 @@ def main():
         elapsed, gpu_ms, ep = el_s, gm_s, ep_s
         roof = single["roofline"]
         graphed = not args.no_graph
+    if args.headline == "rollout" and world == 1:
+        # what one direct launch + synchronize costs on the host side (the
+        # driver's --steps 20 is one launch): a near-empty launch on the same
+        # path, wall against its dispatch packet
+        fw, fp = time_host_floor(device)
+        roof["host_floor_us"] = {"wall": round(fw, 2), "kernel_packet": round(fp, 2),
+                                 "launch_and_sync": round(fw - fp, 2),
+                                 "probe": "dr_rollout, 64 envs, 1 step, direct C-ABI call + "
+                                          "torch.cuda.synchronize, median of 55"}
     value = N * world * K / elapsed
     out = {
         "metric": "env-steps/s (whole node) + PPO updates/s, 65 536 envs/GPU, 2x256 MLP",

@@ -95,3 +95,35 @@ def test_crashes_are_not_bootstrapped():
     assert np.array_equal(on["rew"], off["rew"])
     for r in (off, on):
         r["tr"].close()
+
+
+def test_timeout_bootstrap_rollout_graph_is_bitwise_eager():
+    """The default rollout path captures the T-step loop -- the extra value
+    forward of the terminal obs and the masked reward add included -- into a
+    hipGraph (no trajectory tap here).  Three collect_rollouts() calls on the
+    graph path (eager warm-up, capture + replay, replay) give bitwise the
+    rewards, values and dones of the same three calls run eagerly."""
+    from drone_rl_amd.ppo import PPOConfig, PPOTrainer
+    res = []
+    for graph in (True, False):
+        cfg = PPOConfig(num_envs=1024, n_steps=256, batch_size=8192, n_epochs=1, seed=4,
+                        bootstrap_timeouts=True)
+        tr = PPOTrainer(cfg)
+        tr.rollout_graph = graph
+        with torch.no_grad():
+            tr.policy.p("action.w").zero_()
+            tr.policy.p("action.b").fill_(HOVER)
+            tr.policy.p("log_std").fill_(-30.0)
+        out = []
+        for _ in range(3):
+            tr.collect_rollouts()
+            torch.cuda.synchronize()
+            out.append((tr.rewards.clone(), tr.values.clone(), tr.dones.clone()))
+        if graph:
+            assert tr._rgraph is not None, "the rollout graph was not captured"
+        res.append(out)
+    n_trunc = 0
+    for (rg, vg, dg), (re, ve, de) in zip(*res):
+        assert torch.equal(rg, re) and torch.equal(vg, ve) and torch.equal(dg, de)
+        n_trunc += int(dg.sum())
+    assert n_trunc > 0          # the hover policy reaches the step limit
