@@ -364,6 +364,8 @@ def time_host_floor(device, reps=60):
     fn = b.L.dr_rollout
     walls, pkts = [], []
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    for e in (e0, e1):
+        e.record(stream)        # creates the events (torch creates them lazily)
     for r in range(reps):
         torch.cuda.synchronize(device)
         t0 = time.perf_counter()
@@ -767,11 +769,15 @@ def main():
         # what one direct launch + synchronize costs on the host side (the
         # driver's --steps 20 is one launch): a near-empty launch on the same
         # path, wall against its dispatch packet
-        fw, fp = time_host_floor(device)
-        roof["host_floor_us"] = {"wall": round(fw, 2), "kernel_packet": round(fp, 2),
-                                 "launch_and_sync": round(fw - fp, 2),
-                                 "probe": "dr_rollout, 64 envs, 1 step, direct C-ABI call + "
-                                          "torch.cuda.synchronize, median of 55"}
+        # (a failure here is reported in the line, not fatal to it)
+        try:
+            fw, fp = time_host_floor(device)
+            roof["host_floor_us"] = {"wall": round(fw, 2), "kernel_packet": round(fp, 2),
+                                     "launch_and_sync": round(fw - fp, 2),
+                                     "probe": "dr_rollout, 64 envs, 1 step, direct C-ABI call "
+                                              "+ torch.cuda.synchronize, median of 55"}
+        except Exception as ex:  # noqa: BLE001
+            roof["host_floor_us"] = {"error": repr(ex)[:300]}
     value = N * world * K / elapsed
     out = {
         "metric": "env-steps/s (whole node) + PPO updates/s, 65 536 envs/GPU, 2x256 MLP",

@@ -114,18 +114,12 @@ __global__ __launch_bounds__(256) void split_weights_kernel(const float *__restr
     *reinterpret_cast<u32x4_t *>(base + 2 * W_FRAG) = l;
 }
 
-// global_load_lds_dwordx4 by inline asm: lane l's 16 bytes land at LDS
-// byte lds_base + 16 l.  Issued by hand because hipcc's waitcnt pass drains
-// every pending LDS DMA (vmcnt(0)) before any ds_read it cannot prove
-// disjoint from it -- once per stage here; the waits are counted by hand.
-__device__ inline void glds16(const void *gptr, uint32_t lds_base) {
-    asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off"
-                 ::"v"(gptr), "s"(lds_base)
-                 : "memory", "m0");
-}
-// The same with the global address split into a wave-uniform 64-bit base
-// (SGPRs) and a 32-bit per-lane byte offset (the saddr form): a loop of
-// these keeps one offset VGPR instead of a 64-bit address per instruction.
+// global_load_lds_dwordx4 by inline asm (the saddr form: a wave-uniform
+// 64-bit base in SGPRs and a 32-bit per-lane byte offset, so a loop of these
+// keeps one offset VGPR): lane l's 16 bytes land at LDS byte lds_base + 16 l.
+// Issued by hand because hipcc's waitcnt pass drains every pending LDS DMA
+// (vmcnt(0)) before any ds_read it cannot prove disjoint from it; the waits
+// are counted by hand.
 __device__ inline void glds16_s(const void *sbase, uint32_t voff, uint32_t lds_base) {
     asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, %1"
                  ::"v"(voff), "s"(sbase), "s"(lds_base)
@@ -356,8 +350,11 @@ __global__ __launch_bounds__(WS_THREADS, 1) void gemm_x6_ws_kernel(
     // per-lane offset plus an SGPR offset per register: no VALU per store)
     const int st_off = (4 * fh * XN + fr) * 4;
     auto store_one = [&](int k, int t, int r) {
+        // k = -1 (tile 1 of no row step, in row step 0): a 0-byte range, the
+        // stores are dropped
         const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-            Cb + (int64_t)(j0 + k * per) * WS_RS * XN, 0, WS_RS * XN * 4, 0x00020000);
+            Cb + (int64_t)(j0 + k * per) * WS_RS * XN, 0, k < 0 ? 0 : WS_RS * XN * 4,
+            0x00020000);
         if (DR_WS_ABL == 3 && acc_h[t][r] != 12345.f) return;
         __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(acc_h[t][r]), rs, st_off,
                                               ((8 * (r >> 2) + (r & 3)) * XN + 64 * w + 32 * t) * 4,
@@ -383,7 +380,8 @@ __global__ __launch_bounds__(WS_THREADS, 1) void gemm_x6_ws_kernel(
         split_write(0, q >> 1, q & 1, v);
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");       // staging slot 0 read
-    if (R > 2) issue_rows(2);
+    issue_rows(R > 2 ? 2 : R - 1);                           // clamped: never split
+    asm volatile("s_waitcnt vmcnt(8)" ::: "memory");         // step 1's staging
     asm volatile("s_barrier" ::: "memory");                  // planes of step 0
     WS_STAMP(23, 1);
     AFrag fb[WS_NF];
@@ -396,36 +394,28 @@ __global__ __launch_bounds__(WS_THREADS, 1) void gemm_x6_ws_kernel(
     // steps 1, 5, 9, 13 of each phase (read one step before), the DMA of step
     // k + 3 two pieces at a time behind the split reads of its slot; then
     // lgkmcnt(0) + barrier.
-    // (one body per (split?, phase-0 stores?) pair, so that the loop has no
-    // branch that could make the compiler copy an accumulator between asm
-    // MFMA groups: a compiler VALU read of an MFMA result right after the asm
-    // would miss its wait states)
+    // The body has no data-dependent branch (measured 99-100 vs 105-106 us
+    // with branches around the first and last steps' work, bitwise the same
+    // C): row step 0's phase-0 stores go through a 0-byte buffer range (no
+    // row step -1), the last steps split their successor's staging into the
+    // unused plane buffer, and the staging DMA past the last step re-loads it
+    // (clamped rows).  Branches also risk the compiler copying an accumulator
+    // between asm MFMA groups, a VALU read of an MFMA result inside its wait
+    // states (tests/test_x6_asm_hazards.py).
     auto row_step = [&](int k) {
-        const bool nxt = k + 1 < R;
-        const bool st0 = k > 0;
         WS_STAMP(k, 0);
-        if (nxt) {
-            // the staging of step k + 1 (issued in step k - 2, or the
-            // prologue): at least 8 (k = 0, with step 2's rows), 16 (k = 1)
-            // or 32 (k >= 2) vector-memory ops are younger
-            __builtin_amdgcn_sched_barrier(0);
-            if (k >= 2)
-                asm volatile("s_waitcnt vmcnt(32)" ::: "memory");
-            else if (k == 1)
-                asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
-            else if (R > 2)
-                asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-            else
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        }
+        // the staging of step k + 1 (issued in step k - 2): every vector
+        // memory op of step k - 1 (32 stores + 8 DMA pieces) is younger; for
+        // k = 0 the prologue waited
+        __builtin_amdgcn_sched_barrier(0);
+        asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
         WS_STAMP(k, 1);
 #pragma unroll
         for (int t = 0; t < 2; ++t) {
             if (t == 1) WS_STAMP(k, 2);
             // the other tile's finished outputs (t = 0: tile 1 of step k - 1)
-            const bool st = t == 1 || st0;
             const int ko = t == 1 ? k : k - 1;
-            if (st) finish_tile(1 - t);
+            finish_tile(1 - t);
             float4 v;
             uint32_t sh0, sm0, sl0, sh1, sm1, sl1;
 #pragma unroll
@@ -440,12 +430,12 @@ __global__ __launch_bounds__(WS_THREADS, 1) void gemm_x6_ws_kernel(
                 // half-unit q: read before k16 step 4 (q - 4 t) + 1; its two
                 // pairs split inside the MFMA groups of steps + 2 and + 3;
                 // written (3 x 8 B) after the second
-                const bool sp = nxt && DR_WS_ABL != 1;
+                const bool sp = DR_WS_ABL != 1;
                 if (sp && (s & 3) == 0) split_read(k + 1, q >> 1, q & 1, v);
                 const AFrag &x = fb[g % WS_NF];
                 mfma_x6_group(s == 0, acc_h[t], acc_l[t], x[0], x[1], x[2], Wa[t][s][0],
                               Wa[t][s][1], Wv[t][s]);
-                if (st && DR_WS_ABL != 3) store_one(ko, 1 - t, s);
+                if (DR_WS_ABL != 3) store_one(ko, 1 - t, s);
                 if (sp && (s & 3) == 1) {
                     // the half-unit's split (its read, one k16 step ago, has
                     // landed behind the MFMAs)
@@ -460,13 +450,15 @@ __global__ __launch_bounds__(WS_THREADS, 1) void gemm_x6_ws_kernel(
                 }
                 if (sp && (s & 3) == 1) {
                     split_store(k + 1, q >> 1, q & 1, sh0, sh1, sm0, sm1, sl0, sl1);
-                    if ((q & 1) && k + 3 < R && DR_WS_ABL != 2) {
+                    if ((q & 1) && DR_WS_ABL != 2) {
                         // unit q >> 1's two staging pieces were read (the
                         // split above consumed the data, and asm volatile
                         // keeps the DMA behind it): refill them with step k + 3
+                        // (clamped to the last step: such rows are never split)
                         const int u = q >> 1;
+                        const int k3 = k + 3 >= R ? R - 1 : k + 3;
                         const float *r0 =
-                            Ab + ((int64_t)(j0 + (k + 3) * per) * WS_RS + 8 * w) * XK;
+                            Ab + ((int64_t)(j0 + k3 * per) * WS_RS + 8 * w) * XK;
                         uint8_t *dst = sh + WS_LDS_F + ((k + 3) & 1) * WS_FSLOT + w * 8 * 1024;
                         glds16_s(r0 + 32 * (2 * u), voff_f, lds_addr(dst + (2 * u) * 1024));
                         glds16_s(r0 + 32 * (2 * u + 1), voff_f,
@@ -485,10 +477,8 @@ __global__ __launch_bounds__(WS_THREADS, 1) void gemm_x6_ws_kernel(
         else
             asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
         WS_STAMP(k, 5);
-        if (nxt) {
-            read_frag(k + 1, 0, fb[0]);
-            if (WS_NF == 3) read_frag(k + 1, 1, fb[1]);
-        }
+        read_frag(k + 1, 0, fb[0]);          // after the last step: unused
+        if (WS_NF == 3) read_frag(k + 1, 1, fb[1]);
     };
     for (int k = 0; k < R; ++k) row_step(k);
     // tile 1 of the last row step
@@ -497,35 +487,57 @@ __global__ __launch_bounds__(WS_THREADS, 1) void gemm_x6_ws_kernel(
 #pragma unroll
         for (int r = 0; r < 16; ++r) store_one(R - 1, 1, r);
     }
+    // the clamped staging DMA of the last steps lands before the block's LDS
+    // is released
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
 // ---------------------------------------------------------------------------
 // Weight gradient of the same layer, dW[b] = G[b]^T H[b] (G = grad_z, H = the
 // layer input, both (m, 256) f32 row-major), split over C row chunks: block
 // (b, n-half, chunk) writes the 128 x 256 partial ws[b][chunk][n][k] of its
-// (m / C)-row chunk; the chunk sum is left to the caller (the
-// trainer's deferred finish sums C = 64 chunks in a fixed order).  Both
-// operands are reduced over rows, so a fragment needs 8 consecutive ROWS of
-// one column: each lane gathers them with ds_read_b32 from the f32 stage
-// images (rows of 128 / 256 floats, consecutive lanes on consecutive columns:
-// conflict-free) and splits them into the three bf16 planes in registers.
-// Stages of 32 rows arrive by global_load_lds two stages ahead (three
-// buffers); 8 waves as 2 (n) x 4 (k) of 64 x 64, the same split hi/lo
-// accumulation as gemm_x6_kernel.
-constexpr int TN_BM = 32;                          // rows per stage
-constexpr int TN_G = TN_BM * 128 * 4;              // 16 KB: G stage (128 n)
-constexpr int TN_H = TN_BM * 256 * 4;              // 32 KB: H stage (256 k)
-constexpr int TN_STAGE = TN_G + TN_H;              // 48 KB
-constexpr int TN_LDS = 3 * TN_STAGE;               // 144 KB
-constexpr int TN_NG = TN_G / 1024 / XWAVES;        // 2 glds per wave per stage
-constexpr int TN_NH = TN_H / 1024 / XWAVES;        // 4
-#define TN_VM_YOUNG 6                              // TN_NG + TN_NH
-#define TN_VM_PRO 12
+// (m / C)-row chunk; the chunk sum is left to the caller (the trainer's
+// deferred finish sums C = 64 chunks in a fixed order).  8 waves as 2 (n) x
+// 4 (k) of 64 x 64 outputs, the same split hi/lo accumulation as the forward.
+//
+// Both operands are reduced over rows, so an MFMA fragment is 8 consecutive
+// ROWS of one column.  Round 3's kernel had each lane gather its fragments
+// with ds_read_b32 from f32 stage images and split them itself: a G column
+// was split by each of the 4 k waves that read it and an H column by both n
+// waves, 64 elements per lane and stage (~350 VALU + 64 ds_read_b32 per wave
+// against 48 MFMAs), and the SIMD's issue, not the matrix pipe, bounded it.
+// Here each 32-row stage is split ONCE (round 4): every thread loads 6 float4
+// of the stage (2 of G's 32 x 128 half, 4 of H's 32 x 256) into registers
+// one stage ahead, splits them and writes the three bf16 planes ROW-major
+// into LDS; the fragments come back column-major through gfx950's
+// transposing read ds_read_b64_tr_b16 (two per fragment).  Per wave and
+// stage: 24 split elements (~130 VALU), 18 ds_write_b64, 48 transposed
+// reads, 48 MFMAs, one barrier.  Bitwise round 3's partials (same splits,
+// products and per-output order); 110-111 vs 119-124 us for both nets at
+// 65,536 rows, 64 chunks (scripts/micro/wgrad_ab.py, same box).
+//
+constexpr int TW_BM = 32;                          // rows per stage
+constexpr int TW_PLANE_ROW = (128 + 256) * 2;      // 768 B: one plane of one row
+constexpr int TW_ROW = 3 * TW_PLANE_ROW + 64;      // 2,368 B
+constexpr int TW_STAGE = TW_BM * TW_ROW;           // 75,776 B
+constexpr int TW_LDS = 2 * TW_STAGE;               // 151,552 B
+
+typedef short i16x4_t __attribute__((ext_vector_type(4)));
+typedef float f32x4_t __attribute__((ext_vector_type(4)));
+
+__device__ inline bf16x8_t tr_frag(const uint8_t *p) {
+    typedef __attribute__((address_space(3))) i16x4_t lds_i16x4;
+    const i16x4_t a = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+        (lds_i16x4 *)(uintptr_t)lds_addr(p));
+    const i16x4_t c = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+        (lds_i16x4 *)(uintptr_t)lds_addr(p + 4 * TW_ROW));
+    return __builtin_bit_cast(bf16x8_t, __builtin_shufflevector(a, c, 0, 1, 2, 3, 4, 5, 6, 7));
+}
 
 __global__ __launch_bounds__(XTHREADS) void gemm_x6_wgrad_kernel(
     const float *__restrict__ Gm, const float *__restrict__ Hm, float *__restrict__ ws,
     int64_t m, int chunks) {
-    __shared__ __attribute__((aligned(16))) uint8_t sh[TN_LDS];
+    __shared__ __attribute__((aligned(16))) uint8_t sh[TW_LDS];
     const int tid = threadIdx.x, lane = tid & 63;
     const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int wn = wid >> 2, wk = wid & 3;
@@ -533,53 +545,57 @@ __global__ __launch_bounds__(XTHREADS) void gemm_x6_wgrad_kernel(
     const int nh = (int)((blockIdx.x / chunks) & 1);
     const int b = (int)(blockIdx.x / chunks / 2);
     const int64_t rows = m / chunks;
-    const int G_ = (int)(rows / TN_BM);
+    const int G_ = (int)(rows / TW_BM);
     const float *Gb = Gm + ((int64_t)b * m + (int64_t)chunk * rows) * 256 + nh * 128;
     const float *Hb = Hm + ((int64_t)b * m + (int64_t)chunk * rows) * 256;
 
-    // stage g -> buffer g % 3; a G wave-instruction moves 2 rows x 512 B, an H
-    // one 1 row x 1 KB (lane-linear, no swizzle: the b32 reads below are
-    // conflict-free on plain rows)
-    auto issue = [&](int g) {
-        uint8_t *dst = sh + (g % 3) * TN_STAGE;
-        const int64_t r0 = (int64_t)g * TN_BM;
+    // thread tid's six float4 of a stage: G item i (row (tid + 512 i) / 32,
+    // columns 4 ((tid + 512 i) % 32) ..), H item i (row (tid + 512 i) / 64)
+    int ld_src[6], ld_dst[6];
 #pragma unroll
-        for (int i = 0; i < TN_NG; ++i) {
-            const int ins = wid + XWAVES * i;                 // rows 2 ins, 2 ins + 1
-            const int row = 2 * ins + (lane >> 5);
-            glds16(Gb + (r0 + row) * 256 + (lane & 31) * 4, lds_addr(dst + ins * 1024));
-        }
+    for (int i = 0; i < 6; ++i) {
+        const int q = tid + 512 * (i < 2 ? i : i - 2);
+        const int r = i < 2 ? q >> 5 : q >> 6;
+        const int c = i < 2 ? (q & 31) * 4 : (q & 63) * 4;
+        ld_src[i] = (i < 2 ? r * 256 + c : r * 256 + c);
+        ld_dst[i] = r * TW_ROW + (i < 2 ? c : 128 + c) * 2;
+    }
+    f32x4_t ld[6];
+    auto load = [&](int g) {
+        const int64_t r0 = (int64_t)g * TW_BM * 256;
 #pragma unroll
-        for (int i = 0; i < TN_NH; ++i) {
-            const int ins = wid + XWAVES * i;                 // row ins
-            glds16(Hb + (r0 + ins) * 256 + lane * 4, lds_addr(dst + TN_G + ins * 1024));
+        for (int i = 0; i < 6; ++i)
+            ld[i] = *reinterpret_cast<const f32x4_t *>((i < 2 ? Gb : Hb) + r0 + ld_src[i]);
+    };
+    auto split_store = [&](int buf) {
+        uint8_t *S = sh + buf * TW_STAGE;
+#pragma unroll
+        for (int i = 0; i < 6; ++i) {
+            const f32x4_t x = ld[i];
+            uint32_t h[2], mm[2], l[2];
+#pragma unroll
+            for (int q = 0; q < 2; ++q) {
+                const float a = x[2 * q], c = x[2 * q + 1];
+                const uint32_t ph = pk_bf16(a, c);
+                const float ra = a - lo_f(ph), rc = c - hi_f(ph);
+                const uint32_t pm = pk_bf16(ra, rc);
+                h[q] = ph;
+                mm[q] = pm;
+                l[q] = pk_bf16(ra - lo_f(pm), rc - hi_f(pm));
+            }
+            uint8_t *d = S + ld_dst[i];
+            *reinterpret_cast<uint2 *>(d) = make_uint2(h[0], h[1]);
+            *reinterpret_cast<uint2 *>(d + TW_PLANE_ROW) = make_uint2(mm[0], mm[1]);
+            *reinterpret_cast<uint2 *>(d + 2 * TW_PLANE_ROW) = make_uint2(l[0], l[1]);
         }
     };
 
-    const int fr = lane & 31, fh = lane >> 5;
-    // fragment of k16 step s: rows 16 s + 8 fh + j (j = 0..7) of one column
-    int g_off[2][2], h_off[2][2];
-#pragma unroll
-    for (int s2 = 0; s2 < 2; ++s2)
-#pragma unroll
-        for (int i = 0; i < 2; ++i) {
-            g_off[i][s2] = (16 * s2 + 8 * fh) * 512 + (wn * 64 + i * 32 + fr) * 4;
-            h_off[i][s2] = TN_G + (16 * s2 + 8 * fh) * 1024 + (wk * 64 + i * 32 + fr) * 4;
-        }
-    struct RawFrag {
-        float g[2][8];
-        float h[2][8];
-    };
-    auto read_frag = [&](int g, int s2, RawFrag &f) {
-        const uint8_t *S = sh + (g % 3) * TN_STAGE;
-#pragma unroll
-        for (int i = 0; i < 2; ++i)
-#pragma unroll
-            for (int j = 0; j < 8; ++j) {
-                f.g[i][j] = *reinterpret_cast<const float *>(S + g_off[i][s2] + j * 512);
-                f.h[i][j] = *reinterpret_cast<const float *>(S + h_off[i][s2] + j * 1024);
-            }
-    };
+    // transposed-read lane address: the 16-lane group gq reads rows
+    // 8 (gq >> 1) + (0..3) (+ 4 for the second read), columns 16 (gq & 1) + 4 p
+    const int li = lane & 15, gq = lane >> 4;
+    const int fbase = (8 * (gq >> 1) + (li >> 2)) * TW_ROW + (16 * (gq & 1) + 4 * (li & 3)) * 2;
+    const int gcol = (wn * 64) * 2, hcol = (128 + wk * 64) * 2;
+
     f32x16_t acc_h[2][2], acc_l[2][2];                    // [n tile i][k tile j]
 #pragma unroll
     for (int i = 0; i < 2; ++i)
@@ -588,62 +604,51 @@ __global__ __launch_bounds__(XTHREADS) void gemm_x6_wgrad_kernel(
             acc_h[i][j] = (f32x16_t){};
             acc_l[i][j] = (f32x16_t){};
         }
-    auto mfma_step = [&](const RawFrag &f) {
-        bf16x8_t fg[2][3], fhp[2][3];
-#pragma unroll
-        for (int i = 0; i < 2; ++i) {
-            u32x4_t a0, a1, a2, c0, c1, c2;
-            split8(f.g[i], a0, a1, a2);
-            split8(f.h[i], c0, c1, c2);
-            fg[i][0] = __builtin_bit_cast(bf16x8_t, a0);
-            fg[i][1] = __builtin_bit_cast(bf16x8_t, a1);
-            fg[i][2] = __builtin_bit_cast(bf16x8_t, a2);
-            fhp[i][0] = __builtin_bit_cast(bf16x8_t, c0);
-            fhp[i][1] = __builtin_bit_cast(bf16x8_t, c1);
-            fhp[i][2] = __builtin_bit_cast(bf16x8_t, c2);
-        }
-#pragma unroll
-        for (int i = 0; i < 2; ++i)
-#pragma unroll
-            for (int j = 0; j < 2; ++j) {
-                const bf16x8_t *a = fg[i], *c = fhp[j];
-                acc_h[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], c[0], acc_h[i][j],
-                                                                      0, 0, 0);
-                f32x16_t t = acc_l[i][j];
-                t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], c[1], t, 0, 0, 0);
-                t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], c[0], t, 0, 0, 0);
-                t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], c[2], t, 0, 0, 0);
-                t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[2], c[0], t, 0, 0, 0);
-                t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], c[1], t, 0, 0, 0);
-                acc_l[i][j] = t;
-            }
-    };
 
-    issue(0);
-    issue(1);
-    issue(2);                                      // G_ >= 3 (checked by the host)
-    asm volatile("s_waitcnt vmcnt(" X6_S(TN_VM_PRO) ")\n\ts_barrier" ::: "memory");
-    RawFrag f0, f1;
-    read_frag(0, 0, f0);
+    load(0);
+    split_store(0);
+    load(G_ > 1 ? 1 : 0);
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
     for (int g = 0; g < G_; ++g) {
-        read_frag(g, 1, f1);
-        mfma_step(f0);
-        // stage g + 1 has landed (the loads of g + 2 may be in flight), and
-        // every wave's reads of stage g are done
-        __builtin_amdgcn_sched_barrier(0);
-        if (g + 2 < G_)
-            asm volatile("s_waitcnt vmcnt(" X6_S(TN_VM_YOUNG) ") lgkmcnt(0)\n\ts_barrier" ::: "memory");
-        else
-            asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
-        if (g + 3 < G_) issue(g + 3);
-        // unconditional (the last iteration re-reads stage g; unused): a read
-        // on one path only would make the waitcnt pass merge the two paths'
-        // LDS counts into an lgkmcnt(0) before the next split
-        read_frag(g + 1 < G_ ? g + 1 : g, 0, f0);
-        __builtin_amdgcn_sched_barrier(0);
-        mfma_step(f1);
+        const uint8_t *S = sh + (g & 1) * TW_STAGE + fbase;
+        bf16x8_t fg[2][2][3], fhp[2][2][3];               // [k16 step][tile][plane]
+#pragma unroll
+        for (int s = 0; s < 2; ++s)
+#pragma unroll
+            for (int i = 0; i < 2; ++i)
+#pragma unroll
+                for (int p = 0; p < 3; ++p) {
+                    const uint8_t *q = S + 16 * s * TW_ROW + p * TW_PLANE_ROW;
+                    fg[s][i][p] = tr_frag(q + gcol + 64 * i);
+                    fhp[s][i][p] = tr_frag(q + hcol + 64 * i);
+                }
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+#pragma unroll
+            for (int i = 0; i < 2; ++i)
+#pragma unroll
+                for (int j = 0; j < 2; ++j) {
+                    const bf16x8_t *a = fg[s][i], *c = fhp[s][j];
+                    acc_h[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], c[0], acc_h[i][j],
+                                                                          0, 0, 0);
+                    f32x16_t t = acc_l[i][j];
+                    t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], c[1], t, 0, 0, 0);
+                    t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], c[0], t, 0, 0, 0);
+                    t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], c[2], t, 0, 0, 0);
+                    t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[2], c[0], t, 0, 0, 0);
+                    t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], c[1], t, 0, 0, 0);
+                    acc_l[i][j] = t;
+                }
+            // the split of stage g + 1 (loaded one stage ago) into the other
+            // buffer, beside the MFMAs (the last iteration re-splits the
+            // last stage into the unused buffer: no branch in the loop)
+            if (s == 0) split_store((g + 1) & 1);
+        }
+        load(g + 2 < G_ ? g + 2 : G_ - 1);
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
     }
     // D[n][k]: column k = fr, row n = (r & 3) + 8 (r >> 2) + 4 fh
+    const int fr = lane & 31, fh = lane >> 5;
     float *out = ws + ((int64_t)b * chunks + chunk) * 256 * 256 + (int64_t)(nh * 128) * 256;
 #pragma unroll
     for (int i = 0; i < 2; ++i)
@@ -714,10 +719,10 @@ int dr_gemm_x6(int64_t batch, int64_t m, const float *a, const void *img, float 
 int dr_gemm_x6_wgrad(int64_t batch, int64_t m, int64_t chunks, const float *g, const float *h,
                      float *ws, void *stream) {
     if (batch < 1 || batch > 2 || chunks < 1 || m < 1 || m % chunks ||
-        (m / chunks) % TN_BM || m / chunks < 3 * TN_BM || m > (int64_t(1) << 26) || !g || !h ||
+        (m / chunks) % TW_BM || m > (int64_t(1) << 26) || !g || !h ||
         !ws || (((uintptr_t)g) & 15) || (((uintptr_t)h) & 15) || (((uintptr_t)ws) & 15))
         return fail_g(DR_ERR_INVALID,
-                      "dr_gemm_x6_wgrad: bad arguments (m / chunks a multiple of 32, >= 96; "
+                      "dr_gemm_x6_wgrad: bad arguments (m / chunks a positive multiple of 32; "
                       "pointers 16-byte aligned)");
     hipLaunchKernelGGL(gemm_x6_wgrad_kernel, dim3((unsigned)(batch * 2 * chunks)),
                        dim3(XTHREADS), 0, static_cast<hipStream_t>(stream), g, h, ws, m,

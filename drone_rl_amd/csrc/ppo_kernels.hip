@@ -509,6 +509,13 @@ __global__ __launch_bounds__(kBlock) void gather_minibatch_kernel(
     if (b < nb_obs) {
         const int64_t e = (int64_t)b * kBlock + threadIdx.x;
         if (e >= m * obs_dim) return;
+        if (m * obs_dim <= (int64_t)UINT32_MAX) {
+            // 32-bit element index: the row division is a few VALU, not the
+            // ~40 of a 64-bit one
+            const uint32_t e32 = (uint32_t)e, k = e32 / (uint32_t)obs_dim;
+            obs_out[e] = obs[(int64_t)idx[k] * obs_dim + (e32 - k * (uint32_t)obs_dim)];
+            return;
+        }
         const int64_t k = e / obs_dim, j = e - k * obs_dim;
         obs_out[e] = obs[(int64_t)idx[k] * obs_dim + j];
         return;

@@ -337,7 +337,7 @@ class FusedTrainStep:
         ws = self._ws2[:2 * C * N * Kd].view(2 * C, N, Kd)
         rows = M // C
         if (x6_weights(self.pol, M) is not None and N == 256 and Kd == 256 and rows % 32 == 0
-                and rows >= 96):
+                and rows >= 32):
             from . import _lib
             _lib.check(_lib.lib().dr_gemm_x6_wgrad(
                 2, M, C, gz.data_ptr(), x.data_ptr(), ws.data_ptr(),

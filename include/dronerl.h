@@ -549,7 +549,7 @@ int dr_gemm_x6(int64_t batch, int64_t m, const float *a, const void *img, float 
    row chunks: ws[b][c] (256 x 256) = G[b][rows of chunk c]^T H[b][rows of
    chunk c] for G (batch, m, 256) = grad_z and H (batch, m, 256) = the layer
    input (torch's split-K bmm layout; the caller sums the chunks).
-   m / chunks a multiple of 32 and >= 96; pointers 16-byte aligned.
+   m / chunks a positive multiple of 32; pointers 16-byte aligned.
    Deterministic.  (ABI v10.) */
 int dr_gemm_x6_wgrad(int64_t batch, int64_t m, int64_t chunks, const float *g, const float *h,
                      float *ws, void *stream);

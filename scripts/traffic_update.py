@@ -16,11 +16,11 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 N = 65536
 
 
-def avg(path, counter):
+def avg(path, counter, kernel="env_rollout"):
     vals = []
     for f in glob.glob(os.path.join(path, "**", "*counter_collection.csv"), recursive=True):
         for r in csv.DictReader(open(f)):
-            if "env_rollout" in r["Kernel_Name"] and r["Counter_Name"] == counter:
+            if kernel in r["Kernel_Name"] and r["Counter_Name"] == counter:
                 vals.append(float(r["Counter_Value"]))
     if not vals:
         raise SystemExit(f"no {counter} rows under {path}")
@@ -42,6 +42,21 @@ def main():
             "source": "scripts/rollout_traffic.sh (rocprofv3 --pmc FETCH_SIZE, WRITE_SIZE "
                       "passes; FETCH_SIZE x2 gfx950 correction + WRITE_SIZE, KiB -> B)"}
         print(k, json.dumps(tj[f"rollout_f64_{N}_k{k}"]))
+    # the companion: 4,194,304 envs, K = 32, the one-role kernel (the headline
+    # at 65,536 envs runs the warp-specialised forms, other kernel names)
+    n4, k = 1 << 22, 32
+    if os.path.isdir(os.path.join(out, "c4m_FETCH_SIZE")):
+        f, nf = avg(os.path.join(out, "c4m_FETCH_SIZE"), "FETCH_SIZE", "env_rollout_kernel")
+        w, nw = avg(os.path.join(out, "c4m_WRITE_SIZE"), "WRITE_SIZE", "env_rollout_kernel")
+        rd, wr = f * 2048, w * 1024
+        tj[f"rollout_f64_{n4}_k{k}"] = {
+            "algorithmic_bytes_per_launch": n4 * (k * 81 + 224),
+            "hbm_bytes_per_launch": round(rd + wr), "read_bytes": round(rd),
+            "write_bytes": round(wr), "dispatches": [nf, nw],
+            "source": "scripts/rollout_traffic.sh companion passes (bench.py's "
+                      "companion_rollout; rocprofv3 --pmc FETCH_SIZE, WRITE_SIZE; FETCH_SIZE "
+                      "x2 gfx950 correction + WRITE_SIZE, KiB -> B)"}
+        print("companion", json.dumps(tj[f"rollout_f64_{n4}_k{k}"]))
     json.dump(tj, open(tj_path, "w"), indent=1, sort_keys=True)
 
 

@@ -82,7 +82,7 @@ def test_gemm_x6_one_net_and_bad_arguments():
     assert L.dr_gemm_x6(3, 128, ptr(A), ptr(W), ptr(C), s) == _lib.DR_ERR_INVALID
 
 
-@pytest.mark.parametrize("m,chunks", [(65536, 64), (3072, 4)])
+@pytest.mark.parametrize("m,chunks", [(65536, 64), (3072, 4), (64, 2)])
 def test_gemm_x6_wgrad_as_accurate_as_fp32(m, chunks):
     """The weight-gradient form: ws[b][c] = G[b, chunk c]^T H[b, chunk c]
     (torch's split-K bmm layout), against f64, relative to sum|g h|."""
