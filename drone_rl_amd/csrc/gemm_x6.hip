@@ -34,6 +34,7 @@
 #include <type_traits>
 
 #include "common.h"
+#include "x6_split.h"
 
 #pragma clang fp contract(off)
 // glds16 clobbers m0 (reserved: the compiler sets it before each own use)
@@ -49,35 +50,6 @@ constexpr int XN = 256;                 // output columns
 constexpr int XWAVES = 8;               // waves of the weight-gradient kernel
 constexpr int XTHREADS = 64 * XWAVES;
 constexpr int64_t W_IMG = (int64_t)3 * XN * XK * 2;   // 384 KB per net: 3 bf16 planes
-
-typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
-typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
-typedef float f32x2_t __attribute__((ext_vector_type(2)));
-typedef float f32x16_t __attribute__((ext_vector_type(16)));
-typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
-
-__device__ inline uint32_t pk_bf16(float a, float b) {
-    return __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2_t){a, b}, bf16x2_t));
-}
-__device__ inline float lo_f(uint32_t p) { return __uint_as_float(p << 16); }
-__device__ inline float hi_f(uint32_t p) { return __uint_as_float(p & 0xffff0000u); }
-
-// x[0..7] = h + m + l exactly, packed as 8 bf16 per plane (element j in
-// bits 16j of the 128-bit value).
-__device__ inline void split8(const float x[8], u32x4_t &h, u32x4_t &m, u32x4_t &l) {
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-        const float a = x[2 * q], b = x[2 * q + 1];
-        const uint32_t ph = pk_bf16(a, b);
-        const float ra = a - lo_f(ph), rb = b - hi_f(ph);
-        const uint32_t pm = pk_bf16(ra, rb);
-        const float sa = ra - lo_f(pm), sb = rb - hi_f(pm);
-        h[q] = ph;
-        m[q] = pm;
-        l[q] = pk_bf16(sa, sb);
-    }
-}
-
 
 // Weight image of `batch` nets in the weight-stationary kernel's register
 // order: img[b][w][j][s][p][lane][16 B] is the MFMA B fragment of plane p of
@@ -516,6 +488,28 @@ __global__ __launch_bounds__(WS_THREADS, 1) void gemm_x6_ws_kernel(
 // products and per-output order); 110-111 vs 119-124 us for both nets at
 // 65,536 rows, 64 chunks (scripts/micro/wgrad_ab.py, same box).
 //
+// DR_WG_STAMPS (diagnostic builds only): s_memtime at five points of every
+// stage for the waves of blocks 0-7 (read back by dr_x6_diag_wg_stamps,
+// scripts/micro/wg_stamps.py); the stamps' scheduling barriers separate the
+// phases the compiler otherwise interleaves
+#ifndef DR_WG_STAMPS
+#define DR_WG_STAMPS 0
+#endif
+#if DR_WG_STAMPS
+__device__ unsigned long long g_wg_st[8 * 8 * 24 * 8];
+#define WG_STAMP(k, i)                                                                     \
+    do {                                                                                   \
+        __builtin_amdgcn_sched_barrier(0);                                                 \
+        const unsigned long long t__ = __builtin_amdgcn_s_memtime();                       \
+        if (blockIdx.x < 8 && (k) < 24 && lane == 0)                                       \
+            g_wg_st[((blockIdx.x * 8 + wid) * 24 + (k)) * 8 + (i)] = t__;                   \
+        __builtin_amdgcn_sched_barrier(0);                                                 \
+    } while (0)
+#else
+#define WG_STAMP(k, i) \
+    do {               \
+    } while (0)
+#endif
 constexpr int TW_BM = 32;                          // rows per stage
 constexpr int TW_PLANE_ROW = (128 + 256) * 2;      // 768 B: one plane of one row
 constexpr int TW_ROW = 3 * TW_PLANE_ROW + 64;      // 2,368 B
@@ -610,6 +604,7 @@ __global__ __launch_bounds__(XTHREADS) void gemm_x6_wgrad_kernel(
     load(G_ > 1 ? 1 : 0);
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
     for (int g = 0; g < G_; ++g) {
+        WG_STAMP(g, 0);
         const uint8_t *S = sh + (g & 1) * TW_STAGE + fbase;
         bf16x8_t fg[2][2][3], fhp[2][2][3];               // [k16 step][tile][plane]
 #pragma unroll
@@ -622,6 +617,7 @@ __global__ __launch_bounds__(XTHREADS) void gemm_x6_wgrad_kernel(
                     fg[s][i][p] = tr_frag(q + gcol + 64 * i);
                     fhp[s][i][p] = tr_frag(q + hcol + 64 * i);
                 }
+        WG_STAMP(g, 1);
 #pragma unroll
         for (int s = 0; s < 2; ++s) {
 #pragma unroll
@@ -642,10 +638,16 @@ __global__ __launch_bounds__(XTHREADS) void gemm_x6_wgrad_kernel(
             // the split of stage g + 1 (loaded one stage ago) into the other
             // buffer, beside the MFMAs (the last iteration re-splits the
             // last stage into the unused buffer: no branch in the loop)
-            if (s == 0) split_store((g + 1) & 1);
+            if (s == 0) {
+                WG_STAMP(g, 2);
+                split_store((g + 1) & 1);
+                WG_STAMP(g, 3);
+            }
         }
+        WG_STAMP(g, 4);
         load(g + 2 < G_ ? g + 2 : G_ - 1);
         asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        WG_STAMP(g, 5);
     }
     // D[n][k]: column k = fr, row n = (r & 3) + 8 (r >> 2) + 4 fh
     const int fr = lane & 31, fh = lane >> 5;
@@ -733,6 +735,14 @@ int dr_gemm_x6_wgrad(int64_t batch, int64_t m, int64_t chunks, const float *g, c
                                                     hipGetErrorString(e));
 }
 
+#if DR_WG_STAMPS
+int dr_x6_diag_wg_stamps(void *host_out, size_t bytes) {
+    if (bytes < sizeof(g_wg_st)) return DR_ERR_INVALID;
+    return hipMemcpyFromSymbol(host_out, HIP_SYMBOL(g_wg_st), sizeof(g_wg_st)) == hipSuccess
+               ? DR_OK
+               : DR_ERR_HIP;
+}
+#endif
 #if DR_WS_STAMPS
 int dr_x6_diag_stamps(void *host_out, size_t bytes) {
     if (bytes < sizeof(g_ws_st)) return DR_ERR_INVALID;

@@ -17,6 +17,7 @@
 #include <string>
 
 #include "common.h"
+#include "x6_split.h"
 
 #pragma clang fp contract(off)
 
@@ -1060,6 +1061,111 @@ __global__ __launch_bounds__(kBlock) void linear_tanh_kernel(int64_t m, int n,
                             tanh_fast(acc[2] + bb[2]), tanh_fast(acc[3] + bb[3])));
     }
 #endif
+}
+
+// The same layer on the bf16 matrix cores (round 4), for K <= 16 inputs and
+// n = 32 NT outputs: z = x W^T by the x6 scheme of gemm_x6.hip (x and W
+// split exactly into three bf16 planes, x zero-padded to 16 inputs; six plane
+// products per 32 x 32 tile, h.h in one accumulator and the five small ones
+// in another, added once), then + b and tanh.  The FMA chain of
+// linear_tanh_kernel was the kernel's VALU budget (15 FMAs per output against
+// 6 MFMAs per 32 x 32 x 16 tile here).  A row's outputs depend only on its
+// own inputs (no cross-row arithmetic), so the rollout's and the training
+// minibatches' h1 agree bitwise whatever the batch.  Waves own 32-row tiles
+// (grid-strided); the weights' B fragments (W[32 t + fr][8 fh ..]) stay in
+// registers; the accumulator layout (lane = column 32 t + fr, register r =
+// row (r & 3) + 8 (r >> 2) + 4 fh) makes each store instruction two full
+// 128-B row segments, through a buffer descriptor (per-register SGPR row
+// offsets) on full tiles.
+// DR_LT_MFMA 0 (A/B builds): the FMA-chain kernel for every shape
+#ifndef DR_LT_MFMA
+#define DR_LT_MFMA 1
+#endif
+template <int NT>
+__global__ __launch_bounds__(kBlock) void linear_tanh_mfma_kernel(int64_t m, int k,
+                                                                  const float *__restrict__ x,
+                                                                  const int32_t *__restrict__ rows,
+                                                                  LayerPair lp) {
+    constexpr int n = 32 * NT;
+    const float *__restrict__ w = lp.w[blockIdx.y];
+    const float *__restrict__ b = lp.b[blockIdx.y];
+    float *__restrict__ h = lp.h[blockIdx.y];
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const int fr = lane & 31, fh = lane >> 5;
+    bf16x8_t wh[NT], wm[NT], wl[NT];
+    float bias[NT];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+        float v[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+            const int kk = 8 * fh + e;
+            v[e] = kk < k ? w[(32 * t + fr) * k + kk] : 0.f;
+        }
+        u32x4_t ph, pm, pl;
+        split8(v, ph, pm, pl);
+        wh[t] = __builtin_bit_cast(bf16x8_t, ph);
+        wm[t] = __builtin_bit_cast(bf16x8_t, pm);
+        wl[t] = __builtin_bit_cast(bf16x8_t, pl);
+        bias[t] = b[32 * t + fr];
+    }
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+        h, 0, (int)min(m * n * 4, (int64_t)0x7fffffff), 0x00020000);
+    const int64_t ntiles = (m + 31) >> 5;
+    for (int64_t tile = (int64_t)blockIdx.x * 4 + wid; tile < ntiles;
+         tile += (int64_t)gridDim.x * 4) {
+        const int64_t r0 = tile * 32, row = r0 + fr;
+        float v[8];
+        const float *xr = x + (row < m ? (rows ? (int64_t)rows[row] : row) : 0) * k;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+            const int kk = 8 * fh + e;
+            v[e] = (row < m && kk < k) ? xr[kk] : 0.f;
+        }
+        u32x4_t qh, qm, ql;
+        split8(v, qh, qm, ql);
+        const bf16x8_t xh = __builtin_bit_cast(bf16x8_t, qh);
+        const bf16x8_t xm = __builtin_bit_cast(bf16x8_t, qm);
+        const bf16x8_t xl = __builtin_bit_cast(bf16x8_t, ql);
+        const bool full = r0 + 32 <= m && (r0 + 32) * n * 4 <= 0x7fffffff;
+        const uint32_t voff = (uint32_t)(((r0 + 4 * fh) * n + fr) * 4);
+#pragma unroll
+        for (int t = 0; t < NT; ++t) {
+            const f32x16_t zero = {};
+            const f32x16_t ah = __builtin_amdgcn_mfma_f32_32x32x16_bf16(xh, wh[t], zero, 0, 0, 0);
+            f32x16_t al = __builtin_amdgcn_mfma_f32_32x32x16_bf16(xh, wm[t], zero, 0, 0, 0);
+            al = __builtin_amdgcn_mfma_f32_32x32x16_bf16(xm, wh[t], al, 0, 0, 0);
+            al = __builtin_amdgcn_mfma_f32_32x32x16_bf16(xh, wl[t], al, 0, 0, 0);
+            al = __builtin_amdgcn_mfma_f32_32x32x16_bf16(xl, wh[t], al, 0, 0, 0);
+            al = __builtin_amdgcn_mfma_f32_32x32x16_bf16(xm, wm[t], al, 0, 0, 0);
+            float o[16];
+#pragma unroll
+            for (int r = 0; r < 16; r += 2) {
+#if DR_TANH_RAT
+                const f32x2 tz = tanh_rat2(f32x2{(ah[r] + al[r]) + bias[t],
+                                                 (ah[r + 1] + al[r + 1]) + bias[t]});
+                o[r] = tz.x;
+                o[r + 1] = tz.y;
+#else
+                o[r] = tanh_fast((ah[r] + al[r]) + bias[t]);
+                o[r + 1] = tanh_fast((ah[r + 1] + al[r + 1]) + bias[t]);
+#endif
+            }
+            if (full) {
+#pragma unroll
+                for (int r = 0; r < 16; ++r)
+                    __builtin_amdgcn_raw_buffer_store_b32(
+                        __float_as_uint(o[r]), rs, voff,
+                        (((r & 3) + 8 * (r >> 2)) * n + 32 * t) * 4, 0);
+            } else {
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const int64_t rr = r0 + (r & 3) + 8 * (r >> 2) + 4 * fh;
+                    if (rr < m) h[rr * n + 32 * t + fr] = o[r];
+                }
+            }
+        }
+    }
 }
 
 // Policy heads for inference (rollouts): mean = h_pi Wa^T + ba (m,4),
@@ -2274,9 +2380,26 @@ static int launch_linear_tanh(const char *who, int nets, int64_t m, int64_t k, i
         if ((((uintptr_t)lp.h[j]) | ((uintptr_t)lp.w[j])) & 15)
             return fail0(DR_ERR_INVALID, std::string(who) + ": h and w must be 16-byte aligned");
     }
+    hipStream_t st = as_stream(stream);
+    if (DR_LT_MFMA && k >= 1 && k <= 16 && n % 32 == 0) {
+        // the matrix-core form: 32-row tiles, 4 per block, one block per CU
+        // and net (two nets: 8 waves per CU)
+        const int64_t tiles = (m + 31) / 32, cap = device_cu_count();
+        const int nbm = (int)((tiles + 3) / 4 < cap ? (tiles + 3) / 4 : cap);
+        switch (n / 32) {
+#define DR_LTM_CASE(NT)                                                                        \
+    case NT:                                                                                   \
+        hipLaunchKernelGGL(linear_tanh_mfma_kernel<NT>, dim3(nbm, nets), dim3(kBlock), 0, st,   \
+                           m, (int)k, x, rows, lp);                                            \
+        break;
+            DR_LTM_CASE(1) DR_LTM_CASE(2) DR_LTM_CASE(3) DR_LTM_CASE(4) DR_LTM_CASE(5)
+            DR_LTM_CASE(6) DR_LTM_CASE(7) DR_LTM_CASE(8)
+#undef DR_LTM_CASE
+        }
+        return check_launch(who);
+    }
     const int64_t nbl = (m + DR_LT_RPB - 1) / DR_LT_RPB;    // >= RPB / 4 rows per wave
     const int nb = (int)(nbl < DR_LT_MAXB ? nbl : DR_LT_MAXB);
-    hipStream_t st = as_stream(stream);
     switch (k) {
 #define DR_LT_CASE(K)                                                                      \
     case K:                                                                                \
