@@ -1372,7 +1372,7 @@ __global__ __launch_bounds__(kWsThreads) void env_rollout_ws_kernel(EnvView<S> v
 }
 
 // ----------------------------------------------------------------------------
-// Split-physics K-step rollout (gym variant; DRONERL_ROLLOUT_AB).  The
+// Split-physics K-step rollout (gym variant, actions read from HBM).  The
 // warp-specialised kernel's physics wave, split by DATA into two waves on the
 // same SIMD, so that two dependent f64 chains interleave where one wave per
 // SIMD left the VALU idle about half of its cycles (two physics waves per

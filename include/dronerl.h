@@ -39,7 +39,7 @@
 extern "C" {
 #endif
 
-#define DR_ABI_VERSION 13
+#define DR_ABI_VERSION 14
 
 enum dr_status {
     DR_OK = 0,
