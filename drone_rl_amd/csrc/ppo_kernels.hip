@@ -1063,6 +1063,10 @@ __global__ __launch_bounds__(kBlock) void linear_tanh_kernel(int64_t m, int n,
 #endif
 }
 
+// DR_LT_MFMA 0 (A/B builds): the FMA-chain kernel for every shape
+#ifndef DR_LT_MFMA
+#define DR_LT_MFMA 1
+#endif
 // The same layer on the bf16 matrix cores (round 4), for K <= 16 inputs and
 // n = 32 NT outputs: z = x W^T by the x6 scheme of gemm_x6.hip (x and W
 // split exactly into three bf16 planes, x zero-padded to 16 inputs; six plane
@@ -1072,15 +1076,11 @@ __global__ __launch_bounds__(kBlock) void linear_tanh_kernel(int64_t m, int n,
 // 6 MFMAs per 32 x 32 x 16 tile here).  A row's outputs depend only on its
 // own inputs (no cross-row arithmetic), so the rollout's and the training
 // minibatches' h1 agree bitwise whatever the batch.  Waves own 32-row tiles
-// (grid-strided); the weights' B fragments (W[32 t + fr][8 fh ..]) stay in
-// registers; the accumulator layout (lane = column 32 t + fr, register r =
-// row (r & 3) + 8 (r >> 2) + 4 fh) makes each store instruction two full
-// 128-B row segments, through a buffer descriptor (per-register SGPR row
-// offsets) on full tiles.
-// DR_LT_MFMA 0 (A/B builds): the FMA-chain kernel for every shape
-#ifndef DR_LT_MFMA
-#define DR_LT_MFMA 1
-#endif
+// (grid-strided); the weights' fragments (W[32 t + fr][8 fh ..]) stay in
+// registers as the MFMA A operand, so D is the transposed tile: lane = row
+// r0 + fr, register 4 q + p = column 32 t + 8 q + 4 fh + p, i.e. one float4
+// per register quad and 4 store instructions per tile, through a buffer
+// descriptor over the tile's rows (rows past m fall outside it: dropped).
 template <int NT>
 __global__ __launch_bounds__(kBlock) void linear_tanh_mfma_kernel(int64_t m, int k,
                                                                   const float *__restrict__ x,
@@ -1093,7 +1093,6 @@ __global__ __launch_bounds__(kBlock) void linear_tanh_mfma_kernel(int64_t m, int
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     const int fr = lane & 31, fh = lane >> 5;
     bf16x8_t wh[NT], wm[NT], wl[NT];
-    float bias[NT];
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
         float v[8];
@@ -1107,11 +1106,9 @@ __global__ __launch_bounds__(kBlock) void linear_tanh_mfma_kernel(int64_t m, int
         wh[t] = __builtin_bit_cast(bf16x8_t, ph);
         wm[t] = __builtin_bit_cast(bf16x8_t, pm);
         wl[t] = __builtin_bit_cast(bf16x8_t, pl);
-        bias[t] = b[32 * t + fr];
     }
-    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-        h, 0, (int)min(m * n * 4, (int64_t)0x7fffffff), 0x00020000);
     const int64_t ntiles = (m + 31) >> 5;
+    const uint32_t voff = (uint32_t)((fr * n + 4 * fh) * 4);
     for (int64_t tile = (int64_t)blockIdx.x * 4 + wid; tile < ntiles;
          tile += (int64_t)gridDim.x * 4) {
         const int64_t r0 = tile * 32, row = r0 + fr;
@@ -1127,42 +1124,35 @@ __global__ __launch_bounds__(kBlock) void linear_tanh_mfma_kernel(int64_t m, int
         const bf16x8_t xh = __builtin_bit_cast(bf16x8_t, qh);
         const bf16x8_t xm = __builtin_bit_cast(bf16x8_t, qm);
         const bf16x8_t xl = __builtin_bit_cast(bf16x8_t, ql);
-        const bool full = r0 + 32 <= m && (r0 + 32) * n * 4 <= 0x7fffffff;
-        const uint32_t voff = (uint32_t)(((r0 + 4 * fh) * n + fr) * 4);
+        const int64_t nrow = m - r0 < 32 ? m - r0 : 32;
+        const __amdgpu_buffer_rsrc_t rs =
+            __builtin_amdgcn_make_buffer_rsrc(h + r0 * n, 0, (int)(nrow * n * 4), 0x00020000);
 #pragma unroll
         for (int t = 0; t < NT; ++t) {
             const f32x16_t zero = {};
-            const f32x16_t ah = __builtin_amdgcn_mfma_f32_32x32x16_bf16(xh, wh[t], zero, 0, 0, 0);
-            f32x16_t al = __builtin_amdgcn_mfma_f32_32x32x16_bf16(xh, wm[t], zero, 0, 0, 0);
-            al = __builtin_amdgcn_mfma_f32_32x32x16_bf16(xm, wh[t], al, 0, 0, 0);
-            al = __builtin_amdgcn_mfma_f32_32x32x16_bf16(xh, wl[t], al, 0, 0, 0);
-            al = __builtin_amdgcn_mfma_f32_32x32x16_bf16(xl, wh[t], al, 0, 0, 0);
-            al = __builtin_amdgcn_mfma_f32_32x32x16_bf16(xm, wm[t], al, 0, 0, 0);
-            float o[16];
+            const f32x16_t ah = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wh[t], xh, zero, 0, 0, 0);
+            f32x16_t al = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wm[t], xh, zero, 0, 0, 0);
+            al = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wh[t], xm, al, 0, 0, 0);
+            al = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wl[t], xh, al, 0, 0, 0);
+            al = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wh[t], xl, al, 0, 0, 0);
+            al = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wm[t], xm, al, 0, 0, 0);
 #pragma unroll
-            for (int r = 0; r < 16; r += 2) {
+            for (int q = 0; q < 4; ++q) {
+                const float4 bq = ld4(b + 32 * t + 8 * q + 4 * fh);
+                const float z0 = (ah[4 * q] + al[4 * q]) + bq.x;
+                const float z1 = (ah[4 * q + 1] + al[4 * q + 1]) + bq.y;
+                const float z2 = (ah[4 * q + 2] + al[4 * q + 2]) + bq.z;
+                const float z3 = (ah[4 * q + 3] + al[4 * q + 3]) + bq.w;
+                typedef uint32_t lt_u32x4 __attribute__((ext_vector_type(4)));
 #if DR_TANH_RAT
-                const f32x2 tz = tanh_rat2(f32x2{(ah[r] + al[r]) + bias[t],
-                                                 (ah[r + 1] + al[r + 1]) + bias[t]});
-                o[r] = tz.x;
-                o[r + 1] = tz.y;
+                const f32x2 t01 = tanh_rat2(f32x2{z0, z1}), t23 = tanh_rat2(f32x2{z2, z3});
+                const lt_u32x4 o = {__float_as_uint(t01.x), __float_as_uint(t01.y),
+                                    __float_as_uint(t23.x), __float_as_uint(t23.y)};
 #else
-                o[r] = tanh_fast((ah[r] + al[r]) + bias[t]);
-                o[r + 1] = tanh_fast((ah[r + 1] + al[r + 1]) + bias[t]);
+                const lt_u32x4 o = {__float_as_uint(tanh_fast(z0)), __float_as_uint(tanh_fast(z1)),
+                                    __float_as_uint(tanh_fast(z2)), __float_as_uint(tanh_fast(z3))};
 #endif
-            }
-            if (full) {
-#pragma unroll
-                for (int r = 0; r < 16; ++r)
-                    __builtin_amdgcn_raw_buffer_store_b32(
-                        __float_as_uint(o[r]), rs, voff,
-                        (((r & 3) + 8 * (r >> 2)) * n + 32 * t) * 4, 0);
-            } else {
-#pragma unroll
-                for (int r = 0; r < 16; ++r) {
-                    const int64_t rr = r0 + (r & 3) + 8 * (r >> 2) + 4 * fh;
-                    if (rr < m) h[rr * n + 32 * t + fr] = o[r];
-                }
+                __builtin_amdgcn_raw_buffer_store_b128(o, rs, voff, (32 * t + 8 * q) * 4, 0);
             }
         }
     }
