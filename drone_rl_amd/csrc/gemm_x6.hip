@@ -197,26 +197,14 @@ __device__ unsigned long long g_ws_st[8 * 4 * 24 * 8];
 // epilogue pads them, and tests/test_x6_asm_hazards.py checks that no
 // compiler-generated instruction reads an accumulator between these
 // statements.
-// DR_WS_TSTORE (A/B): 1 = the weight fragment as the A operand, so D holds
-// the transposed tile (lane = output row, 4 consecutive columns per register
-// quad) and each lane stores float4s: 4 store instructions per tile instead
-// of 16
-#ifndef DR_WS_TSTORE
-#define DR_WS_TSTORE 0
-#endif
-#if DR_WS_TSTORE
-#define X6_OPS "%2, %1"
-#else
-#define X6_OPS "%1, %2"
-#endif
 __device__ inline void mfma_x6_a(f32x16_t &d, const bf16x8_t &x, const bf16x8_t &w) {
-    asm volatile("v_mfma_f32_32x32x16_bf16 %0, " X6_OPS ", %0" : "+v"(d) : "v"(x), "a"(w));
+    asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+v"(d) : "v"(x), "a"(w));
 }
 __device__ inline void mfma_x6_v(f32x16_t &d, const bf16x8_t &x, const bf16x8_t &w) {
-    asm volatile("v_mfma_f32_32x32x16_bf16 %0, " X6_OPS ", %0" : "+v"(d) : "v"(x), "v"(w));
+    asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+v"(d) : "v"(x), "v"(w));
 }
 __device__ inline void mfma_x6_first(f32x16_t &d, const bf16x8_t &x, const bf16x8_t &w) {
-    asm volatile("v_mfma_f32_32x32x16_bf16 %0, " X6_OPS ", 0" : "=v"(d) : "v"(x), "a"(w));
+    asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, 0" : "=v"(d) : "v"(x), "a"(w));
 }
 // The six products of one (column tile, k16 step): h += xh.wh; l += xh.wm,
 // xm.wh, xh.wl, xl.wh, xm.wm (round 3's order, so bitwise its C)
@@ -333,19 +321,6 @@ __global__ __launch_bounds__(WS_THREADS, 1) void gemm_x6_ws_kernel(
     // segments, through a buffer descriptor of the row step's 32 KB of C (a
     // per-lane offset plus an SGPR offset per register: no VALU per store)
     const int st_off = (4 * fh * XN + fr) * 4;
-    // DR_WS_TSTORE: D[n][m], lane = row m (fr), register 4 q + p = column
-    // 8 q + 4 fh + p of the tile: one float4 per register quad
-    const int st_off4 = (fr * XN + 4 * fh) * 4;
-    auto store_quad = [&](int k, int t, int q) {
-        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-            Cb + (int64_t)(j0 + k * per) * WS_RS * XN, 0, k < 0 ? 0 : WS_RS * XN * 4,
-            0x00020000);
-        typedef uint32_t u32x4_t_ __attribute__((ext_vector_type(4)));
-        const u32x4_t_ v = {__float_as_uint(acc_h[t][4 * q]), __float_as_uint(acc_h[t][4 * q + 1]),
-                            __float_as_uint(acc_h[t][4 * q + 2]),
-                            __float_as_uint(acc_h[t][4 * q + 3])};
-        __builtin_amdgcn_raw_buffer_store_b128(v, rs, st_off4, (64 * w + 32 * t + 8 * q) * 4, 0);
-    };
     auto store_one = [&](int k, int t, int r) {
         // k = -1 (tile 1 of no row step, in row step 0): a 0-byte range, the
         // stores are dropped
@@ -432,11 +407,7 @@ __global__ __launch_bounds__(WS_THREADS, 1) void gemm_x6_ws_kernel(
                 const AFrag &x = fb[g % WS_NF];
                 mfma_x6_group(s == 0, acc_h[t], acc_l[t], x[0], x[1], x[2], Wa[t][s][0],
                               Wa[t][s][1], Wv[t][s]);
-                if (DR_WS_TSTORE) {
-                    if (DR_WS_ABL != 3 && (s & 3) == 2) store_quad(ko, 1 - t, s >> 2);
-                } else if (DR_WS_ABL != 3) {
-                    store_one(ko, 1 - t, s);
-                }
+                if (DR_WS_ABL != 3) store_one(ko, 1 - t, s);
                 if (sp && (s & 3) == 1) {
                     // the half-unit's split (its read, one k16 step ago, has
                     // landed behind the MFMAs)
@@ -486,13 +457,7 @@ __global__ __launch_bounds__(WS_THREADS, 1) void gemm_x6_ws_kernel(
     if (R > 0) {
         finish_tile(1);
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-            if (DR_WS_TSTORE) {
-                if ((r & 3) == 0) store_quad(R - 1, 1, r >> 2);
-            } else {
-                store_one(R - 1, 1, r);
-            }
-        }
+        for (int r = 0; r < 16; ++r) store_one(R - 1, 1, r);
     }
     // the clamped staging DMA of the last steps lands before the block's LDS
     // is released

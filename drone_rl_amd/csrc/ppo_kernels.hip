@@ -17,7 +17,6 @@
 #include <string>
 
 #include "common.h"
-#include "x6_split.h"
 
 #pragma clang fp contract(off)
 
@@ -830,6 +829,8 @@ __device__ inline float4 ld4(const float *p) { return *reinterpret_cast<const fl
 // backward 31.8 -> 30.3 us); with the dr_gemm_x6 GEMMs reading these rows
 // back, plain stores leave them in the Infinity Cache for those GEMMs:
 // 6.000 -> 6.033 / 5.999 -> 6.056 updates/s (bench.py, same box), so 0.
+// Round 4 (weight-stationary GEMMs): 6.46-6.48 with NT stores against
+// 6.48-6.51 without (two alternating pairs, one box).
 #ifndef DR_PPO_NT
 #define DR_PPO_NT 0
 #endif
@@ -1061,101 +1062,6 @@ __global__ __launch_bounds__(kBlock) void linear_tanh_kernel(int64_t m, int n,
                             tanh_fast(acc[2] + bb[2]), tanh_fast(acc[3] + bb[3])));
     }
 #endif
-}
-
-// DR_LT_MFMA 0 (A/B builds): the FMA-chain kernel for every shape
-#ifndef DR_LT_MFMA
-#define DR_LT_MFMA 1
-#endif
-// The same layer on the bf16 matrix cores (round 4), for K <= 16 inputs and
-// n = 32 NT outputs: z = x W^T by the x6 scheme of gemm_x6.hip (x and W
-// split exactly into three bf16 planes, x zero-padded to 16 inputs; six plane
-// products per 32 x 32 tile, h.h in one accumulator and the five small ones
-// in another, added once), then + b and tanh.  The FMA chain of
-// linear_tanh_kernel was the kernel's VALU budget (15 FMAs per output against
-// 6 MFMAs per 32 x 32 x 16 tile here).  A row's outputs depend only on its
-// own inputs (no cross-row arithmetic), so the rollout's and the training
-// minibatches' h1 agree bitwise whatever the batch.  Waves own 32-row tiles
-// (grid-strided); the weights' fragments (W[32 t + fr][8 fh ..]) stay in
-// registers as the MFMA A operand, so D is the transposed tile: lane = row
-// r0 + fr, register 4 q + p = column 32 t + 8 q + 4 fh + p, i.e. one float4
-// per register quad and 4 store instructions per tile, through a buffer
-// descriptor over the tile's rows (rows past m fall outside it: dropped).
-template <int NT>
-__global__ __launch_bounds__(kBlock) void linear_tanh_mfma_kernel(int64_t m, int k,
-                                                                  const float *__restrict__ x,
-                                                                  const int32_t *__restrict__ rows,
-                                                                  LayerPair lp) {
-    constexpr int n = 32 * NT;
-    const float *__restrict__ w = lp.w[blockIdx.y];
-    const float *__restrict__ b = lp.b[blockIdx.y];
-    float *__restrict__ h = lp.h[blockIdx.y];
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    const int fr = lane & 31, fh = lane >> 5;
-    bf16x8_t wh[NT], wm[NT], wl[NT];
-#pragma unroll
-    for (int t = 0; t < NT; ++t) {
-        float v[8];
-#pragma unroll
-        for (int e = 0; e < 8; ++e) {
-            const int kk = 8 * fh + e;
-            v[e] = kk < k ? w[(32 * t + fr) * k + kk] : 0.f;
-        }
-        u32x4_t ph, pm, pl;
-        split8(v, ph, pm, pl);
-        wh[t] = __builtin_bit_cast(bf16x8_t, ph);
-        wm[t] = __builtin_bit_cast(bf16x8_t, pm);
-        wl[t] = __builtin_bit_cast(bf16x8_t, pl);
-    }
-    const int64_t ntiles = (m + 31) >> 5;
-    const uint32_t voff = (uint32_t)((fr * n + 4 * fh) * 4);
-    for (int64_t tile = (int64_t)blockIdx.x * 4 + wid; tile < ntiles;
-         tile += (int64_t)gridDim.x * 4) {
-        const int64_t r0 = tile * 32, row = r0 + fr;
-        float v[8];
-        const float *xr = x + (row < m ? (rows ? (int64_t)rows[row] : row) : 0) * k;
-#pragma unroll
-        for (int e = 0; e < 8; ++e) {
-            const int kk = 8 * fh + e;
-            v[e] = (row < m && kk < k) ? xr[kk] : 0.f;
-        }
-        u32x4_t qh, qm, ql;
-        split8(v, qh, qm, ql);
-        const bf16x8_t xh = __builtin_bit_cast(bf16x8_t, qh);
-        const bf16x8_t xm = __builtin_bit_cast(bf16x8_t, qm);
-        const bf16x8_t xl = __builtin_bit_cast(bf16x8_t, ql);
-        const int64_t nrow = m - r0 < 32 ? m - r0 : 32;
-        const __amdgpu_buffer_rsrc_t rs =
-            __builtin_amdgcn_make_buffer_rsrc(h + r0 * n, 0, (int)(nrow * n * 4), 0x00020000);
-#pragma unroll
-        for (int t = 0; t < NT; ++t) {
-            const f32x16_t zero = {};
-            const f32x16_t ah = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wh[t], xh, zero, 0, 0, 0);
-            f32x16_t al = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wm[t], xh, zero, 0, 0, 0);
-            al = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wh[t], xm, al, 0, 0, 0);
-            al = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wl[t], xh, al, 0, 0, 0);
-            al = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wh[t], xl, al, 0, 0, 0);
-            al = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wm[t], xm, al, 0, 0, 0);
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                const float4 bq = ld4(b + 32 * t + 8 * q + 4 * fh);
-                const float z0 = (ah[4 * q] + al[4 * q]) + bq.x;
-                const float z1 = (ah[4 * q + 1] + al[4 * q + 1]) + bq.y;
-                const float z2 = (ah[4 * q + 2] + al[4 * q + 2]) + bq.z;
-                const float z3 = (ah[4 * q + 3] + al[4 * q + 3]) + bq.w;
-                typedef uint32_t lt_u32x4 __attribute__((ext_vector_type(4)));
-#if DR_TANH_RAT
-                const f32x2 t01 = tanh_rat2(f32x2{z0, z1}), t23 = tanh_rat2(f32x2{z2, z3});
-                const lt_u32x4 o = {__float_as_uint(t01.x), __float_as_uint(t01.y),
-                                    __float_as_uint(t23.x), __float_as_uint(t23.y)};
-#else
-                const lt_u32x4 o = {__float_as_uint(tanh_fast(z0)), __float_as_uint(tanh_fast(z1)),
-                                    __float_as_uint(tanh_fast(z2)), __float_as_uint(tanh_fast(z3))};
-#endif
-                __builtin_amdgcn_raw_buffer_store_b128(o, rs, voff, (32 * t + 8 * q) * 4, 0);
-            }
-        }
-    }
 }
 
 // Policy heads for inference (rollouts): mean = h_pi Wa^T + ba (m,4),
@@ -2371,23 +2277,6 @@ static int launch_linear_tanh(const char *who, int nets, int64_t m, int64_t k, i
             return fail0(DR_ERR_INVALID, std::string(who) + ": h and w must be 16-byte aligned");
     }
     hipStream_t st = as_stream(stream);
-    if (DR_LT_MFMA && k >= 1 && k <= 16 && n % 32 == 0) {
-        // the matrix-core form: 32-row tiles, 4 per block, one block per CU
-        // and net (two nets: 8 waves per CU)
-        const int64_t tiles = (m + 31) / 32, cap = device_cu_count();
-        const int nbm = (int)((tiles + 3) / 4 < cap ? (tiles + 3) / 4 : cap);
-        switch (n / 32) {
-#define DR_LTM_CASE(NT)                                                                        \
-    case NT:                                                                                   \
-        hipLaunchKernelGGL(linear_tanh_mfma_kernel<NT>, dim3(nbm, nets), dim3(kBlock), 0, st,   \
-                           m, (int)k, x, rows, lp);                                            \
-        break;
-            DR_LTM_CASE(1) DR_LTM_CASE(2) DR_LTM_CASE(3) DR_LTM_CASE(4) DR_LTM_CASE(5)
-            DR_LTM_CASE(6) DR_LTM_CASE(7) DR_LTM_CASE(8)
-#undef DR_LTM_CASE
-        }
-        return check_launch(who);
-    }
     const int64_t nbl = (m + DR_LT_RPB - 1) / DR_LT_RPB;    // >= RPB / 4 rows per wave
     const int nb = (int)(nbl < DR_LT_MAXB ? nbl : DR_LT_MAXB);
     switch (k) {

@@ -323,10 +323,7 @@ int dr_tanh_backward(int64_t m, int64_t n, const float *grad_h, const float *h,
    n <= 256; h 16-byte aligned.  Replaces an addmm plus a separate tanh pass
    over the (m,n) activation.  `rows` (nullable, m int32): input row r is
    x[rows[r]] -- a minibatch read in place from the rollout buffer through
-   its permutation (RolloutBuffer.get without the gather copy).  For k <= 16
-   and n % 32 == 0 the product runs on the bf16 matrix cores with the x6
-   exact split (fp32-accurate; each row depends only on its own inputs), else
-   as an f32 FMA chain. */
+   its permutation (RolloutBuffer.get without the gather copy). */
 int dr_linear_tanh(int64_t m, int64_t k, int64_t n, const float *x,
                    const int32_t *rows, const float *w, const float *b, float *h,
                    void *stream);
