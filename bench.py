@@ -103,6 +103,9 @@ def parse():
     ap.add_argument("--rollout-k", type=int, default=32,
                     help="steps per launch of the K-step rollout kernel line (0 = skip)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"))
+    ap.add_argument("--kernel-stats",
+                    default=os.path.join(ROOT, "profiles", "r04_kernel_stats.csv"),
+                    help="rocprofv3 --stats csv whose kernel averages the ppo block reports")
     ap.add_argument("--headline", choices=["rollout", "step"], default="rollout",
                     help="kernel of the headline value: the K-step rollout kernel or one "
                          "dr_step launch per step")
@@ -510,7 +513,31 @@ def ppo_kernel_times(tr, reps=20):
     return {n: tj[i + 1] - tj[i] for i, n in enumerate(names)}
 
 
-def ppo_roofline(cfg, s_per_update, ktimes):
+# bench.py's PPO step names -> the kernel each launches (rocprofv3 names)
+PPO_KERNEL_NAMES = {"gather_minibatch": "gather_minibatch_kernel",
+                    "linear_tanh": "linear_tanh_kernel", "ppo_head": "ppo_head_kernel",
+                    "first_layer_bwd": "first_layer_bwd_kernel",
+                    "gemm_x6_fwd": "gemm_x6_ws_kernel", "gemm_x6_bwd": "gemm_x6_ws_kernel",
+                    "gemm_x6_wgrad": "gemm_x6_wgrad_kernel", "split_weights": "split_weights_kernel"}
+
+
+def rocprof_averages(path):
+    """{kernel name: average us} from a committed rocprofv3 --stats csv
+    (profiles/r04_kernel_stats.csv: scripts/micro/r4p3.sh's run of this
+    bench), or {} when absent."""
+    import csv
+    out = {}
+    try:
+        for r in csv.DictReader(open(path)):
+            for k in set(PPO_KERNEL_NAMES.values()):
+                if k + "(" in r["Name"] or k + "<" in r["Name"]:
+                    out[k] = float(r["AverageNs"]) / 1e3
+    except (OSError, KeyError, ValueError):
+        return {}
+    return out
+
+
+def ppo_roofline(cfg, s_per_update, ktimes, rocprof=None):
     """The ppo block's roofline: the whole update's fp32-equivalent FLOP
     rate against the f32 matrix peak, the 256x256 layer's x6 GEMMs against
     the bf16 MFMA peak (6 bf16 products per fp32 product), and the
@@ -525,17 +552,29 @@ def ppo_roofline(cfg, s_per_update, ktimes):
             "ppo_head": 2 * 1024 + 2 * 1024 + 44,
             "first_layer_bwd": 2 * 2 * 1024 + 60}
     kern = {}
+    rocprof = rocprof or {}
     for name, us in ktimes.items():
         e = {"us": round(us, 2)}
+        rp = rocprof.get(PPO_KERNEL_NAMES.get(name, ""))
+        if rp is not None:
+            # the kernel's own average duration (rocprofv3, committed csv;
+            # the forward / input-gradient GEMM share one kernel), beside the
+            # in-step event split above (which includes the launch boundary)
+            e["rocprof_us"] = round(rp, 2)
         if name.startswith("gemm_x6"):
             tf32 = gemm_flop / (us * 1e-6) / 1e12
             e.update({"bound": "mfma", "fp32_equiv_tflops": round(tf32, 1),
                       "bf16_mfma_tflops": round(6 * tf32, 1),
                       "frac": round(6 * tf32 / BF16_DENSE_PEAK_TFLOPS, 4)})
+            if rp is not None:
+                e["rocprof_frac"] = round(6 * gemm_flop / (rp * 1e-6) / 1e12 /
+                                          BF16_DENSE_PEAK_TFLOPS, 4)
         elif name in rows:
             gbs = rows[name] * M / (us * 1e-6) / 1e9
             e.update({"bound": "hbm", "bytes": rows[name] * M, "achieved_GBs": round(gbs, 1),
                       "frac": round(gbs / HBM_PEAK_GBS, 4)})
+            if rp is not None:
+                e["rocprof_frac"] = round(rows[name] * M / (rp * 1e-6) / 1e9 / HBM_PEAK_GBS, 4)
         kern[name] = e
     ach = flop_update / s_per_update / 1e12
     x6 = kern.get("gemm_x6_fwd")
@@ -545,10 +584,12 @@ def ppo_roofline(cfg, s_per_update, ktimes):
            "frac": round(ach / F32_MATRIX_PEAK_TFLOPS, 4),
            "basis": "fp32-equivalent FLOP per update (rollout forward 280,064 FLOP/sample + "
                     "3 x forward per sample and epoch, SURVEY.md 8d) / s_per_update, against "
-                    "the f32 matrix peak",
+                    "the f32 matrix peak (the model's arithmetic at fp32 accuracy; the "
+                    "hardware runs the 256x256 GEMMs as 6 bf16 MFMA products each: "
+                    "kernels_per_minibatch.gemm_x6_* carry their bf16-MFMA fractions)",
            "kernels_per_minibatch": kern}
     if x6 is not None:
-        out["dominant_kernel"] = {"kernel": "gemm_x6_cs_kernel (forward)", "bound": "mfma",
+        out["dominant_kernel"] = {"kernel": "gemm_x6_ws_kernel (forward)", "bound": "mfma",
                                   "achieved": x6["bf16_mfma_tflops"],
                                   "peak": BF16_DENSE_PEAK_TFLOPS, "unit": "TFLOP/s",
                                   "frac": x6["frac"]}
@@ -620,7 +661,8 @@ def time_ppo(args, rank, world, device, force_dp=False, dp_graph=False, profile=
                       if world > 1 or tr.dp_collective else "none"},
            "last_update_stats": stats, "episodes": es}
     if profile and world == 1 and tr._train_fast() and not tr.dp_step:
-        res["roofline"] = ppo_roofline(cfg, el / K, ppo_kernel_times(tr))
+        res["roofline"] = ppo_roofline(cfg, el / K, ppo_kernel_times(tr),
+                                       rocprof_averages(args.kernel_stats))
         res["roofline"]["kernel_timing"] = (
             "per kernel of one optimizer step: graph replays of the step's first j kernels "
             "x 20, timed by HIP events; kernel j = T_j - T_(j-1) (launch gap included)")

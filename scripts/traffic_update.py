@@ -17,11 +17,15 @@ N = 65536
 
 
 def avg(path, counter, kernel="env_rollout"):
-    vals = []
+    """Mean counter value over the matching dispatches of the largest grid
+    (bench.py's host-floor probe launches the same kernel on 64 envs)."""
+    rows = []
     for f in glob.glob(os.path.join(path, "**", "*counter_collection.csv"), recursive=True):
         for r in csv.DictReader(open(f)):
             if kernel in r["Kernel_Name"] and r["Counter_Name"] == counter:
-                vals.append(float(r["Counter_Value"]))
+                rows.append((int(r["Grid_Size"]), float(r["Counter_Value"])))
+    big = max((g for g, _ in rows), default=0)
+    vals = [v for g, v in rows if g == big]
     if not vals:
         raise SystemExit(f"no {counter} rows under {path}")
     return sum(vals) / len(vals), len(vals)
