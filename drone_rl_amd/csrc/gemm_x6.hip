@@ -607,8 +607,7 @@ __global__ __launch_bounds__(XTHREADS) void gemm_x6_wgrad_kernel(
         WG_STAMP(g, 0);
         const uint8_t *S = sh + (g & 1) * TW_STAGE + fbase;
         bf16x8_t fg[2][2][3], fhp[2][2][3];               // [k16 step][tile][plane]
-#pragma unroll
-        for (int s = 0; s < 2; ++s)
+        auto read_step = [&](int s) {
 #pragma unroll
             for (int i = 0; i < 2; ++i)
 #pragma unroll
@@ -617,6 +616,14 @@ __global__ __launch_bounds__(XTHREADS) void gemm_x6_wgrad_kernel(
                     fg[s][i][p] = tr_frag(q + gcol + 64 * i);
                     fhp[s][i][p] = tr_frag(q + hcol + 64 * i);
                 }
+        };
+        // the split of stage g + 1 (loaded one stage ago) into the other
+        // buffer sits between the two k16 steps' MFMAs (the last iteration
+        // re-splits the last stage into the unused buffer: no branch in the
+        // loop).  After both k16 steps, before the fragment reads, or with
+        // each k16 step's reads in front of its MFMAs measured the same.
+        read_step(0);
+        read_step(1);
         WG_STAMP(g, 1);
 #pragma unroll
         for (int s = 0; s < 2; ++s) {
@@ -635,9 +642,6 @@ __global__ __launch_bounds__(XTHREADS) void gemm_x6_wgrad_kernel(
                     t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], c[1], t, 0, 0, 0);
                     acc_l[i][j] = t;
                 }
-            // the split of stage g + 1 (loaded one stage ago) into the other
-            // buffer, beside the MFMAs (the last iteration re-splits the
-            // last stage into the unused buffer: no branch in the loop)
             if (s == 0) {
                 WG_STAMP(g, 2);
                 split_store((g + 1) & 1);
