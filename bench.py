@@ -537,71 +537,6 @@ def rocprof_averages(path):
     return out
 
 
-def ppo_kernel_times_events(tr, reps=20):
-    """Every kernel of one optimizer step timed INSIDE whole steps: `reps`
-    full steps are captured into one hipGraph with a HIP event recorded
-    after each kernel (FusedTrainStep.mark), and kernel j takes the median
-    over the repetitions of E_j - E_(j-1) on the replay.  Unlike the prefix
-    form (ppo_kernel_times), each kernel runs between its real neighbours,
-    so the cache state it inherits and leaves is the step's own.  Returns
-    None if the events cannot be timed in a graph."""
-    import statistics
-
-    import torch
-
-    from drone_rl_amd import ppo_kernels as K
-    cfg = tr.cfg
-    T, N, M = cfg.n_steps, cfg.num_envs, cfg.batch_size
-    obs_flat = tr.obs[:T].reshape(T * N, -1)
-    act_flat = tr.actions.reshape(T * N, 4)
-    idx = tr.perm(seed=99, counter=0)[:M]
-    stream = torch.cuda.current_stream(tr.device)
-    sched = tr.opt.schedule(tr.opt.t + 1, 1).to(tr.device)
-
-    def step(rec):
-        def mark(name):
-            # external: recorded as an event node of the captured graph
-            e = torch.cuda.Event(enable_timing=True, external=True)
-            e.record()
-            rec.append((name, e))
-        mark("start")
-        tr.fused.mark = mark
-        try:
-            K.gather_minibatch(idx, obs_flat, act_flat, tr.aux, tr.mb_obs, tr.mb_act,
-                               tr.mb_aux, adv_part=tr.head.adv_part)
-            mark("gather_minibatch")
-            grad, _ = tr.fused.step(tr.mb_obs, tr.mb_act, tr.mb_aux, tr.head, adv_ready=True,
-                                    defer_finish=True)
-            tr.opt.step_finish_sched(grad, tr.fused.finish, sched)
-            mark("grad_finish_clip_adam")
-        finally:
-            tr.fused.mark = None
-
-    try:
-        step([])                         # eager once: lazy init
-        torch.cuda.synchronize(tr.device)
-        recs = [[] for _ in range(reps)]
-        cs = torch.cuda.Stream(tr.device)
-        cs.wait_stream(stream)
-        g = torch.cuda.CUDAGraph()
-        with torch.cuda.stream(cs), torch.cuda.graph(g, stream=cs):
-            for r in range(reps):
-                step(recs[r])
-        stream.wait_stream(cs)
-        g.replay()                       # upload
-        g.replay()
-        torch.cuda.synchronize(tr.device)
-        per = {}
-        for rec in recs:
-            for (_, e0), (name, e1) in zip(rec, rec[1:]):
-                per.setdefault(name, []).append(e0.elapsed_time(e1) * 1e3)
-        del g
-        return {n: statistics.median(v) for n, v in per.items()}
-    except (RuntimeError, ValueError, TypeError) as ex:
-        print(f"bench: in-step kernel events unavailable: {ex!r}"[:300], file=sys.stderr)
-        return None
-
-
 def ppo_roofline(cfg, s_per_update, ktimes, rocprof=None):
     """The ppo block's roofline: the whole update's fp32-equivalent FLOP
     rate against the f32 matrix peak, the 256x256 layer's x6 GEMMs against
@@ -726,13 +661,14 @@ def time_ppo(args, rank, world, device, force_dp=False, dp_graph=False, profile=
                       if world > 1 or tr.dp_collective else "none"},
            "last_update_stats": stats, "episodes": es}
     if profile and world == 1 and tr._train_fast() and not tr.dp_step:
-        kt = ppo_kernel_times_events(tr)
-        res["roofline"] = ppo_roofline(cfg, el / K, kt if kt else ppo_kernel_times(tr),
+        res["roofline"] = ppo_roofline(cfg, el / K, ppo_kernel_times(tr),
                                        rocprof_averages(args.kernel_stats))
         res["roofline"]["kernel_timing"] = (
-            "HIP events after every kernel inside reps of whole steps captured in one "
-            "hipGraph (median per kernel)" if kt else
-            "graph-replayed step prefixes, T_j - T_(j-1) (in-graph events unavailable)")
+            "us: graph replays of the step's first j kernels x 20, timed by HIP events, kernel "
+            "j = T_j - T_(j-1) (the step's tail and the next repetition's head shift with j, "
+            "so cache effects land on neighbours); rocprof_us: the kernel's own duration in "
+            "whole training steps (rocprofv3 --stats, --kernel-stats csv; HIP graphs on ROCm "
+            "take no timed event nodes)")
     tr.close()
     return res
 
