@@ -1,0 +1,59 @@
+"""CPU checks of the bench line's profile plumbing: the committed rocprofv3
+kernel stats feed the ppo roofline's in-step kernel durations, and the PMC
+traffic reduction keeps only the headline-sized dispatches (bench.py's
+host-floor probe launches the same rollout kernel on 64 envs)."""
+import csv
+import importlib.util
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import bench  # noqa: E402
+
+
+def _traffic_update():
+    spec = importlib.util.spec_from_file_location(
+        "traffic_update", os.path.join(ROOT, "scripts", "traffic_update.py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod
+
+
+def test_committed_kernel_stats_cover_every_ppo_kernel():
+    r = bench.rocprof_averages(os.path.join(ROOT, "profiles", "r04_kernel_stats.csv"))
+    for k in set(bench.PPO_KERNEL_NAMES.values()):
+        assert k in r and r[k] > 0, k
+    assert bench.rocprof_averages(os.path.join(ROOT, "profiles", "no_such.csv")) == {}
+
+
+def test_ppo_roofline_carries_rocprof_durations_and_fractions():
+    class Cfg:
+        batch_size, num_envs, n_steps, n_epochs = 65536, 65536, 32, 10
+    rp = {"gemm_x6_ws_kernel": 80.0, "linear_tanh_kernel": 30.0}
+    out = bench.ppo_roofline(Cfg, 0.15, {"gemm_x6_fwd": 100.0, "linear_tanh": 35.0,
+                                         "grad_finish_clip_adam": 10.0}, rp)
+    k = out["kernels_per_minibatch"]
+    # 6 bf16 products x 2 nets x 2 M 256 256 FLOP over 80 us against 2.5 PF
+    flop = 6 * 2 * 2 * 65536 * 256 * 256
+    assert abs(k["gemm_x6_fwd"]["rocprof_frac"] - flop / 80e-6 / 2.5e15) < 1e-3
+    assert k["gemm_x6_fwd"]["rocprof_us"] == 80.0 and k["gemm_x6_fwd"]["us"] == 100.0
+    assert abs(k["linear_tanh"]["rocprof_frac"] - (15 * 4 + 2 * 256 * 4) * 65536 / 30e-6 / 8e12) < 1e-3
+    assert "rocprof_us" not in k["grad_finish_clip_adam"]
+    assert out["dominant_kernel"]["kernel"].startswith("gemm_x6_ws_kernel")
+
+
+def test_traffic_average_keeps_the_largest_grid(tmp_path):
+    d = tmp_path / "k32_FETCH_SIZE"
+    d.mkdir()
+    with open(d / "run_counter_collection.csv", "w", newline="") as f:
+        w = csv.DictWriter(f, ["Kernel_Name", "Grid_Size", "Counter_Name", "Counter_Value"])
+        w.writeheader()
+        for g, v in ((196608, 100.0), (196608, 102.0), (768, 1.0), (768, 1.0), (768, 1.0)):
+            w.writerow({"Kernel_Name": "void dr::env_rollout_ab_kernel<double, false>(...)",
+                        "Grid_Size": g, "Counter_Name": "FETCH_SIZE", "Counter_Value": v})
+        w.writerow({"Kernel_Name": "gemm_x6_ws_kernel", "Grid_Size": 999999,
+                    "Counter_Name": "FETCH_SIZE", "Counter_Value": 5.0})
+    mean, n = _traffic_update().avg(str(d), "FETCH_SIZE")
+    assert n == 2 and mean == 101.0
