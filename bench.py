@@ -796,6 +796,11 @@ def main():
                                "launch and env the f64 state read (124 B) and written (100 B) "
                                "once",
                 "avg_launch_us": round(per_launch_s * 1e6, 3),
+                # the same algorithmic bytes over the timed region's host wall
+                # (launch + synchronize included; the value's own clock)
+                "frac_wall": round(N * K * bpe / elapsed / 1e9 / HBM_PEAK_GBS, 4),
+                "rocprof_summary": "profiles/r04_kernel_stats.csv (the same kernel at K = 32 "
+                                   "in a bench run of K = 32 launches only)",
                 # the same launches (median of 5 untimed repetitions right
                 # before the timed one, after a warm-up) by their dispatch
                 # packets' own timestamps: the kernel alone, without the
