@@ -2,7 +2,7 @@
 replayed dr_step launches: env-steps/s and algorithmic GB/s per launch.
 
   python scripts/micro/rollout_bench.py [--envs 65536] [--reps 20]
-Rows per wave come from DRONERL_ROLLOUT_RPW (read per launch)."""
+The kernel form follows dr_rollout's launch rule (DRONERL_ROLLOUT_WS=0/1 forces it)."""
 import argparse
 import json
 import os
@@ -24,7 +24,7 @@ a = ap.parse_args()
 dev = torch.device("cuda", 0)
 dt = torch.float64 if a.dtype == "f64" else torch.float32
 sb = 8 if a.dtype == "f64" else 4
-res = {"rpw": os.environ.get("DRONERL_ROLLOUT_RPW", "64"),
+res = {"ws": os.environ.get("DRONERL_ROLLOUT_WS", "auto"),
        "dtype": a.dtype, "act_sets": a.act_sets}
 
 
