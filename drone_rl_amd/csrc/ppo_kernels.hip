@@ -866,15 +866,9 @@ struct LayerPair {
     float *h[2];
 };
 
-// 1: the input row through scalar loads (A/B knob, see the kernel body)
-#ifndef DR_LT_SCALAR
-#define DR_LT_SCALAR 1
-#endif
-// rows per wave and iteration of linear_tanh_kernel (A/B knob: 1 | 2; 2
-// measured 38.1 vs 37.6-37.8 us per call, scripts/micro/ppo_prof.sh)
-#ifndef DR_LT_RPI
-#define DR_LT_RPI 1
-#endif
+// (round 3 A/B, removed in round 4: two rows per wave and iteration measured
+// 38.1 vs 37.6-37.8 us per call; the input row through per-lane loads and
+// readlanes instead of scalar loads, slower)
 // diagnostic builds of linear_tanh_kernel (wrong by construction; timing
 // only, scripts/micro/ab_ppo_kern.sh): 1 = no tanh, 2 = no per-row store
 #ifndef DR_LT_ABL
@@ -921,55 +915,6 @@ __global__ __launch_bounds__(kBlock) void linear_tanh_kernel(int64_t m, int n,
             for (int k = 0; k < K; ++k) wr[q][k] = flat[q * K + k];
         }
     }
-#if DR_LT_SCALAR && DR_LT_RPI == 2
-    // two rows per iteration (r, r + stride): two independent FMA / tanh
-    // chains per wave and two stores in flight; the next pair's inputs are
-    // scalar-loaded before this pair's arithmetic
-    const int64_t stride = (int64_t)gridDim.x * 4;
-    int64_t r = (int64_t)blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(wid);
-    auto xrow = [&](int64_t q) -> int64_t { return rows ? (int64_t)rows[q] : q; };
-    float xn[2][K];
-#pragma unroll
-    for (int u = 0; u < 2; ++u) {
-        const int64_t ru = r + u * stride;
-        if (ru < m) {
-            const float *xr = x + xrow(ru) * K;
-#pragma unroll
-            for (int k = 0; k < K; ++k) xn[u][k] = xr[k];
-        }
-    }
-    for (; r < m; r += 2 * stride) {
-        float xv[2][K];
-#pragma unroll
-        for (int u = 0; u < 2; ++u)
-#pragma unroll
-            for (int k = 0; k < K; ++k) xv[u][k] = xn[u][k];
-#pragma unroll
-        for (int u = 0; u < 2; ++u) {
-            const int64_t rn = r + (2 + u) * stride;
-            if (rn < m) {
-                const float *xr = x + xrow(rn) * K;
-#pragma unroll
-                for (int k = 0; k < K; ++k) xn[u][k] = xr[k];
-            }
-        }
-        float acc[2][4] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
-#pragma unroll
-        for (int k = 0; k < K; ++k)
-#pragma unroll
-            for (int u = 0; u < 2; ++u)
-#pragma unroll
-                for (int q = 0; q < 4; ++q) acc[u][q] = fmaf(xv[u][k], wr[q][k], acc[u][q]);
-#pragma unroll
-        for (int u = 0; u < 2; ++u) {
-            const int64_t ru = r + u * stride;
-            if (act && ru < m)
-                st4(h + ru * n + c0,
-                    make_float4(tanh_fast(acc[u][0] + bb[0]), tanh_fast(acc[u][1] + bb[1]),
-                                tanh_fast(acc[u][2] + bb[2]), tanh_fast(acc[u][3] + bb[3])));
-        }
-    }
-#elif DR_LT_SCALAR
     // rows are wave-strided; row r is wave-uniform, so its K inputs are
     // scalar loads straight into SGPRs (no per-lane load + K readlanes), the
     // next row's issued before this row's arithmetic
@@ -1035,32 +980,6 @@ __global__ __launch_bounds__(kBlock) void linear_tanh_kernel(int64_t m, int n,
     }
 #if DR_LT_ABL == 2
     if (act && keep.x == 12345.f) st4(h + c0, keep);
-#endif
-#else
-    // rows are wave-strided; the next row's input is loaded before this
-    // row's arithmetic (software pipelining hides the load latency)
-    const int64_t stride = (int64_t)gridDim.x * 4;
-    int64_t r = (int64_t)blockIdx.x * 4 + wid;
-    // row r of the input is x[rows[r]] when a row index is given (a
-    // minibatch read in place from the rollout buffer), else x[r]
-    auto xrow = [&](int64_t q) -> int64_t { return rows ? (int64_t)rows[q] : q; };
-    float xnext = (r < m && lane < K) ? x[xrow(r) * K + lane] : 0.f;
-    for (; r < m; r += stride) {
-        const float xv = xnext;
-        const int64_t rn = r + stride;
-        xnext = (rn < m && lane < K) ? x[xrow(rn) * K + lane] : 0.f;
-        float acc[4] = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int k = 0; k < K; ++k) {
-            const float xk = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(xv), k));
-#pragma unroll
-            for (int q = 0; q < 4; ++q) acc[q] = fmaf(xk, wr[q][k], acc[q]);
-        }
-        if (act)
-            st4(h + r * n + c0,
-                make_float4(tanh_fast(acc[0] + bb[0]), tanh_fast(acc[1] + bb[1]),
-                            tanh_fast(acc[2] + bb[2]), tanh_fast(acc[3] + bb[3])));
-    }
 #endif
 }
 
@@ -1151,11 +1070,8 @@ constexpr int kHeadTile = DR_HEAD_TILE;
 #ifndef DR_HEAD_DIAG
 #define DR_HEAD_DIAG 0
 #endif
-// A/B knob: 1 = the next tile's activation rows are loaded while this
-// tile computes (software pipelining, +16 VGPRs per wave)
-#ifndef DR_HEAD_PF
-#define DR_HEAD_PF 0
-#endif
+// (round 3 A/B, removed in round 4: the next tile's activation rows loaded
+// while this tile computes, +16 VGPRs per wave, slower)
 
 // policy waves: accumulate u[0], u[2..7] (loss terms), u[9..12] (d b_act),
 // and per lane d b_pi (4 columns) and d W_act (4 x 4)
@@ -1170,30 +1086,13 @@ __device__ inline void head_policy_wave(const HeadArgs &a, const RowLossConst &c
     for (int j = 0; j < 4; ++j) wa[j] = act ? ld4(a.w_act + j * hd + c0) : z4;
     const float4 zb = (act && a.zb_pi) ? ld4(a.zb_pi + c0) : z4;
     const float ba[4] = {a.b_act[0], a.b_act[1], a.b_act[2], a.b_act[3]};
-#if DR_HEAD_PF
-    float4 hn[kHeadTile];
-    auto load_h = [&](int64_t tile, float4 *dst) {
-        const int64_t r0 = tile * kHeadTile;
-        const int nr = (int)min((int64_t)kHeadTile, a.m - r0);
-#pragma unroll
-        for (int i = 0; i < kHeadTile; ++i)
-            dst[i] = (act && i < nr) ? ld4(a.h_pi + (r0 + i) * hd + c0) : z4;
-    };
-    if (tile0 * kHeadTile < a.m) load_h(tile0, hn);
-#endif
     for (int64_t tile = tile0; tile * kHeadTile < a.m; tile += tstride) {
         const int64_t r0 = tile * kHeadTile;
         const int nr = (int)min((int64_t)kHeadTile, a.m - r0);
         float4 h[kHeadTile];
-#if DR_HEAD_PF
-#pragma unroll
-        for (int i = 0; i < kHeadTile; ++i) h[i] = hn[i];
-        if ((tile + tstride) * kHeadTile < a.m) load_h(tile + tstride, hn);
-#else
 #pragma unroll
         for (int i = 0; i < kHeadTile; ++i)
             h[i] = (act && i < nr) ? ld4(a.h_pi + (r0 + i) * hd + c0) : z4;
-#endif
         // this lane's row (lane < nr): its loss inputs, loaded while the dots run
         const bool own = lane < nr;
         const int64_t rr = r0 + (own ? lane : 0);
@@ -1267,30 +1166,13 @@ __device__ inline void head_value_wave(const HeadArgs &a, const RowLossConst &c,
     const float4 zb = (act && a.zb_vf) ? ld4(a.zb_vf + c0) : z4;
     const float bv = a.b_val[0];
     const float wvq[4] = {wv.x, wv.y, wv.z, wv.w};
-#if DR_HEAD_PF
-    float4 hn[kHeadTile];
-    auto load_h = [&](int64_t tile, float4 *dst) {
-        const int64_t r0 = tile * kHeadTile;
-        const int nr = (int)min((int64_t)kHeadTile, a.m - r0);
-#pragma unroll
-        for (int i = 0; i < kHeadTile; ++i)
-            dst[i] = (act && i < nr) ? ld4(a.h_vf + (r0 + i) * hd + c0) : z4;
-    };
-    if (tile0 * kHeadTile < a.m) load_h(tile0, hn);
-#endif
     for (int64_t tile = tile0; tile * kHeadTile < a.m; tile += tstride) {
         const int64_t r0 = tile * kHeadTile;
         const int nr = (int)min((int64_t)kHeadTile, a.m - r0);
         float4 h[kHeadTile];
-#if DR_HEAD_PF
-#pragma unroll
-        for (int i = 0; i < kHeadTile; ++i) h[i] = hn[i];
-        if ((tile + tstride) * kHeadTile < a.m) load_h(tile + tstride, hn);
-#else
 #pragma unroll
         for (int i = 0; i < kHeadTile; ++i)
             h[i] = (act && i < nr) ? ld4(a.h_vf + (r0 + i) * hd + c0) : z4;
-#endif
         const bool own = lane < nr;
         const int64_t rr = r0 + (own ? lane : 0);
         const int64_t ro = a.rows ? (int64_t)a.rows[rr] : rr;
@@ -1393,22 +1275,16 @@ __global__ __launch_bounds__(kBlock) void ppo_head_kernel(HeadArgs a) {
 // Replaces tanh_backward (write of grad_z) + the split-K weight-gradient
 // GEMM (re-read of grad_z).  Tiles of kFirstTile rows per wave, loads first.
 // Partial layout per block (P = (K+1) n): [k*n + c] = dW[c][k], [K*n + c] = db[c].
-// A/B build knobs of first_layer_bwd_kernel: rows per tile, next-tile
-// prefetch, a two-slot LDS reduction, and the cap on blocks per net
-// (scripts/micro/ab_ppo_kern.sh).  4-row tiles fit 115 VGPRs and the two-slot
-// reduction 32 KB of LDS, so 4 waves per SIMD are resident: 59.0 -> 56.3 us
-// per minibatch against 8-row tiles / four slots (152 VGPRs, 64 KB, 2 waves);
-// the prefetch needs 203 VGPRs and is slower (64.7 us).
+// A/B build knobs of first_layer_bwd_kernel: rows per tile and the cap on
+// blocks per net (scripts/micro/ab_ppo_kern.sh).  4-row tiles fit 115 VGPRs
+// and a two-slot LDS reduction 32 KB, so 4 waves per SIMD are resident: 59.0
+// -> 56.3 us per minibatch against 8-row tiles / four slots (152 VGPRs, 64
+// KB, 2 waves); a next-tile prefetch needed 203 VGPRs and was slower (64.7
+// us; removed in round 4 with the four-slot form).
 #ifndef DR_FL_TILE
 #define DR_FL_TILE 4
 #endif
 constexpr int kFirstTile = DR_FL_TILE;
-#ifndef DR_FL_PF
-#define DR_FL_PF 0
-#endif
-#ifndef DR_FL_LDS2
-#define DR_FL_LDS2 1
-#endif
 // 256 blocks per net (round 3): 52.5-53.2 vs 54.2-54.7 us per minibatch at
 // 512 (scripts/micro/round3_z.sh), fewer partials for the deferred finish
 #ifndef DR_FL_MAXB
@@ -1475,41 +1351,14 @@ __global__ __launch_bounds__(kBlock) void first_layer_bwd_kernel(int64_t m, int 
             }
         }
     };
-#if DR_FL_PF
-    // software-pipelined: the next tile's loads are in flight while this
-    // tile's FMAs run (rows past the end load nothing and add zeros)
-    int64_t tile = (int64_t)blockIdx.x * 4 + wid;
-    if (tile * kFirstTile < m) {
-        float4 g[kFirstTile], y[kFirstTile];
-        float xv[kFirstTile];
-        load_tile(tile, g, y, xv);
-        for (; tile * kFirstTile < m; tile += nwaves) {
-            float4 g2[kFirstTile], y2[kFirstTile];
-            float xv2[kFirstTile];
-            const bool more = (tile + nwaves) * kFirstTile < m;
-            if (more) load_tile(tile + nwaves, g2, y2, xv2);
-            use_tile(g, y, xv);
-            if (more) {
-#pragma unroll
-                for (int i = 0; i < kFirstTile; ++i) {
-                    g[i] = g2[i];
-                    y[i] = y2[i];
-                    xv[i] = xv2[i];
-                }
-            }
-        }
-    }
-#else
     for (int64_t tile = (int64_t)blockIdx.x * 4 + wid; tile * kFirstTile < m; tile += nwaves) {
         float4 g[kFirstTile], y[kFirstTile];
         float xv[kFirstTile];
         load_tile(tile, g, y, xv);
         use_tile(g, y, xv);
     }
-#endif
     const int P = (K + 1) * n;
     float *__restrict__ out = part + ((int64_t)blockIdx.x * gridDim.y + blockIdx.y) * P;
-#if DR_FL_LDS2
     // two slots of P: waves 2 / 3 park their partials, waves 0 / 1 fold theirs
     // in, then the two slots are summed (half the LDS of four slots, so the
     // LDS no longer caps the CU at two blocks)
@@ -1533,20 +1382,6 @@ __global__ __launch_bounds__(kBlock) void first_layer_bwd_kernel(int64_t m, int 
     }
     __syncthreads();
     for (int p = threadIdx.x; p < P; p += kBlock) out[p] = sh_fl[p] + sh_fl[P + p];
-#else
-    float *mine = sh_fl + wid * P;
-    if (act) {
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-#pragma unroll
-            for (int k = 0; k < K; ++k) mine[k * n + c0 + q] = aw[k][q];
-            mine[K * n + c0 + q] = ab[q];
-        }
-    }
-    __syncthreads();
-    for (int p = threadIdx.x; p < P; p += kBlock)
-        out[p] = ((sh_fl[p] + sh_fl[P + p]) + sh_fl[2 * P + p]) + sh_fl[3 * P + p];
-#endif
 }
 
 // Sum of the grouped partials (ng rows of nets * P) scattered to d W (n,K)
@@ -2446,7 +2281,7 @@ static int launch_first_bwd(const char *who, int nets, int64_t m, int64_t k, int
     float *part2 = reinterpret_cast<float *>(static_cast<char *>(workspace) +
                                              align_up(sizeof(float) * (size_t)(nb * P)));
     hipStream_t st = as_stream(stream);
-    const size_t lds = sizeof(float) * (DR_FL_LDS2 ? 2 : 4) * P1;
+    const size_t lds = sizeof(float) * 2 * P1;
     switch (k) {
 #define DR_FL_CASE(K)                                                                      \
     case K:                                                                                \
