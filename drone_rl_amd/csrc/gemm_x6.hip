@@ -484,9 +484,10 @@ __global__ __launch_bounds__(WS_THREADS, 1) void gemm_x6_ws_kernel(
 // into LDS; the fragments come back column-major through gfx950's
 // transposing read ds_read_b64_tr_b16 (two per fragment).  Per wave and
 // stage: 24 split elements (~130 VALU), 18 ds_write_b64, 48 transposed
-// reads, 48 MFMAs, one barrier.  Bitwise round 3's partials (same splits,
-// products and per-output order); 110-111 vs 119-124 us for both nets at
-// 65,536 rows, 64 chunks (scripts/micro/wgrad_ab.py, same box).
+// reads, 48 MFMAs, one barrier (mid-stage, see the loop).  Bitwise round 3's
+// partials (same splits, products and per-output order); 110-111 vs 119-124
+// us for both nets at 65,536 rows, 64 chunks (scripts/micro/wgrad_ab.py, same
+// box), 101.5-103.5 vs 105.5-109.0 with the barrier moved mid-stage.
 //
 // DR_WG_STAMPS (diagnostic builds only): s_memtime at five points of every
 // stage for the waves of blocks 0-7 (read back by dr_x6_diag_wg_stamps,
@@ -599,58 +600,66 @@ __global__ __launch_bounds__(XTHREADS) void gemm_x6_wgrad_kernel(
             acc_l[i][j] = (f32x16_t){};
         }
 
+    auto frag_addr = [&](int g, int s) { return sh + (g & 1) * TW_STAGE + fbase + 16 * s * TW_ROW; };
+    auto read_step = [&](int g, int s, bf16x8_t (&fg)[2][3], bf16x8_t (&fhp)[2][3]) {
+        const uint8_t *S = frag_addr(g, s);
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int p = 0; p < 3; ++p) {
+                const uint8_t *q = S + p * TW_PLANE_ROW;
+                fg[i][p] = tr_frag(q + gcol + 64 * i);
+                fhp[i][p] = tr_frag(q + hcol + 64 * i);
+            }
+    };
+    auto mfma_step = [&](const bf16x8_t (&fg)[2][3], const bf16x8_t (&fhp)[2][3]) {
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                const bf16x8_t *a = fg[i], *c = fhp[j];
+                acc_h[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], c[0], acc_h[i][j],
+                                                                      0, 0, 0);
+                f32x16_t t = acc_l[i][j];
+                t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], c[1], t, 0, 0, 0);
+                t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], c[0], t, 0, 0, 0);
+                t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], c[2], t, 0, 0, 0);
+                t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[2], c[0], t, 0, 0, 0);
+                t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], c[1], t, 0, 0, 0);
+                acc_l[i][j] = t;
+            }
+    };
+
     load(0);
     split_store(0);
     load(G_ > 1 ? 1 : 0);
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    // Stage g, per wave: (its first k16 step's fragments were read in stage
+    // g - 1) read the second k16 step's; the first k16 step's 24 MFMAs; the
+    // split of stage g + 1 into the other buffer; lgkmcnt(0) + barrier
+    // (publishes stage g + 1); read stage g + 1's
+    // first-step fragments; the second k16 step's 24 MFMAs; the loads of stage
+    // g + 2 (consumed by the next stage's split).  The barrier sits
+    // mid-stage, so the next stage's first reads hide behind MFMAs instead of
+    // all 48 reads of every wave queueing on the LDS right after it.  Stage
+    // g's buffer is rewritten only in stage g + 1, after this stage's
+    // barrier, by when every read of it has completed (lgkmcnt(0)).  The last
+    // iteration re-splits and re-reads the last stage (no branch).
+    bf16x8_t f0g[2][3], f0h[2][3], f1g[2][3], f1h[2][3];
+    read_step(0, 0, f0g, f0h);
     for (int g = 0; g < G_; ++g) {
         WG_STAMP(g, 0);
-        const uint8_t *S = sh + (g & 1) * TW_STAGE + fbase;
-        bf16x8_t fg[2][2][3], fhp[2][2][3];               // [k16 step][tile][plane]
-        auto read_step = [&](int s) {
-#pragma unroll
-            for (int i = 0; i < 2; ++i)
-#pragma unroll
-                for (int p = 0; p < 3; ++p) {
-                    const uint8_t *q = S + 16 * s * TW_ROW + p * TW_PLANE_ROW;
-                    fg[s][i][p] = tr_frag(q + gcol + 64 * i);
-                    fhp[s][i][p] = tr_frag(q + hcol + 64 * i);
-                }
-        };
-        // the split of stage g + 1 (loaded one stage ago) into the other
-        // buffer sits between the two k16 steps' MFMAs (the last iteration
-        // re-splits the last stage into the unused buffer: no branch in the
-        // loop).  After both k16 steps, before the fragment reads, or with
-        // each k16 step's reads in front of its MFMAs measured the same.
-        read_step(0);
-        read_step(1);
+        read_step(g, 1, f1g, f1h);
         WG_STAMP(g, 1);
-#pragma unroll
-        for (int s = 0; s < 2; ++s) {
-#pragma unroll
-            for (int i = 0; i < 2; ++i)
-#pragma unroll
-                for (int j = 0; j < 2; ++j) {
-                    const bf16x8_t *a = fg[s][i], *c = fhp[s][j];
-                    acc_h[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], c[0], acc_h[i][j],
-                                                                          0, 0, 0);
-                    f32x16_t t = acc_l[i][j];
-                    t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], c[1], t, 0, 0, 0);
-                    t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], c[0], t, 0, 0, 0);
-                    t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], c[2], t, 0, 0, 0);
-                    t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[2], c[0], t, 0, 0, 0);
-                    t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], c[1], t, 0, 0, 0);
-                    acc_l[i][j] = t;
-                }
-            if (s == 0) {
-                WG_STAMP(g, 2);
-                split_store((g + 1) & 1);
-                WG_STAMP(g, 3);
-            }
-        }
-        WG_STAMP(g, 4);
-        load(g + 2 < G_ ? g + 2 : G_ - 1);
+        mfma_step(f0g, f0h);
+        WG_STAMP(g, 2);
+        split_store((g + 1) & 1);
+        WG_STAMP(g, 3);
         asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        read_step(g + 1 < G_ ? g + 1 : g, 0, f0g, f0h);
+        WG_STAMP(g, 4);
+        mfma_step(f1g, f1h);
+        load(g + 2 < G_ ? g + 2 : G_ - 1);
         WG_STAMP(g, 5);
     }
     // D[n][k]: column k = fr, row n = (r & 3) + 8 (r >> 2) + 4 fh

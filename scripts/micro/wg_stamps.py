@@ -1,10 +1,10 @@
 """Stage timeline of gemm_x6_wgrad_kernel from a DR_WG_STAMPS=1 build
 (s_memtime = shader clock), blocks 0-7, waves 0-7, stages 0-23:
-  reads  = loop top -> the stage's 48 transposed fragment reads issued
+  reads  = loop top -> the second k16 step's 24 transposed reads issued
   mfma0  = k16 step 0's 24 MFMAs (and the wait for their fragments)
   split  = the next stage's split + plane writes
-  mfma1  = k16 step 1's 24 MFMAs
-  bar    = next stage's loads + lgkmcnt(0) + barrier
+  bar    = lgkmcnt(0) + barrier + the next stage's first-step reads issued
+  mfma1  = k16 step 1's 24 MFMAs + the loads of stage g + 2
 Usage: python scripts/micro/wg_stamps.py path/to/lib.so"""
 import ctypes
 import os
@@ -36,8 +36,8 @@ assert L.dr_x6_diag_wg_stamps(buf.ctypes.data, buf.nbytes) == 0
 st = buf.reshape(8, 8, 24, 8).astype(np.int64)
 R = 24
 d = {"reads": st[..., 1] - st[..., 0], "mfma0": st[..., 2] - st[..., 1],
-     "split": st[..., 3] - st[..., 2], "mfma1": st[..., 4] - st[..., 3],
-     "bar": st[..., 5] - st[..., 4]}
+     "split": st[..., 3] - st[..., 2], "bar": st[..., 4] - st[..., 3],
+     "mfma1": st[..., 5] - st[..., 4]}
 for k, v in d.items():
     v = v[:, :, 1:R]
     print(f"{k:6s} median {np.median(v):6.0f}  p10 {np.percentile(v, 10):6.0f}  "
