@@ -1,7 +1,7 @@
 """dr_gemm_x6_wgrad at the trainer's shape (2 nets, 65,536 rows, 64 chunks):
 time per launch (median of 5 event-timed batches) and the SHA-256 of the
-partials, for an A/B of kernel forms run in separate processes
-(DRONERL_WGRAD_TR=0/1).
+partials, for an A/B of library builds run in separate processes
+(DRONERL_LIB=...).
 
   python scripts/micro/wgrad_ab.py [--m 65536] [--chunks 64] [--reps 50]
 """
@@ -47,5 +47,6 @@ for _ in range(5):
     torch.cuda.synchronize()
     ts.append(st.elapsed_time(en) * 1e3 / a.reps)
 ts.sort()
-print(json.dumps({"form": os.environ.get("DRONERL_WGRAD_TR", "default"), "us": round(ts[2], 2),
+print(json.dumps({"lib": os.path.basename(os.path.dirname(_lib.LIB_PATH)) + "/" +
+                  os.path.basename(_lib.LIB_PATH), "us": round(ts[2], 2),
                   "us_min": round(ts[0], 2), "sha": sha, "rel_err": err}))
