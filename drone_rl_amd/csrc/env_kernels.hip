@@ -130,45 +130,50 @@ __device__ inline void st_out(T *p, T x) {
     if (DR_NT_STORES) store_nt(p, x);
     else *p = x;
 }
-// The three Euler angles at once: the fast path runs unconditionally for
-// all three (independent chains interleave; the polynomial constants are
-// materialised once), the library path only for out-of-range lanes.
-template <typename S>
-__device__ inline void m_sincos3(const S x[3], S s[3], S c[3]) {
+// N of the Euler angles at once: the fast path runs unconditionally for
+// all N (independent chains interleave; the polynomial constants are
+// materialised once), the library path only for out-of-range lanes.  Each
+// angle's result depends on that angle alone.
+template <int N, typename S>
+__device__ inline void m_sincos_n(const S *x, S *s, S *c) {
     if constexpr (sizeof(S) == 8) {
         // trig.h: 3-FMA reduction + shared polynomials (<= 1 ulp); the
         // library sincos only for |x| >= 2^19 rad, inf and NaN (a branch no
         // lane usually takes)
+        int fast = 1;
 #pragma unroll
-        for (int k = 0; k < 3; ++k) {
+        for (int k = 0; k < N; ++k) {
             const SinCos t = sincos_medium(x[k]);
             s[k] = t.s;
             c[k] = t.c;
+            fast &= (int)sincos_fast_range(x[k]);
         }
-        const bool fast = (int)sincos_fast_range(x[0]) & (int)sincos_fast_range(x[1]) &
-                          (int)sincos_fast_range(x[2]);
         if (!fast) {
 #pragma unroll
-            for (int k = 0; k < 3; ++k)
+            for (int k = 0; k < N; ++k)
                 if (!sincos_fast_range(x[k])) sincos(x[k], &s[k], &c[k]);
         }
     } else {
         // f32 state mode: trig.h's sincosf_medium (f64 reduction, f32
         // polynomials, <= 2 ulp); the library sincosf only out of range
+        int fast = 1;
 #pragma unroll
-        for (int k = 0; k < 3; ++k) {
+        for (int k = 0; k < N; ++k) {
             const SinCosF t = sincosf_medium(x[k]);
             s[k] = t.s;
             c[k] = t.c;
+            fast &= (int)sincosf_fast_range(x[k]);
         }
-        const bool fast = (int)sincosf_fast_range(x[0]) & (int)sincosf_fast_range(x[1]) &
-                          (int)sincosf_fast_range(x[2]);
         if (!fast) {
 #pragma unroll
-            for (int k = 0; k < 3; ++k)
+            for (int k = 0; k < N; ++k)
                 if (!sincosf_fast_range(x[k])) sincosf(x[k], &s[k], &c[k]);
         }
     }
+}
+template <typename S>
+__device__ inline void m_sincos3(const S x[3], S s[3], S c[3]) {
+    m_sincos_n<3>(x, s, c);
 }
 __device__ inline double m_sqrt(double x) { return sqrt(x); }
 __device__ inline float m_sqrt(float x) { return sqrtf(x); }
@@ -1378,24 +1383,30 @@ __global__ __launch_bounds__(kWsThreads) void env_rollout_ws_kernel(EnvView<S> v
 // SIMD left the VALU idle about half of its cycles (two physics waves per
 // SIMD were measured to hide 24 % per env):
 //   * the TRANSLATION wave (waves 0-3) owns pos / vel / target, the step
-//     counter, the curriculum and the reset draws: R's column 2 from the
-//     step's Euler sincos, acceleration, velocity, position, reward, crash,
-//     done, the reset, and the obs fields pos / vel / target - pos;
+//     counter, the curriculum and the reset draws: the yaw's sincos, R's
+//     column 2 from the step's Euler sincos, acceleration, velocity,
+//     position, reward, crash, done, the reset, and the obs fields pos / vel
+//     / target - pos;
 //   * the ROTATION wave (waves 4-7) owns the Euler angles and body rates:
-//     their sincos, the Euler rates and the angular update, and the obs
-//     fields euler / omega;
+//     the roll and pitch sincos, the Euler rates and the angular update, and
+//     the obs fields euler / omega;
 //   * the MEMORY waves (8-11) load actions and stream outputs as in the
 //     warp-specialised kernel.
 // Wave p, p + 4 and p + 8 share SIMD p.  The two halves of a step touch
-// disjoint state; what crosses is the sincos of the step's angles (rotation ->
-// translation, computed one step ahead from the updated angles, through a
-// double-buffered LDS slot) and the done flag (translation -> rotation, read
-// one phase later: a reset zeroes the angles and rates before the next step,
-// and their sincos is then exactly (+0, 1), which both waves substitute).  The
-// rotation wave therefore writes step t's euler / omega obs fields in phase
-// t + 1, and the memory waves store step t's outputs in phase t + 2 from
-// three output slots.  Every expression is physics_step_mixed's, in its
-// order: outputs bitwise those of the other kernels (tests/test_rollout_gpu.py).
+// disjoint state; what crosses is the roll / pitch sincos and the yaw
+// (rotation -> translation, formed one step ahead from the updated angles,
+// through a double-buffered LDS slot) and the done flag (translation ->
+// rotation, read one phase later: a reset zeroes the angles and rates before
+// the next step, and their sincos is then exactly (+0, 1), which both waves
+// substitute).  The rotation wave therefore writes step t's euler / omega
+// obs fields in phase t + 1, and the memory waves store step t's outputs in
+// phase t + 2 from three output slots.  Every expression is
+// physics_step_mixed's, in its order: outputs bitwise those of the other
+// kernels (tests/test_rollout_gpu.py).  Each angle's sincos depends on that
+// angle alone, so the yaw's moving waves changes no bit: 41.6-43.3 vs
+// 42.6-44.7 us per 32-step launch (round 4, alternating on one box; without
+// the rotation wave's sincos altogether, a wrong-result diagnostic build,
+// 33.3-34.4 us: that sincos was the launch's critical path).
 // ----------------------------------------------------------------------------
 // The translation wave stages the squared target distance and the memory
 // wave forms the reward from it (the same sqrt and reward arithmetic, off the
@@ -1410,7 +1421,8 @@ struct AbLds {
     S d2[kAbOut][kWsEnvs];                // squared target distance
     uint8_t done[kAbOut][kWsEnvs];
     float4 act[kWsNA][kWsEnvs];
-    S sc[2][6][kWsEnvs];                  // sin phi, theta, psi, cos phi, theta, psi
+    S sc[2][4][kWsEnvs];                  // sin phi, theta, cos phi, theta
+    S psi[2][kWsEnvs];                    // the yaw itself
 };
 
 template <typename S, bool GEN>
@@ -1530,12 +1542,13 @@ __global__ __launch_bounds__(kAbThreads) void env_rollout_ab_kernel(EnvView<S> v
             omg[k] = *at(fp.p[F_OMG + k], i);
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        S sn[3], cs[3];
-        m_sincos3(eul, sn, cs);
+        S sn[2], cs[2];
+        m_sincos_n<2>(eul, sn, cs);
+        sh.psi[0][ps] = eul[2];
 #pragma unroll
-        for (int k = 0; k < 3; ++k) {
+        for (int k = 0; k < 2; ++k) {
             sh.sc[0][k][ps] = sn[k];
-            sh.sc[0][3 + k][ps] = cs[k];
+            sh.sc[0][2 + k][ps] = cs[k];
         }
         asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");   // B_(-1)
         // the reset of step t - 1 (done flag staged by the translation wave
@@ -1547,6 +1560,9 @@ __global__ __launch_bounds__(kAbThreads) void env_rollout_ab_kernel(EnvView<S> v
                 for (int k = 0; k < 3; ++k) {
                     eul[k] = (S)0;
                     omg[k] = (S)0;
+                }
+#pragma unroll
+                for (int k = 0; k < 2; ++k) {
                     sn[k] = (S)0;      // sincos(+0) = (+0, 1) exactly
                     cs[k] = (S)1;
                 }
@@ -1584,13 +1600,14 @@ __global__ __launch_bounds__(kAbThreads) void env_rollout_ab_kernel(EnvView<S> v
             omg[2] += wd2 * v.dt;
             // the next step's sincos (of the angles before any reset of this
             // step: the translation wave substitutes (+0, 1) after one)
-            m_sincos3(eul, sn, cs);
+            m_sincos_n<2>(eul, sn, cs);
             if (t + 1 < K) {
 #pragma unroll
-                for (int k = 0; k < 3; ++k) {
+                for (int k = 0; k < 2; ++k) {
                     sh.sc[(t + 1) & 1][k][ps] = sn[k];
-                    sh.sc[(t + 1) & 1][3 + k][ps] = cs[k];
+                    sh.sc[(t + 1) & 1][2 + k][ps] = cs[k];
                 }
+                sh.psi[(t + 1) & 1][ps] = eul[2];
             }
             __builtin_amdgcn_sched_barrier(0);
             asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");   // B_t
@@ -1630,11 +1647,15 @@ __global__ __launch_bounds__(kAbThreads) void env_rollout_ab_kernel(EnvView<S> v
     for (int t = 0; t < K; ++t) {
         asm volatile("" : "+s"(vk.seed_lo), "+s"(vk.seed_hi));
         const float4 a_cur = sh.act[t % kWsNA][ps];
+        // the yaw's sincos here (only R's column 2 needs it), the roll and
+        // pitch's from the rotation wave
         S sn[3], cs[3];
+        const S psi = sh.psi[t & 1][ps];
+        m_sincos_n<1>(&psi, &sn[2], &cs[2]);
 #pragma unroll
         for (int k = 0; k < 3; ++k) {
-            sn[k] = prev_rs ? (S)0 : sh.sc[t & 1][k][ps];
-            cs[k] = prev_rs ? (S)1 : sh.sc[t & 1][3 + k][ps];
+            sn[k] = prev_rs ? (S)0 : (k < 2 ? sh.sc[t & 1][k][ps] : sn[k]);
+            cs[k] = prev_rs ? (S)1 : (k < 2 ? sh.sc[t & 1][2 + k][ps] : cs[k]);
         }
         const MotorMix mx = motor_mix(a_cur);
         if (t % kResetAhead == 0 && !nd_ok) {
