@@ -106,6 +106,10 @@ def parse():
     ap.add_argument("--kernel-stats",
                     default=os.path.join(ROOT, "profiles", "r04_kernel_stats.csv"),
                     help="rocprofv3 --stats csv whose kernel averages the ppo block reports")
+    ap.add_argument("--rollout-grid-stats",
+                    default=os.path.join(ROOT, "profiles", "r04_rollout_grid_stats.json"),
+                    help="scripts/kernel_grid_stats.py output: the headline kernel's rocprof "
+                         "durations at K = 32 on 65,536 envs")
     ap.add_argument("--headline", choices=["rollout", "step"], default="rollout",
                     help="kernel of the headline value: the K-step rollout kernel or one "
                          "dr_step launch per step")
@@ -521,6 +525,28 @@ PPO_KERNEL_NAMES = {"gather_minibatch": "gather_minibatch_kernel",
                     "gemm_x6_wgrad": "gemm_x6_wgrad_kernel", "split_weights": "split_weights_kernel"}
 
 
+def rollout_rocprof_k32(path, n, state_dtype):
+    """The split-physics rollout kernel's rocprofv3 durations at its largest
+    grid (65,536 f64 envs, K = 32 launches only: scripts/micro/r4p3.sh's run,
+    split by grid by scripts/kernel_grid_stats.py), with the HBM fraction of
+    a K = 32 launch's algorithmic bytes; None when absent or for another
+    configuration."""
+    if n != 65536 or state_dtype != "f64":
+        return None
+    try:
+        rows = [r for r in json.load(open(path)) if "env_rollout_ab_kernel<double" in r["kernel"]]
+    except (OSError, ValueError, KeyError, TypeError):
+        return None
+    if not rows:
+        return None
+    r = max(rows, key=lambda r: r["grid"])
+    byt = n * (32 * 81 + 224)
+    return {"dispatches": r["dispatches"], "mean_us": r["mean_us"], "median_us": r["median_us"],
+            "min_us": r["min_us"], "max_us": r["max_us"],
+            "frac": round(byt / (r["mean_us"] * 1e-6) / 1e9 / HBM_PEAK_GBS, 4),
+            "source": os.path.relpath(path, ROOT)}
+
+
 def rocprof_averages(path):
     """{kernel name: average us} from a committed rocprofv3 --stats csv
     (profiles/r04_kernel_stats.csv: scripts/micro/r4p3.sh's run of this
@@ -799,8 +825,10 @@ def main():
                 # the same algorithmic bytes over the timed region's host wall
                 # (launch + synchronize included; the value's own clock)
                 "frac_wall": round(N * K * bpe / elapsed / 1e9 / HBM_PEAK_GBS, 4),
-                "rocprof_summary": "profiles/r04_kernel_stats.csv (the same kernel at K = 32 "
-                                   "in a bench run of K = 32 launches only)",
+                # the same kernel's own rocprofv3 durations, K = 32 launches
+                # on 65,536 envs (the host-floor probe's 64-env launches of it
+                # split off by grid)
+                "rocprof_k32": rollout_rocprof_k32(args.rollout_grid_stats, N, args.state_dtype),
                 # the same launches (median of 5 untimed repetitions right
                 # before the timed one, after a warm-up) by their dispatch
                 # packets' own timestamps: the kernel alone, without the

@@ -3,6 +3,7 @@ kernel stats feed the ppo roofline's in-step kernel durations, and the PMC
 traffic reduction keeps only the headline-sized dispatches (bench.py's
 host-floor probe launches the same rollout kernel on 64 envs)."""
 import csv
+import json
 import importlib.util
 import os
 import sys
@@ -57,3 +58,34 @@ def test_traffic_average_keeps_the_largest_grid(tmp_path):
                     "Counter_Name": "FETCH_SIZE", "Counter_Value": 5.0})
     mean, n = _traffic_update().avg(str(d), "FETCH_SIZE")
     assert n == 2 and mean == 101.0
+
+
+def _grid_stats():
+    spec = importlib.util.spec_from_file_location(
+        "kernel_grid_stats", os.path.join(ROOT, "scripts", "kernel_grid_stats.py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod
+
+
+def test_grid_stats_split_the_probe_from_the_headline_launches(tmp_path):
+    p = tmp_path / "run_kernel_trace.csv"
+    name = "void dr::env_rollout_ab_kernel<double, false>(...)"
+    with open(p, "w", newline="") as f:
+        w = csv.DictWriter(f, ["Kernel_Name", "Grid_Size_X", "Grid_Size_Y", "Grid_Size_Z",
+                               "Start_Timestamp", "End_Timestamp"])
+        w.writeheader()
+        for g, us in ((196608, 42.0), (196608, 44.0), (196608, 43.0), (768, 4.0), (768, 4.5)):
+            w.writerow({"Kernel_Name": name, "Grid_Size_X": g, "Grid_Size_Y": 1,
+                        "Grid_Size_Z": 1, "Start_Timestamp": 1000,
+                        "End_Timestamp": 1000 + int(us * 1000)})
+    rows = _grid_stats().summarise(str(p), ("env_rollout_ab_kernel",))
+    assert [(r["grid"], r["dispatches"]) for r in rows] == [(196608, 3), (768, 2)]
+    assert rows[0]["mean_us"] == 43.0 and rows[0]["median_us"] == 43.0
+    out = tmp_path / "g.json"
+    out.write_text(json.dumps(rows))
+    k = bench.rollout_rocprof_k32(str(out), 65536, "f64")
+    assert k["dispatches"] == 3 and k["mean_us"] == 43.0
+    assert abs(k["frac"] - 65536 * (32 * 81 + 224) / 43e-6 / 8e12) < 1e-3
+    assert bench.rollout_rocprof_k32(str(out), 4096, "f64") is None
+    assert bench.rollout_rocprof_k32(str(tmp_path / "none.json"), 65536, "f64") is None
