@@ -870,7 +870,9 @@ struct LayerPair {
 // 38.1 vs 37.6-37.8 us per call; the input row through per-lane loads and
 // readlanes instead of scalar loads, slower)
 // diagnostic builds of linear_tanh_kernel (wrong by construction; timing
-// only, scripts/micro/ab_ppo_kern.sh): 1 = no tanh, 2 = no per-row store
+// only, scripts/micro/ab_ppo_kern.sh, scripts/micro/lt_ab.py): 1 = no tanh,
+// 2 = no per-row store, 3 = no input loads, 4 = no input loads and no
+// arithmetic (the row stores alone), 5 = no weight loads
 #ifndef DR_LT_ABL
 #define DR_LT_ABL 0
 #endif
@@ -902,7 +904,8 @@ __global__ __launch_bounds__(kBlock) void linear_tanh_kernel(int64_t m, int n,
         float flat[4 * K];
 #pragma unroll
         for (int t = 0; t < K; ++t) {
-            const float4 v4 = w4[t];
+            const float4 v4 = DR_LT_ABL == 5 ? make_float4(0.01f * t, 0.02f, 0.03f, 0.04f * c0)
+                                             : w4[t];
             flat[4 * t + 0] = v4.x;
             flat[4 * t + 1] = v4.y;
             flat[4 * t + 2] = v4.z;
@@ -925,7 +928,7 @@ __global__ __launch_bounds__(kBlock) void linear_tanh_kernel(int64_t m, int n,
     if (r < m) {
         const float *xr = x + xrow(r) * K;
 #pragma unroll
-        for (int k = 0; k < K; ++k) xn[k] = xr[k];
+        for (int k = 0; k < K; ++k) xn[k] = DR_LT_ABL >= 3 ? 0.1f * (float)k : xr[k];
     }
 #if DR_LT_ABL == 2
     float4 keep = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -938,8 +941,13 @@ __global__ __launch_bounds__(kBlock) void linear_tanh_kernel(int64_t m, int n,
         if (rn < m) {
             const float *xr = x + xrow(rn) * K;
 #pragma unroll
-            for (int k = 0; k < K; ++k) xn[k] = xr[k];
+            for (int k = 0; k < K; ++k)
+                xn[k] = DR_LT_ABL >= 3 ? xv[k] + 1e-3f * (float)(rn & 7) : xr[k];
         }
+#if DR_LT_ABL == 4      // diagnostic: the row stores alone
+        if (act) st4(h + r * n + c0, make_float4(xv[0], xv[1], xv[2], xv[3]));
+        continue;
+#endif
 #if DR_TANH_RAT
         // the same fmaf chain per column, written as packed pairs (columns
         // 0-1, 2-3), and the pairs' rational tanh
@@ -951,9 +959,17 @@ __global__ __launch_bounds__(kBlock) void linear_tanh_kernel(int64_t m, int n,
             a23 = pk_fma(xk, f32x2{wr[2][k], wr[3][k]}, a23);
         }
         if (act) {
+#if DR_LT_ABL == 1      // diagnostic: no tanh
+            const f32x2 t01 = a01 + f32x2{bb[0], bb[1]}, t23 = a23 + f32x2{bb[2], bb[3]};
+#else
             const f32x2 t01 = tanh_rat2(a01 + f32x2{bb[0], bb[1]});
             const f32x2 t23 = tanh_rat2(a23 + f32x2{bb[2], bb[3]});
+#endif
+#if DR_LT_ABL == 2      // diagnostic: no per-row store
+            keep = add4(keep, make_float4(t01.x, t01.y, t23.x, t23.y));
+#else
             st4(h + r * n + c0, make_float4(t01.x, t01.y, t23.x, t23.y));
+#endif
         }
         continue;
 #endif
