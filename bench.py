@@ -70,12 +70,12 @@ def rollout_kernel_name(n_envs, n_cu, gen, variant="gym"):
 
 
 # SQ_ACTIVE_INST_VALU over the physics waves' share of SQ_WAVE_CYCLES of the
-# K = 32 rollout kernel at 65,536 envs (profiles/r03_pmc_rollout.json; an
+# K = 32 rollout kernel at 65,536 envs (profiles/r04_pmc_rollout.json; an
 # upper bound, the memory waves' VALU included): per physics wave of the
-# split kernel (two per SIMD: 0.67 of the SIMD's cycles together) with actions
+# split kernel (two per SIMD: 0.68 of the SIMD's cycles together) with actions
 # from HBM, of the warp-specialised kernel (one per SIMD) with the in-kernel
 # policy
-PMC_ROLLOUT_VALU_ACTIVE = {"actions_from_hbm": 0.335, "random_policy_in_kernel": 0.637}
+PMC_ROLLOUT_VALU_ACTIVE = {"actions_from_hbm": 0.342, "random_policy_in_kernel": 0.638}
 
 
 def parse():
