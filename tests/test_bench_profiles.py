@@ -89,3 +89,10 @@ def test_grid_stats_split_the_probe_from_the_headline_launches(tmp_path):
     assert abs(k["frac"] - 65536 * (32 * 81 + 224) / 43e-6 / 8e12) < 1e-3
     assert bench.rollout_rocprof_k32(str(out), 4096, "f64") is None
     assert bench.rollout_rocprof_k32(str(tmp_path / "none.json"), 65536, "f64") is None
+
+
+def test_bench_pmc_constants_follow_the_committed_rollout_pmc():
+    d = json.load(open(os.path.join(ROOT, "profiles", "r04_pmc_rollout.json")))
+    for k, v in bench.PMC_ROLLOUT_VALU_ACTIVE.items():
+        assert v == d[k]["valu_active_frac_of_wave_cycles"], k
+    assert d["actions_from_hbm"]["kernel"] == "env_rollout_ab_kernel"
