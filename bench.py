@@ -53,6 +53,21 @@ BYTES_PER_ENV_STEP = {"f64": 305, "f32": 197}
 # moving-target variant: + 9 f32 motion params read, + 3 f32 obs written
 BYTES_PER_ENV_STEP_MOVING = {"f64": 353, "f32": 245}
 HBM_PEAK_GBS = 8000.0      # MI355X HBM3E spec (MI355X_MICROARCH.md)
+# numbers read from committed profiles whose kernel sources differ from this
+# tree's (committed_profile): reported in the line's committed_artefacts
+# block, labelled stale, never inside a live block
+ARTEFACTS = {}
+
+
+def _atoi(v):
+    """C atoi(): leading whitespace, an optional sign and the leading
+    digits; 0 when there are none (how launch_rollout reads its env knobs)."""
+    v = v.lstrip()
+    i = 1 if v[:1] in "+-" else 0
+    j = i
+    while j < len(v) and v[j].isdigit():
+        j += 1
+    return int(v[:j]) if j > i else 0
 
 
 def rollout_kernel_name(n_envs, n_cu, gen, variant="gym"):
@@ -63,19 +78,77 @@ def rollout_kernel_name(n_envs, n_cu, gen, variant="gym"):
     gym variant with actions read from HBM; the one-role rollout kernel above
     that."""
     ws_env = os.environ.get("DRONERL_ROLLOUT_WS")
-    ws = (ws_env != "0") if ws_env is not None else n_envs <= 256 * n_cu
+    ws = _atoi(ws_env) != 0 if ws_env is not None else n_envs <= 256 * n_cu
     if variant == "gym" and ws and not gen:
         return "env_rollout_ab_kernel"
     return "env_rollout_ws_kernel" if ws else "env_rollout_kernel"
 
 
-# SQ_ACTIVE_INST_VALU over the physics waves' share of SQ_WAVE_CYCLES of the
-# K = 32 rollout kernel at 65,536 envs (profiles/r04_pmc_rollout.json; an
-# upper bound, the memory waves' VALU included): per physics wave of the
-# split kernel (two per SIMD: 0.68 of the SIMD's cycles together) with actions
-# from HBM, of the warp-specialised kernel (one per SIMD) with the in-kernel
-# policy
-PMC_ROLLOUT_VALU_ACTIVE = {"actions_from_hbm": 0.342, "random_policy_in_kernel": 0.638}
+PROVENANCE_JSON = os.path.join(ROOT, "profiles", "provenance.json")
+
+
+def kernel_source_hash():
+    """sha256 over the sources of libdronerl.so (csrc/*.hip, *.h, the
+    Makefile and include/dronerl.h, in name order): what a committed
+    profile was measured on.  Computed the same way here and on the GPU box
+    (the sources travel with the tree)."""
+    import hashlib
+    csrc = os.path.join(ROOT, "drone_rl_amd", "csrc")
+    files = sorted(f for f in os.listdir(csrc)
+                   if f.endswith((".hip", ".h")) or f == "Makefile")
+    h = hashlib.sha256()
+    for rel in [os.path.join("drone_rl_amd", "csrc", f) for f in files] + \
+            [os.path.join("include", "dronerl.h")]:
+        h.update(rel.encode() + b"\0")
+        with open(os.path.join(ROOT, rel), "rb") as fh:
+            h.update(fh.read())
+        h.update(b"\0")
+    return h.hexdigest()
+
+
+def committed_profile(path, current_hash=None):
+    """Provenance of a committed profile (profiles/provenance.json: the
+    kernel_source_hash of the tree it was measured on): {"source": path
+    relative to the repo, "matches_tree": bool, "measured_on": hash prefix}.
+    Numbers read from a profile that does not match the current kernel
+    sources are never mixed into the live blocks of the line (they go to
+    the line's committed_artefacts block, labelled stale)."""
+    rel = os.path.relpath(path, ROOT)
+    try:
+        prov = json.load(open(PROVENANCE_JSON))
+    except (OSError, ValueError):
+        prov = {}
+    rec = prov.get(os.path.basename(path), {})
+    h = rec.get("source_hash")
+    cur = current_hash or kernel_source_hash()
+    return {"source": rel, "matches_tree": bool(h) and h == cur,
+            "measured_on": (h or "unknown")[:12]}
+
+
+def committed_or_stale(key, path, value):
+    """value (read from the committed profile at path) when that profile
+    was measured on this tree's kernel sources, with its source; otherwise
+    None here and the value filed under ARTEFACTS[key], labelled stale."""
+    if value is None:
+        return None
+    prov = committed_profile(path)
+    if prov["matches_tree"]:
+        return dict(value, provenance=prov) if isinstance(value, dict) else \
+            {"value": value, "provenance": prov}
+    ARTEFACTS[key] = dict(prov, stale=True, values=value)
+    return None
+
+
+def pmc_rollout_valu_active(path):
+    """SQ_ACTIVE_INST_VALU over the physics waves' share of SQ_WAVE_CYCLES of
+    the K = 32 rollout kernel at 65,536 envs, per action source, from the
+    committed PMC summary (scripts/pmc_summary.py output), or {} when absent."""
+    try:
+        d = json.load(open(path))
+        return {k: d[k]["valu_active_frac_of_wave_cycles"]
+                for k in ("actions_from_hbm", "random_policy_in_kernel") if k in d}
+    except (OSError, ValueError, KeyError, TypeError):
+        return {}
 
 
 def parse():
@@ -110,12 +183,68 @@ def parse():
                     default=os.path.join(ROOT, "profiles", "r04_rollout_grid_stats.json"),
                     help="scripts/kernel_grid_stats.py output: the headline kernel's rocprof "
                          "durations at K = 32 on 65,536 envs")
+    ap.add_argument("--pmc-rollout",
+                    default=os.path.join(ROOT, "profiles", "r04_pmc_rollout.json"),
+                    help="scripts/pmc_summary.py output of the K = 32 rollout kernel (its "
+                         "VALU-active fractions are reported when it matches the tree)")
     ap.add_argument("--headline", choices=["rollout", "step"], default="rollout",
                     help="kernel of the headline value: the K-step rollout kernel or one "
                          "dr_step launch per step")
     ap.add_argument("--headline-k", type=int, default=32,
                     help="max steps per rollout-kernel launch in the headline")
     return ap.parse_args()
+
+
+def timed_region(work, sync, world, clock=time.monotonic_ns):
+    """The timing rule of every bench leg: a barrier
+    and a device synchronize come BEFORE t0; then the work and a device
+    synchronize; then t1.  No torch.distributed call runs between t0 and t1
+    (at --steps 20 the timed region is one ~29 us launch, which an RCCL
+    barrier across 8 GPUs would rival).  Returns (t0, t1) in ns of
+    CLOCK_MONOTONIC, the clock every process of one node shares, so the
+    ranks' spans can be compared after the timer (node_timing)."""
+    if world > 1:
+        import torch.distributed as dist
+        dist.barrier()
+    sync()
+    t0 = clock()
+    work()
+    sync()
+    t1 = clock()
+    return t0, t1
+
+
+def gather_spans(span, world, device=None):
+    """Every rank's (t0_ns, t1_ns, gpu_ns) of one timed region, exchanged
+    AFTER the timer (one all_gather of 3 int64); [span] at world 1."""
+    span = tuple(int(v) for v in span)
+    if world == 1:
+        return [span]
+    import torch
+    import torch.distributed as dist
+    dev = device if dist.get_backend() == "nccl" else "cpu"
+    t = torch.tensor(span, dtype=torch.int64, device=dev)
+    out = [torch.empty_like(t) for _ in range(world)]
+    dist.all_gather(out, t)
+    return [tuple(int(v) for v in o.tolist()) for o in out]
+
+
+def node_timing(spans):
+    """Pure arithmetic over every rank's (t0_ns, t1_ns, gpu_ns): the whole
+    node's wall of the timed region, max(t1) - min(t0) (CLOCK_MONOTONIC is
+    shared by the node's processes; it covers the slowest rank and any skew
+    between the ranks' starts), the slowest rank's own span, and the max
+    over ranks of the GPU time.  Seconds / ms."""
+    if not spans:
+        raise ValueError("no spans")
+    t0 = min(s[0] for s in spans)
+    t1 = max(s[1] for s in spans)
+    if any(s[1] < s[0] for s in spans):
+        raise ValueError("a span ends before it starts")
+    return {"wall_s": (t1 - t0) / 1e9,
+            "max_rank_s": max(s[1] - s[0] for s in spans) / 1e9,
+            "gpu_ms": max(s[2] for s in spans) / 1e6,
+            "ranks": len(spans)}
 
 
 def cpu_share():
@@ -164,7 +293,6 @@ def cpu_baseline(seconds):
 
 def time_env(args, dtype_name, n_envs, rank, world, device, steps, warmup, variant="gym"):
     import torch
-    import torch.distributed as dist
 
     from drone_rl_amd import DroneBatch, random_actions
     dtype = torch.float64 if dtype_name == "f64" else torch.float32
@@ -197,26 +325,20 @@ def time_env(args, dtype_name, n_envs, rank, world, device, steps, warmup, varia
     torch.cuda.synchronize(device)
     ev0 = torch.cuda.Event(enable_timing=True)
     ev1 = torch.cuda.Event(enable_timing=True)
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize(device)
-    t0 = time.perf_counter()
-    ev0.record(stream)
-    if graph is not None:
-        graph.replay()
-    else:
-        for t in range(warmup, total):
-            b.step(acts[t])
-    ev1.record(stream)
-    torch.cuda.synchronize(device)
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    gpu_ms = ev0.elapsed_time(ev1)
-    if world > 1:
-        t = torch.tensor([elapsed, gpu_ms], dtype=torch.float64, device=device)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed, gpu_ms = float(t[0]), float(t[1])
+    for e in (ev0, ev1):
+        e.record(stream)        # the events' lazy creation stays out of the timed region
+
+    def work():
+        ev0.record(stream)
+        if graph is not None:
+            graph.replay()
+        else:
+            for t in range(warmup, total):
+                b.step(acts[t])
+        ev1.record(stream)
+    span = timed_region(work, lambda: torch.cuda.synchronize(device), world)
+    tm = node_timing(gather_spans((*span, round(ev0.elapsed_time(ev1) * 1e6)), world, device))
+    elapsed, gpu_ms = tm["wall_s"], tm["gpu_ms"]
     # sanity: the env is alive (episodes end and reset under a random policy)
     ep = b.get("ep_num").float().mean().item()
     b.close()
@@ -234,7 +356,6 @@ def time_headline(args, n_envs, rank, world, device, steps, warmup, kmax):
     with prebuilt arguments (repeated three times untimed first).
     Returns (wall seconds, GPU ms over the timed launches, launches, mean ep_num)."""
     import torch
-    import torch.distributed as dist
 
     from drone_rl_amd import DroneBatch, random_actions
     dtype = torch.float64 if args.state_dtype == "f64" else torch.float32
@@ -302,8 +423,6 @@ def time_headline(args, n_envs, rank, world, device, steps, warmup, kmax):
     pk1 = torch.cuda.Event(enable_timing=True)
     for e in (ev0, ev1, pk0, pk1):
         e.record(stream)        # the events' lazy creation stays out of the timed region
-    if world > 1:
-        dist.barrier()
     packet_ms = None
     if g is None:
         # untimed repetitions right before the timed one, through
@@ -323,26 +442,19 @@ def time_headline(args, n_envs, rank, world, device, steps, warmup, kmax):
             if rep > 0:
                 reps.append(pk0.elapsed_time(pk1))
         packet_ms = sorted(reps)[len(reps) // 2]
+    def work():
+        ev0.record(stream)
+        timed()
+        ev1.record(stream)
     gc.disable()
-    torch.cuda.synchronize(device)
-    t0 = time.perf_counter()
-    ev0.record(stream)
-    timed()
-    ev1.record(stream)
-    torch.cuda.synchronize(device)
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
+    span = timed_region(work, lambda: torch.cuda.synchronize(device), world)
     gc.enable()
-    gpu_ms = ev0.elapsed_time(ev1)
     if g is None and any(rcs):
         from drone_rl_amd._lib import check
         check(next(r for r in rcs if r), b.handle)
-    if world > 1:
-        t = torch.tensor([elapsed, gpu_ms], dtype=torch.float64, device=device)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed, gpu_ms = float(t[0]), float(t[1])
-    ep = b.get("ep_num").float().mean().item()
+    tm = node_timing(gather_spans((*span, round(ev0.elapsed_time(ev1) * 1e6)), world, device))
+    elapsed, gpu_ms = tm["wall_s"], tm["gpu_ms"]
+    ep =b.get("ep_num").float().mean().item()
     b.close()
     graphed = g is not None
     del g
@@ -497,14 +609,16 @@ def ppo_kernel_times(tr, reps=20):
 
     step_prefix(100, record=True)        # eager once: the kernel order, lazy init
     torch.cuda.synchronize(tr.device)
-    tj = [0.0]
-    for j in range(1, len(names) + 1):
+
+    def graph_us(fn):
+        """fn() x reps captured in one hipGraph, replayed once untimed
+        (upload) and once timed by HIP events on the stream: us per fn()."""
         cs = torch.cuda.Stream(tr.device)
         cs.wait_stream(stream)
         g = torch.cuda.CUDAGraph()
         with torch.cuda.stream(cs), torch.cuda.graph(g, stream=cs):
             for _ in range(reps):
-                step_prefix(j)
+                fn()
         stream.wait_stream(cs)
         g.replay()                       # upload
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -512,9 +626,30 @@ def ppo_kernel_times(tr, reps=20):
         g.replay()
         e1.record(stream)
         torch.cuda.synchronize(tr.device)
-        tj.append(e0.elapsed_time(e1) * 1e3 / reps)
         del g
-    return {n: tj[i + 1] - tj[i] for i, n in enumerate(names)}
+        return e0.elapsed_time(e1) * 1e3 / reps
+    tj = [0.0]
+    for j in range(1, len(names) + 1):
+        tj.append(graph_us(lambda: step_prefix(j)))
+    prefix = {n: tj[i + 1] - tj[i] for i, n in enumerate(names)}
+    # the 256x256 layer's three GEMMs alone, each launch repeated back to back
+    # on the trainer's buffers as the last step left them (the same kernels,
+    # grids and operands; idempotent launches)
+    from drone_rl_amd import _lib
+    from drone_rl_amd.policy import gemm_x6, x6_weights
+    f, pol = tr.fused, tr.policy
+    iso = {}
+    xw = x6_weights(pol, M)
+    if xw is not None and getattr(f, "_acts2", None) is not None and f.C > 1:
+        a0, a1, gz = f._acts2[0], f._acts2[1], f._gz2[1]
+        g = f._g2.view(-1)[:2 * M * 256].view(2, M, 256)
+        ws = f._ws2
+        st = stream.cuda_stream
+        iso["gemm_x6_fwd"] = graph_us(lambda: gemm_x6(a0, xw.fwd, a1))
+        iso["gemm_x6_bwd"] = graph_us(lambda: gemm_x6(gz, xw.bwd, g))
+        iso["gemm_x6_wgrad"] = graph_us(lambda: _lib.check(_lib.lib().dr_gemm_x6_wgrad(
+            2, M, f.C, gz.data_ptr(), a0.data_ptr(), ws.data_ptr(), st)))
+    return prefix, iso
 
 
 # bench.py's PPO step names -> the kernel each launches (rocprofv3 names)
@@ -563,62 +698,79 @@ def rocprof_averages(path):
     return out
 
 
-def ppo_roofline(cfg, s_per_update, ktimes, rocprof=None):
-    """The ppo block's roofline: the whole update's fp32-equivalent FLOP
-    rate against the f32 matrix peak, the 256x256 layer's x6 GEMMs against
-    the bf16 MFMA peak (6 bf16 products per fp32 product), and the
-    memory-bound kernels against HBM (algorithmic bytes per 65,536-row
-    minibatch)."""
+def ppo_roofline(cfg, s_per_update, ktimes, rocprof=None, isolated=None, rocprof_source=None):
+    """The ppo block's roofline.  Whole update: fp32-equivalent FLOP per
+    second, reported against the f32 matrix peak only as
+    `fp32_equiv_frac_of_f32_peak` (the 256x256 GEMMs run as 6 bf16 MFMA
+    products per fp32 product, so that ratio may exceed 1 and is not a
+    hardware utilisation).  Per kernel of one optimizer step: the prefix
+    split's time (`prefix_split_us`, its method in kernel_timing) with the
+    x6 GEMMs priced as bf16 MFMA work against the dense bf16 peak and the
+    memory-bound kernels as algorithmic bytes (per 65,536-row minibatch,
+    DESIGN.md 3) against HBM (`prefix_split_frac`); the GEMMs also timed
+    alone (`isolated_us`, live); `rocprof_us` / `rocprof_frac` from a
+    committed rocprofv3 summary that matches the current kernel sources
+    (`rocprof_source`).  The dominant kernel (the forward x6 GEMM) takes its
+    fraction from its live isolated launches."""
     M, NT, E = cfg.batch_size, cfg.num_envs * cfg.n_steps, cfg.n_epochs
     flop_update = NT * PPO_FWD_FLOP * (1 + 3 * E)
     gemm_flop = 2 * 2 * M * 256 * 256            # both nets, one fp32 GEMM
     rows = {"gather_minibatch": 2 * (15 + 4 + 3) * 4,
             "linear_tanh": 15 * 4 + 2 * 256 * 4,
-            "pack_first": 15 * 4 + 16 * 4,
             "ppo_head": 2 * 1024 + 2 * 1024 + 44,
             "first_layer_bwd": 2 * 2 * 1024 + 60}
     kern = {}
     rocprof = rocprof or {}
+    isolated = isolated or {}
+
+    def mfma_frac(us):
+        return round(6 * gemm_flop / (us * 1e-6) / 1e12 / BF16_DENSE_PEAK_TFLOPS, 4)
+
+    def hbm_frac(name, us):
+        return round(rows[name] * M / (us * 1e-6) / 1e9 / HBM_PEAK_GBS, 4)
     for name, us in ktimes.items():
-        e = {"us": round(us, 2)}
+        e = {"prefix_split_us": round(us, 2)}
         rp = rocprof.get(PPO_KERNEL_NAMES.get(name, ""))
         if rp is not None:
-            # the kernel's own average duration (rocprofv3, committed csv;
-            # the forward / input-gradient GEMM share one kernel), beside the
-            # in-step event split above (which includes the launch boundary)
+            # the kernel's own average duration in whole training steps
+            # (rocprofv3; the forward / input-gradient GEMM share one kernel)
             e["rocprof_us"] = round(rp, 2)
         if name.startswith("gemm_x6"):
-            tf32 = gemm_flop / (us * 1e-6) / 1e12
-            e.update({"bound": "mfma", "fp32_equiv_tflops": round(tf32, 1),
-                      "bf16_mfma_tflops": round(6 * tf32, 1),
-                      "frac": round(6 * tf32 / BF16_DENSE_PEAK_TFLOPS, 4)})
+            e.update({"bound": "mfma", "prefix_split_frac": mfma_frac(us)})
+            if name in isolated:
+                e.update({"isolated_us": round(isolated[name], 2),
+                          "isolated_frac": mfma_frac(isolated[name])})
             if rp is not None:
-                e["rocprof_frac"] = round(6 * gemm_flop / (rp * 1e-6) / 1e12 /
-                                          BF16_DENSE_PEAK_TFLOPS, 4)
+                e["rocprof_frac"] = mfma_frac(rp)
         elif name in rows:
-            gbs = rows[name] * M / (us * 1e-6) / 1e9
-            e.update({"bound": "hbm", "bytes": rows[name] * M, "achieved_GBs": round(gbs, 1),
-                      "frac": round(gbs / HBM_PEAK_GBS, 4)})
+            e.update({"bound": "hbm", "bytes": rows[name] * M,
+                      "prefix_split_frac": hbm_frac(name, us)})
             if rp is not None:
-                e["rocprof_frac"] = round(rows[name] * M / (rp * 1e-6) / 1e9 / HBM_PEAK_GBS, 4)
+                e["rocprof_frac"] = hbm_frac(name, rp)
         kern[name] = e
     ach = flop_update / s_per_update / 1e12
-    x6 = kern.get("gemm_x6_fwd")
-    out = {"bound": "mfma", "unit": "TFLOP/s",
-           "flop_per_update": flop_update,
-           "achieved": round(ach, 2), "peak": F32_MATRIX_PEAK_TFLOPS,
-           "frac": round(ach / F32_MATRIX_PEAK_TFLOPS, 4),
+    out = {"unit": "TFLOP/s", "flop_per_update": flop_update,
+           "fp32_equiv_tflops": round(ach, 2), "f32_matrix_peak": F32_MATRIX_PEAK_TFLOPS,
+           "fp32_equiv_frac_of_f32_peak": round(ach / F32_MATRIX_PEAK_TFLOPS, 4),
            "basis": "fp32-equivalent FLOP per update (rollout forward 280,064 FLOP/sample + "
-                    "3 x forward per sample and epoch, SURVEY.md 8d) / s_per_update, against "
-                    "the f32 matrix peak (the model's arithmetic at fp32 accuracy; the "
-                    "hardware runs the 256x256 GEMMs as 6 bf16 MFMA products each: "
-                    "kernels_per_minibatch.gemm_x6_* carry their bf16-MFMA fractions)",
+                    "3 x forward per sample and epoch, SURVEY.md 8d) / s_per_update; the "
+                    "ratio to the f32 matrix peak is NOT a hardware utilisation (the 256x256 "
+                    "GEMMs run as 6 bf16 MFMA products per fp32 product; their bf16-MFMA "
+                    "fractions are in kernels_per_minibatch and dominant_kernel)",
+           "rocprof_source": rocprof_source,
            "kernels_per_minibatch": kern}
-    if x6 is not None:
-        out["dominant_kernel"] = {"kernel": "gemm_x6_ws_kernel (forward)", "bound": "mfma",
-                                  "achieved": x6["bf16_mfma_tflops"],
-                                  "peak": BF16_DENSE_PEAK_TFLOPS, "unit": "TFLOP/s",
-                                  "frac": x6["frac"]}
+    if "gemm_x6_fwd" in isolated:
+        us = isolated["gemm_x6_fwd"]
+        d = {"kernel": "gemm_x6_ws_kernel (forward, both nets, 65,536 rows)", "bound": "mfma",
+             "achieved": round(6 * gemm_flop / (us * 1e-6) / 1e12, 1),
+             "peak": BF16_DENSE_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": mfma_frac(us),
+             "us": round(us, 2),
+             "timing": "live: 20 back-to-back launches on the trainer's buffers in one "
+                       "hipGraph, HIP events"}
+        rp = rocprof.get("gemm_x6_ws_kernel")
+        if rp is not None:
+            d.update({"rocprof_us": round(rp, 2), "rocprof_frac": mfma_frac(rp)})
+        out["dominant_kernel"] = d
     return out
 
 
@@ -639,22 +791,16 @@ def time_ppo(args, rank, world, device, force_dp=False, dp_graph=False, profile=
     # and training graphs (replayed by every timed iteration)
     tr.learn_step()
     tr.learn_step()
-    torch.cuda.synchronize(device)
-    if world > 1:
-        dist.barrier()
     K = args.ppo_updates if updates is None else updates
-    t0 = time.perf_counter()
-    for _ in range(K):
-        st = tr.learn_step()
-    torch.cuda.synchronize(device)
-    if world > 1:
-        dist.barrier()
-    el = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([el], dtype=torch.float64, device=device)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        el = float(t[0])
-    es = tr.episode_stats()
+    last = []
+
+    def work():
+        for _ in range(K):
+            last[:] = [tr.learn_step()]
+    span = timed_region(work, lambda: torch.cuda.synchronize(device), world)
+    el = node_timing(gather_spans((*span, 0), world, device))["wall_s"]
+    st = last[0]
+    es =tr.episode_stats()
     stats = dict(zip(("loss", "policy_loss", "value_loss", "entropy_loss", "clip_fraction",
                       "approx_kl"), [round(x, 5) for x in st.tolist()[:6]]))
     coll = {"nccl": "RCCL"}.get(dist.get_backend(), dist.get_backend()) if world > 1 else (
@@ -687,14 +833,21 @@ def time_ppo(args, rank, world, device, force_dp=False, dp_graph=False, profile=
                       if world > 1 or tr.dp_collective else "none"},
            "last_update_stats": stats, "episodes": es}
     if profile and world == 1 and tr._train_fast() and not tr.dp_step:
-        res["roofline"] = ppo_roofline(cfg, el / K, ppo_kernel_times(tr),
-                                       rocprof_averages(args.kernel_stats))
+        prefix, iso = ppo_kernel_times(tr)
+        rp = rocprof_averages(args.kernel_stats)
+        prov = committed_profile(args.kernel_stats)
+        if rp and not prov["matches_tree"]:
+            ARTEFACTS["ppo_kernel_rocprof_us"] = dict(prov, stale=True, values=rp)
+        live = prov["matches_tree"]
+        res["roofline"] = ppo_roofline(cfg, el / K, prefix, rp if live else {}, iso,
+                                       prov["source"] if live else None)
         res["roofline"]["kernel_timing"] = (
-            "us: graph replays of the step's first j kernels x 20, timed by HIP events, kernel "
-            "j = T_j - T_(j-1) (the step's tail and the next repetition's head shift with j, "
-            "so cache effects land on neighbours); rocprof_us: the kernel's own duration in "
-            "whole training steps (rocprofv3 --stats, --kernel-stats csv; HIP graphs on ROCm "
-            "take no timed event nodes)")
+            "prefix_split_us: graph replays of the step's first j kernels x 20, timed by HIP "
+            "events, kernel j = T_j - T_(j-1) (the step's tail and the next repetition's head "
+            "shift with j, so cache effects land on neighbours: a per-kernel estimate, not a "
+            "duration); isolated_us: the kernel alone, 20 launches in one graph; rocprof_us: "
+            "the kernel's own duration in whole training steps (rocprofv3 --stats of this "
+            "bench on the same kernel sources; HIP graphs on ROCm take no timed event nodes)")
     tr.close()
     return res
 
@@ -728,19 +881,51 @@ def spawn_ranks(n):
                                       env=env))
     rc = 0
     live = list(procs)
-    while live:
-        for p in list(live):
-            r = p.poll()
-            if r is None:
-                continue
-            live.remove(p)
-            if r != 0 and rc == 0:
-                rc = r if r > 0 else 128 - r
-                sys.stderr.write(f"bench.py: rank {procs.index(p)} exited with {r}; "
-                                 f"stopping the other ranks\n")
-                for q in live:
-                    q.send_signal(signal.SIGTERM)
-        time.sleep(0.05)
+
+    def stop(ps, grace=10.0):
+        """SIGTERM the given ranks, then SIGKILL whatever is left after grace s."""
+        for q in ps:
+            if q.poll() is None:
+                q.send_signal(signal.SIGTERM)
+        end = time.monotonic() + grace
+        for q in ps:
+            try:
+                q.wait(timeout=max(0.0, end - time.monotonic()))
+            except subprocess.TimeoutExpired:
+                q.kill()
+                q.wait()
+
+    def on_signal(signum, frame):
+        # the launcher itself was told to stop (a driver timeout, ^C): take
+        # the ranks down with it instead of leaving them on the GPUs
+        sys.stderr.write(f"bench.py: launcher got signal {signum}; stopping the ranks\n")
+        stop(procs)
+        sys.exit(128 + signum)
+    old = {s: signal.signal(s, on_signal) for s in (signal.SIGTERM, signal.SIGINT)}
+    deadline = time.monotonic() + float(os.environ.get("DRONERL_BENCH_RANK_TIMEOUT", "3600"))
+    try:
+        while live:
+            for p in list(live):
+                r = p.poll()
+                if r is None:
+                    continue
+                live.remove(p)
+                if r != 0 and rc == 0:
+                    rc = r if r > 0 else 128 - r
+                    sys.stderr.write(f"bench.py: rank {procs.index(p)} exited with {r}; "
+                                     f"stopping the other ranks\n")
+                    stop(live)
+            if live and time.monotonic() > deadline:
+                # a rank stuck (e.g. in a collective whose peer died) must not
+                # hold the launcher, or the GPUs, forever
+                sys.stderr.write("bench.py: ranks exceeded DRONERL_BENCH_RANK_TIMEOUT; "
+                                 "stopping them\n")
+                stop(live)
+                rc = rc or 124
+            time.sleep(0.05)
+    finally:
+        for s_, h in old.items():
+            signal.signal(s_, h)
     return rc
 
 
@@ -787,6 +972,12 @@ def main():
         tj = json.load(open(args.traffic_json))
     except (OSError, ValueError):
         pass
+    if tj and not committed_profile(args.traffic_json)["matches_tree"]:
+        # PMC traffic of other kernel sources: filed as stale, not reported live
+        ARTEFACTS["traffic"] = dict(committed_profile(args.traffic_json), stale=True,
+                                    values={k: v.get("hbm_bytes_per_launch")
+                                            for k, v in tj.items() if isinstance(v, dict)})
+        tj = {}
 
     def step_block(elapsed, gpu_ms, steps, n):
         pl = gpu_ms / 1e3 / steps
@@ -828,7 +1019,9 @@ def main():
                 # the same kernel's own rocprofv3 durations, K = 32 launches
                 # on 65,536 envs (the host-floor probe's 64-env launches of it
                 # split off by grid)
-                "rocprof_k32": rollout_rocprof_k32(args.rollout_grid_stats, N, args.state_dtype),
+                "rocprof_k32": committed_or_stale(
+                    "rollout_rocprof_k32", args.rollout_grid_stats,
+                    rollout_rocprof_k32(args.rollout_grid_stats, N, args.state_dtype)),
                 # the same launches (median of 5 untimed repetitions right
                 # before the timed one, after a warm-up) by their dispatch
                 # packets' own timestamps: the kernel alone, without the
@@ -892,12 +1085,7 @@ def main():
         el4, gm4, _ = time_env(args, args.state_dtype, n4, 0, 1, device, k4, 20)
         pl4 = gm4 / 1e3 / k4
         ach4 = n4 * BYTES_PER_ENV_STEP[args.state_dtype] / pl4 / 1e9
-        tr4 = None
-        try:
-            tr4 = json.load(open(args.traffic_json))[f"{args.state_dtype}_{n4}"][
-                "hbm_bytes_per_launch"]
-        except (OSError, ValueError, KeyError):
-            pass
+        tr4 = tj.get(f"{args.state_dtype}_{n4}", {}).get("hbm_bytes_per_launch")
         out["companion"] = {"envs": n4, "steps": k4, "kernel": "env_step_kernel (dr_step)",
                             "env_steps_per_s": round(n4 * k4 / el4, 1),
                             "avg_launch_us": round(pl4 * 1e6, 3),
@@ -942,11 +1130,15 @@ def main():
                 "roofline": {"bound": "hbm", "achieved": round(ach, 1),
                              "peak": HBM_PEAK_GBS, "unit": "GB/s",
                              "frac": round(ach / HBM_PEAK_GBS, 4)},
-                "valu_active_frac_of_wave_cycles": PMC_ROLLOUT_VALU_ACTIVE[
-                    "random_policy_in_kernel" if gen else "actions_from_hbm"]}
+                "valu_active_frac_of_wave_cycles": committed_or_stale(
+                    "rollout_valu_active_" + ("random_policy_in_kernel" if gen
+                                              else "actions_from_hbm"), args.pmc_rollout,
+                    pmc_rollout_valu_active(args.pmc_rollout).get(
+                        "random_policy_in_kernel" if gen else "actions_from_hbm"))}
         out["rollout_kernel"] = ro
     if cpu is not None:
         out["cpu_baseline"] = cpu
+    out["kernel_source_hash"] = kernel_source_hash()[:12]
     if args.ppo_updates > 0:
         out["ppo"] = time_ppo(args, rank, world, device)
     if args.extra and world == 1:
@@ -966,10 +1158,15 @@ def main():
                 sk.close()
                 dist.init_process_group("nccl", rank=0, world_size=1, device_id=device,
                                         init_method=f"tcp://127.0.0.1:{port}")
-                ex["ppo_dp_path_world1_rccl_graph"] = time_ppo(
-                    args, 0, 1, device, force_dp=True, dp_graph=True, profile=False)
+                # the form N > 1 runs by default under RCCL (PPOConfig.dp_graph
+                # off: the training loop eager, one all-reduce per step), then
+                # the captured one
+                for key, cap in (("ppo_dp_path_world1_rccl_eager", False),
+                                 ("ppo_dp_path_world1_rccl_graph", True)):
+                    ex[key] = time_ppo(args, 0, 1, device, force_dp=True, dp_graph=cap,
+                                       profile=False)
             except Exception as e:      # report, keep the rest of the line
-                ex["ppo_dp_path_world1_rccl_graph"] = {"error": repr(e)[:300]}
+                ex["ppo_dp_path_world1_rccl_error"] = {"error": repr(e)[:300]}
             finally:
                 if dist.is_initialized():
                     dist.destroy_process_group()
@@ -1003,6 +1200,8 @@ def main():
                                              "avg_launch_us": round(pl * 1e6, 3),
                                              "us_per_step": round(pl * 1e6 / 32, 3)}
         out["extra"] = ex
+    if ARTEFACTS:
+        out["committed_artefacts"] = ARTEFACTS
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:

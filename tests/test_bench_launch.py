@@ -56,3 +56,28 @@ def test_direct_gpus2_starts_two_ranks():
     assert d["config"]["parallelism"].startswith("dp2")
     assert "cpu_baseline" not in d
     assert d["ppo"]["train_path"].startswith("data-parallel step")
+
+
+def test_launcher_sigterm_takes_the_ranks_down():
+    """A driver timeout that signals only the launcher's PID must not leave
+    the ranks running (advisor r04): the launcher forwards SIGTERM and
+    exits non-zero."""
+    import signal
+    import time
+
+    import psutil
+    p = subprocess.Popen([sys.executable, BENCH, "--gpus", "2", "--no-cpu-baseline",
+                          "--ppo-updates", "0"],
+                         env=_env(HIP_VISIBLE_DEVICES="", CUDA_VISIBLE_DEVICES=""),
+                         stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
+    kids = []
+    end = time.monotonic() + 60
+    while time.monotonic() < end and len(kids) < 2:
+        kids = psutil.Process(p.pid).children()
+        time.sleep(0.02)
+    assert len(kids) == 2
+    p.send_signal(signal.SIGTERM)
+    _, err = p.communicate(timeout=60)
+    assert p.returncode != 0
+    gone, alive = psutil.wait_procs(kids, timeout=30)
+    assert not alive

@@ -34,15 +34,32 @@ def test_ppo_roofline_carries_rocprof_durations_and_fractions():
         batch_size, num_envs, n_steps, n_epochs = 65536, 65536, 32, 10
     rp = {"gemm_x6_ws_kernel": 80.0, "linear_tanh_kernel": 30.0}
     out = bench.ppo_roofline(Cfg, 0.15, {"gemm_x6_fwd": 100.0, "linear_tanh": 35.0,
-                                         "grad_finish_clip_adam": 10.0}, rp)
+                                         "grad_finish_clip_adam": 10.0}, rp,
+                             {"gemm_x6_fwd": 90.0}, "profiles/x.csv")
     k = out["kernels_per_minibatch"]
     # 6 bf16 products x 2 nets x 2 M 256 256 FLOP over 80 us against 2.5 PF
     flop = 6 * 2 * 2 * 65536 * 256 * 256
     assert abs(k["gemm_x6_fwd"]["rocprof_frac"] - flop / 80e-6 / 2.5e15) < 1e-3
-    assert k["gemm_x6_fwd"]["rocprof_us"] == 80.0 and k["gemm_x6_fwd"]["us"] == 100.0
+    assert k["gemm_x6_fwd"]["rocprof_us"] == 80.0 and k["gemm_x6_fwd"]["prefix_split_us"] == 100.0
+    assert abs(k["gemm_x6_fwd"]["isolated_frac"] - flop / 90e-6 / 2.5e15) < 1e-3
     assert abs(k["linear_tanh"]["rocprof_frac"] - (15 * 4 + 2 * 256 * 4) * 65536 / 30e-6 / 8e12) < 1e-3
     assert "rocprof_us" not in k["grad_finish_clip_adam"]
-    assert out["dominant_kernel"]["kernel"].startswith("gemm_x6_ws_kernel")
+    # no field called plain "frac" in the per-kernel entries: the prefix split
+    # is labelled as such (verdict r04 item 6)
+    assert all("frac" not in e for e in k.values())
+    d = out["dominant_kernel"]
+    assert d["kernel"].startswith("gemm_x6_ws_kernel") and d["us"] == 90.0
+    assert abs(d["frac"] - flop / 90e-6 / 2.5e15) < 1e-3 and d["rocprof_us"] == 80.0
+    # the whole-update ratio is named for what it is
+    assert "frac" not in out and "fp32_equiv_frac_of_f32_peak" in out
+    assert out["rocprof_source"] == "profiles/x.csv"
+
+
+def test_ppo_roofline_without_isolated_times_has_no_dominant_kernel():
+    class Cfg:
+        batch_size, num_envs, n_steps, n_epochs = 65536, 65536, 32, 10
+    out = bench.ppo_roofline(Cfg, 0.15, {"gemm_x6_fwd": 100.0})
+    assert "dominant_kernel" not in out
 
 
 def test_traffic_average_keeps_the_largest_grid(tmp_path):
@@ -91,8 +108,59 @@ def test_grid_stats_split_the_probe_from_the_headline_launches(tmp_path):
     assert bench.rollout_rocprof_k32(str(tmp_path / "none.json"), 65536, "f64") is None
 
 
-def test_bench_pmc_constants_follow_the_committed_rollout_pmc():
-    d = json.load(open(os.path.join(ROOT, "profiles", "r04_pmc_rollout.json")))
-    for k, v in bench.PMC_ROLLOUT_VALU_ACTIVE.items():
-        assert v == d[k]["valu_active_frac_of_wave_cycles"], k
-    assert d["actions_from_hbm"]["kernel"] == "env_rollout_ab_kernel"
+def test_pmc_valu_active_read_from_the_committed_summary():
+    p = os.path.join(ROOT, "profiles", "r04_pmc_rollout.json")
+    d = json.load(open(p))
+    v = bench.pmc_rollout_valu_active(p)
+    assert v["actions_from_hbm"] == d["actions_from_hbm"]["valu_active_frac_of_wave_cycles"]
+    assert bench.pmc_rollout_valu_active(os.path.join(ROOT, "profiles", "none.json")) == {}
+
+
+def test_kernel_source_hash_follows_the_sources(tmp_path, monkeypatch):
+    h = bench.kernel_source_hash()
+    assert len(h) == 64 and h == bench.kernel_source_hash()
+    # a copy of the source set with one byte changed hashes differently
+    import shutil
+    root = tmp_path / "r"
+    shutil.copytree(os.path.join(ROOT, "drone_rl_amd", "csrc"), root / "drone_rl_amd" / "csrc",
+                    ignore=shutil.ignore_patterns("build"))
+    (root / "include").mkdir()
+    shutil.copy(os.path.join(ROOT, "include", "dronerl.h"), root / "include" / "dronerl.h")
+    monkeypatch.setattr(bench, "ROOT", str(root))
+    assert bench.kernel_source_hash() == h
+    with open(root / "drone_rl_amd" / "csrc" / "trig.h", "a") as f:
+        f.write("\n")
+    assert bench.kernel_source_hash() != h
+
+
+def test_stale_profiles_go_to_committed_artefacts(tmp_path, monkeypatch):
+    prof = tmp_path / "p.json"
+    prof.write_text("{}")
+    prov = tmp_path / "provenance.json"
+    monkeypatch.setattr(bench, "PROVENANCE_JSON", str(prov))
+    monkeypatch.setattr(bench, "ARTEFACTS", {})
+    prov.write_text(json.dumps({"p.json": {"source_hash": "0" * 64}}))
+    assert bench.committed_or_stale("k", str(prof), {"mean_us": 1.0}) is None
+    assert bench.ARTEFACTS["k"]["stale"] and bench.ARTEFACTS["k"]["values"] == {"mean_us": 1.0}
+    prov.write_text(json.dumps({"p.json": {"source_hash": bench.kernel_source_hash()}}))
+    live = bench.committed_or_stale("k2", str(prof), 0.5)
+    assert live["value"] == 0.5 and live["provenance"]["matches_tree"]
+    assert "k2" not in bench.ARTEFACTS
+
+
+def test_every_committed_provenance_entry_names_a_profile():
+    d = json.load(open(bench.PROVENANCE_JSON))
+    for name, rec in d.items():
+        assert os.path.exists(os.path.join(ROOT, "profiles", name)), name
+        assert len(rec["source_hash"]) == 64
+
+
+def test_rollout_kernel_name_reads_the_knob_like_atoi(monkeypatch):
+    for v, ws in (("0", False), ("1", True), ("", False), ("false", False), (" 2x", True),
+                  ("-0", False)):
+        monkeypatch.setenv("DRONERL_ROLLOUT_WS", v)
+        name = bench.rollout_kernel_name(65536, 256, False)
+        assert name == ("env_rollout_ab_kernel" if ws else "env_rollout_kernel"), v
+    monkeypatch.delenv("DRONERL_ROLLOUT_WS")
+    assert bench.rollout_kernel_name(65536, 256, False) == "env_rollout_ab_kernel"
+    assert bench.rollout_kernel_name(1 << 22, 256, False) == "env_rollout_kernel"
