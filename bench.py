@@ -644,11 +644,12 @@ def ppo_kernel_times(tr, reps=20):
         a0, a1, gz = f._acts2[0], f._acts2[1], f._gz2[1]
         g = f._g2.view(-1)[:2 * M * 256].view(2, M, 256)
         ws = f._ws2
-        st = stream.cuda_stream
         iso["gemm_x6_fwd"] = graph_us(lambda: gemm_x6(a0, xw.fwd, a1))
         iso["gemm_x6_bwd"] = graph_us(lambda: gemm_x6(gz, xw.bwd, g))
+        # launched on the capturing stream (the current one inside graph_us)
         iso["gemm_x6_wgrad"] = graph_us(lambda: _lib.check(_lib.lib().dr_gemm_x6_wgrad(
-            2, M, f.C, gz.data_ptr(), a0.data_ptr(), ws.data_ptr(), st)))
+            2, M, f.C, gz.data_ptr(), a0.data_ptr(), ws.data_ptr(),
+            torch.cuda.current_stream(tr.device).cuda_stream)))
     return prefix, iso
 
 

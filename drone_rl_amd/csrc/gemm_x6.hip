@@ -128,9 +128,10 @@ __device__ inline uint32_t lds_addr(const uint8_t *p) {
 //
 // LDS: planes 2 x 48 KB (32 rows x 256 k x 3 planes, stored chunk-major:
 // the 16-B chunk c (8 k) of row r at c * 512 + 16 r, so the fragment reads'
-// lane groups (16 distinct rows of one chunk) and the split writes' (8
-// consecutive rows of one chunk) are conflict-free, and every address is a
-// per-lane base plus an immediate) + f32 staging 2 x 32 KB (wave w's 8 KB:
+// lane groups (16 distinct rows of one chunk) are conflict-free, and every
+// address is a per-lane base plus an immediate; the split writes' 16-lane
+// groups (8 rows of two adjacent chunks) are conflict-free because the odd
+// chunk's lanes write the other 8-B half of their slots, round 5) + f32 staging 2 x 32 KB (wave w's 8 KB:
 // piece i holds split chunks 4 i .. + 3 of its 8 rows, slot 32 h + 8 c' + r
 // = row r, chunk 4 i + c', float4 h) = 160 KB.
 //
@@ -260,8 +261,12 @@ __global__ __launch_bounds__(WS_THREADS, 1) void gemm_x6_ws_kernel(
     // staging: wave w's 8 rows of row step k in its 8 KB of slot k & 1.  Piece
     // i: lane L = 32 h + 8 c' + r loads float4 h of split chunk 4 i + c' of
     // row r (each row contributes 128 contiguous bytes per piece)
+    // Odd chunks are staged with their two float4 halves swapped (half shf ^ 1
+    // in slot half shf), so that the lanes splitting an odd chunk process its
+    // halves in the opposite order to their even-chunk neighbours (see
+    // wr_base below).
     const int sr = lane & 7, sc = (lane >> 3) & 3, shf = lane >> 5;
-    const uint32_t voff_f = (uint32_t)(sr * 1024 + 32 * sc + 16 * shf);
+    const uint32_t voff_f = (uint32_t)(sr * 1024 + 32 * sc + 16 * (shf ^ (sc & 1)));
     auto issue_rows = [&](int k) {
         const float *r0 = Ab + ((int64_t)(j0 + k * per) * WS_RS + 8 * w) * XK;
         uint8_t *dst = sh + WS_LDS_F + (k & 1) * WS_FSLOT + w * 8 * 1024;
@@ -270,13 +275,23 @@ __global__ __launch_bounds__(WS_THREADS, 1) void gemm_x6_ws_kernel(
     };
     // split unit u of row step k: lane L splits row L & 7 of the wave's 8,
     // chunk 8 u + (L >> 3) (pieces 2 u + (L >> 5), slots L & 31 and 32 + (L & 31)),
-    // in halves of 4 k (one float4 read, 3 ds_write_b64)
+    // in halves of 4 k (one float4 read, 3 ds_write_b64); half-unit hf of a
+    // lane whose chunk is odd is the chunk's half hf ^ 1 (the staging swap)
     const int rd_base = WS_LDS_F + w * 8 * 1024 + fh * 1024 + fr * 16;
     auto split_read = [&](int k, int u, int hf, float4 &v) {
         v = *reinterpret_cast<const float4 *>(sh + rd_base + (k & 1) * WS_FSLOT + u * 2048 +
                                               hf * 512);
     };
+    // ds_write_b64 banks are (a / 4) mod 32 over 16-lane groups: a group is 8
+    // rows of two adjacent chunks (512 B apart, the same banks), so with one
+    // half (8 B) of each 16-B slot written per instruction the two chunks hit
+    // the same 16 banks (2-way: the 1.67 M SQ_LDS_BANK_CONFLICT cycles per
+    // dispatch of profiles/r04_pmc_x6.json, = 1,024 waves x 17 row steps x 24
+    // writes x 4 groups).  Odd chunks write the other half in each
+    // instruction: 16 distinct 8-B positions of a 128-B bank row.
     const int wr_base = (lane >> 3) * 512 + (8 * w + sr) * 16;
+    const int wr_odd = (lane >> 3) & 1;
+    const int wr_half[2] = {wr_base + 8 * wr_odd, wr_base + 8 * (wr_odd ^ 1)};
     auto split_write = [&](int k, int u, int hf, const float4 &v) {
         const float x[4] = {v.x, v.y, v.z, v.w};
         uint32_t h[2], mm[2], l[2];
@@ -290,7 +305,7 @@ __global__ __launch_bounds__(WS_THREADS, 1) void gemm_x6_ws_kernel(
             mm[q] = pm;
             l[q] = pk_bf16(ra - lo_f(pm), rb - hi_f(pm));
         }
-        uint8_t *dst = sh + (k & 1) * WS_PSTAGE + wr_base + u * 8 * 512 + hf * 8;
+        uint8_t *dst = sh + (k & 1) * WS_PSTAGE + wr_half[hf] + u * 8 * 512;
         typedef uint32_t u32x2_t __attribute__((ext_vector_type(2)));
         *reinterpret_cast<u32x2_t *>(dst) = (u32x2_t){h[0], h[1]};
         *reinterpret_cast<u32x2_t *>(dst + WS_PLANE) = (u32x2_t){mm[0], mm[1]};
@@ -298,7 +313,7 @@ __global__ __launch_bounds__(WS_THREADS, 1) void gemm_x6_ws_kernel(
     };
     auto split_store = [&](int k, int u, int hf, uint32_t h0, uint32_t h1, uint32_t m0,
                            uint32_t m1, uint32_t l0, uint32_t l1) {
-        uint8_t *dst = sh + (k & 1) * WS_PSTAGE + wr_base + u * 8 * 512 + hf * 8;
+        uint8_t *dst = sh + (k & 1) * WS_PSTAGE + wr_half[hf] + u * 8 * 512;
         typedef uint32_t u32x2_t __attribute__((ext_vector_type(2)));
         *reinterpret_cast<u32x2_t *>(dst) = (u32x2_t){h0, h1};
         *reinterpret_cast<u32x2_t *>(dst + WS_PLANE) = (u32x2_t){m0, m1};
