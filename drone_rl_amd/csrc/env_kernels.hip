@@ -340,6 +340,41 @@ __device__ inline void gym_reset_regs(const EnvView<S> &v, int64_t i, int mode,
     DR_STAMP(7);
 }
 
+// The state DroneEnv.reset would start episode ep_old + 1 from (drone.py:
+// 48-75), formed from that episode's first Philox block r0 exactly as
+// gym_reset_regs forms it (the curriculum bump, then the draws, the same
+// expressions), so that a reset inside the split-physics rollout kernel is a
+// register copy of state prepared when the block was drawn, off the step in
+// which some lane of the wave resets (round 5).
+template <typename S>
+struct GymNext {
+    S px, py, tx, ty, tz;
+    double eps;               // eps after episode ep_old + 1's curriculum bump
+    bool bump;                // ep_old + 1 bumps the curriculum
+};
+template <typename S>
+__device__ inline GymNext<S> gym_next_reset(const EnvView<S> &v, uint64_t gid, int32_t ep_old,
+                                            double eps, const u32x4 &r0) {
+    const int32_t ep_new = ep_old + 1;
+    GymNext<S> g;
+    g.bump = ep_new % 2000 == 0;
+    if (g.bump) eps += 0.1;
+    double u4 = 0.0;
+    if (eps != 0.0) {
+        const u32x4 r1 = philox4x32_10(
+            u32x4{(uint32_t)ep_new, (uint32_t)gid, (uint32_t)(gid >> 32), TAG_RESET | 1u},
+            v.seed_lo, v.seed_hi);
+        u4 = u01_w32(r1.x);
+    }
+    g.px = (S)(u01_w32(r0.x) - 0.5);
+    g.py = (S)(u01_w32(r0.y) - 0.5);
+    g.tx = (S)(eps * u01_w32(r0.z));
+    g.ty = (S)(eps * u01_w32(r0.w));
+    g.tz = (S)(eps * u4 + 1.0 + 0.0);
+    g.eps = eps;
+    return g;
+}
+
 template <typename S>
 __device__ inline void vec_reset_regs(S st[F_N]) {
     // VectorizedDroneEnv.reset: every env at (0.1,0.1,0.1), at rest
@@ -1569,9 +1604,9 @@ __global__ __launch_bounds__(kAbThreads) void env_rollout_ab_kernel(EnvView<S> v
             }
             float *srow = &sh.obs[tp % kAbOut][ps * OD];
 #pragma unroll
-            for (int k = 0; k < 3; ++k) {
-                srow[F_EUL + k] = live ? (float)eul[k] : 0.f;
-                srow[F_OMG + k] = live ? (float)omg[k] : 0.f;
+            for (int k = 0; k < 3; ++k) {     // dead lanes' rows are never stored
+                srow[F_EUL + k] = (float)eul[k];
+                srow[F_OMG + k] = (float)omg[k];
             }
         };
         for (int t = 0; t < K; ++t) {
@@ -1639,10 +1674,18 @@ __global__ __launch_bounds__(kAbThreads) void env_rollout_ab_kernel(EnvView<S> v
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     bool reset_any = false, prev_rs = false;
     EnvView<S> vk = v;
-    u32x4 nd[1] = {};
+    // the next reset's state, prepared when its Philox block is drawn (once
+    // per group of kResetAhead steps for the lanes whose draw was used)
+    GymNext<S> nx = {};
     bool nd_ok = false;
     int32_t max_steps;
     asm volatile("v_mov_b32 %0, %1" : "=v"(max_steps) : "s"(v.max_steps));
+    auto draw_next = [&]() {
+        const u32x4 r0 = philox4x32_10(u32x4{(uint32_t)(ep_num + 1), (uint32_t)gid,
+                                             (uint32_t)(gid >> 32), TAG_RESET},
+                                       vk.seed_lo, vk.seed_hi);
+        nx = gym_next_reset(vk, gid, ep_num, eps, r0);
+    };
     asm volatile("s_barrier" ::: "memory");                          // B_(-1)
     for (int t = 0; t < K; ++t) {
         asm volatile("" : "+s"(vk.seed_lo), "+s"(vk.seed_hi));
@@ -1659,9 +1702,7 @@ __global__ __launch_bounds__(kAbThreads) void env_rollout_ab_kernel(EnvView<S> v
         }
         const MotorMix mx = motor_mix(a_cur);
         if (t % kResetAhead == 0 && !nd_ok) {
-            nd[0] = philox4x32_10(u32x4{(uint32_t)(ep_num + 1), (uint32_t)gid,
-                                        (uint32_t)(gid >> 32), TAG_RESET},
-                                  vk.seed_lo, vk.seed_hi);
+            draw_next();
             nd_ok = true;
         }
         // physics_step_mixed's translational part, in its order
@@ -1689,28 +1730,40 @@ __global__ __launch_bounds__(kAbThreads) void env_rollout_ab_kernel(EnvView<S> v
         step += 1;
         const bool done = live && (crash || (step >= max_steps));
         const bool rs = done && io.auto_reset;
-        if (rs) {
-            step = 0;
-            reset_any = true;
-            if (!nd_ok)
-                nd[0] = philox4x32_10(u32x4{(uint32_t)(ep_num + 1), (uint32_t)gid,
-                                            (uint32_t)(gid >> 32), TAG_RESET},
-                                      vk.seed_lo, vk.seed_hi);
-            gym_reset_regs(vk, i, 0, st, ep_num, eps, &nd[0]);
-            nd_ok = false;
-            ep_num += 1;
-            if (ep_num % 2000 == 0) eps += 0.1;
-        }
-        prev_rs = rs;
         const int so = t % kAbOut;
-        float *srow = &sh.obs[so][ps * OD];
-#pragma unroll
-        for (int k = 0; k < F_EUL; ++k) srow[k] = live ? (float)st[k] : 0.f;
-#pragma unroll
-        for (int k = 0; k < 3; ++k)
-            srow[12 + k] = live ? (float)(st[F_TGT + k] - st[F_POS + k]) : 0.f;
+        // staged before the reset: the squared distance is of the pre-reset
+        // position (otherwise the compiler sinks it below the reset branch and
+        // keeps both states live, with a copy of each per step)
         sh.d2[so][ps] = dist2;
         sh.done[so][ps] = (uint8_t)done;
+        if (rs) {
+            // gym_reset_regs on the prepared state (a second reset within
+            // the group draws here, as the reset itself would)
+            step = 0;
+            reset_any = true;
+            if (!nd_ok) draw_next();
+            ep_num += 1;
+            vk.ep_num[i] = ep_num;
+            eps = nx.eps;
+            if (nx.bump) vk.eps[i] = eps;
+            st[F_POS + 0] = nx.px;
+            st[F_POS + 1] = nx.py;
+            st[F_POS + 2] = (S)1.0;
+#pragma unroll
+            for (int k = F_VEL; k < F_VEL + 3; ++k) st[k] = (S)0;
+            st[F_TGT + 0] = nx.tx;
+            st[F_TGT + 1] = nx.ty;
+            st[F_TGT + 2] = nx.tz;
+            nd_ok = false;
+        }
+        prev_rs = rs;
+        float *srow = &sh.obs[so][ps * OD];
+        // a dead lane's (i >= n) row is staged but never stored (the memory
+        // wave stores the live rows only), so it needs no zeroing
+#pragma unroll
+        for (int k = 0; k < F_EUL; ++k) srow[k] = (float)st[k];
+#pragma unroll
+        for (int k = 0; k < 3; ++k) srow[12 + k] = (float)(st[F_TGT + k] - st[F_POS + k]);
         __builtin_amdgcn_sched_barrier(0);
         asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");   // B_t
     }
