@@ -336,7 +336,7 @@ def time_env(args, dtype_name, n_envs, rank, world, device, steps, warmup, varia
             for t in range(warmup, total):
                 b.step(acts[t])
         ev1.record(stream)
-    span = timed_region(work, lambda: torch.cuda.synchronize(device), world)
+    span = timed_region(work, torch.cuda.synchronize, world)
     tm = node_timing(gather_spans((*span, round(ev0.elapsed_time(ev1) * 1e6)), world, device))
     elapsed, gpu_ms = tm["wall_s"], tm["gpu_ms"]
     # sanity: the env is alive (episodes end and reset under a random policy)
@@ -446,8 +446,17 @@ def time_headline(args, n_envs, rank, world, device, steps, warmup, kmax):
         ev0.record(stream)
         timed()
         ev1.record(stream)
+    if g is None:
+        # one untimed rehearsal of the whole timed region (event records,
+        # launch, synchronize; the env runs those steps again on the same
+        # actions).  Round 5: the single timed launch read 41.3-42.3 us of
+        # wall where repetitions of the identical sequence in one process
+        # have a 37-39 us median (scripts/micro/host_wait.py); with this
+        # rehearsal and the no-argument torch.cuda.synchronize (no device-
+        # guard switch around it) it reads 38.1-39.2 us (3 runs, one box)
+        timed_region(work, torch.cuda.synchronize, world)
     gc.disable()
-    span = timed_region(work, lambda: torch.cuda.synchronize(device), world)
+    span = timed_region(work, torch.cuda.synchronize, world)
     gc.enable()
     if g is None and any(rcs):
         from drone_rl_amd._lib import check
@@ -798,7 +807,7 @@ def time_ppo(args, rank, world, device, force_dp=False, dp_graph=False, profile=
     def work():
         for _ in range(K):
             last[:] = [tr.learn_step()]
-    span = timed_region(work, lambda: torch.cuda.synchronize(device), world)
+    span = timed_region(work, torch.cuda.synchronize, world)
     el = node_timing(gather_spans((*span, 0), world, device))["wall_s"]
     st = last[0]
     es =tr.episode_stats()

@@ -7,7 +7,11 @@ value (the XDL write -> VALU / VMEM access hazard).  This CPU test compiles
 the kernel to gfx950 assembly and checks every such access: between the asm
 MFMA that last wrote a register and any non-MFMA-asm access to it there must
 be at least WAIT independent wait states (one per instruction, s_nop N counts
-N + 1)."""
+N + 1).  The other direction is checked too (advisor r04): a compiler VALU
+write (v_mov, v_accvgpr_write, ...) of a register that a later asm MFMA reads
+as its A, B or C operand needs VALU_WAIT wait states before that MFMA, which
+the compiler cannot pad either, since it does not see the MFMA inside the
+asm statement."""
 import os
 import re
 import shutil
@@ -22,18 +26,29 @@ KERNEL = "gemm_x6_ws_kernel"
 # XDL (v_mfma_f32_32x32x16_bf16, 8 passes on gfx950) write VGPR -> VALU, VMEM
 # or LDS access of it: 11 wait states on gfx940-class parts; checked with margin
 WAIT = 18
+# VALU (or v_accvgpr_write) write of a VGPR / AGPR -> an MFMA reading it as
+# SrcA / SrcB / SrcC: 2 wait states on gfx940-class parts (the CDNA3/4 ISA
+# manual's required-NOPs table); checked with margin
+VALU_WAIT = 4
 
 _VREG = re.compile(r"\bv\[(\d+):(\d+)\]|\bv(\d+)\b")
+_AREG = re.compile(r"\ba\[(\d+):(\d+)\]|\ba(\d+)\b")
 
 
-def _regs(text):
+def _regs(text, pat=_VREG, tag=""):
     out = set()
-    for m in _VREG.finditer(text):
+    for m in pat.finditer(text):
         if m.group(1) is not None:
-            out.update(range(int(m.group(1)), int(m.group(2)) + 1))
+            out.update(tag + str(r) if tag else r for r in range(int(m.group(1)),
+                                                                 int(m.group(2)) + 1))
         else:
-            out.add(int(m.group(3)))
+            out.add(tag + m.group(3) if tag else int(m.group(3)))
     return out
+
+
+def _any_regs(text):
+    """VGPRs as 'v<n>' and AGPRs as 'a<n>'."""
+    return _regs(text, _VREG, "v") | _regs(text, _AREG, "a")
 
 
 def _kernel_asm():
@@ -59,6 +74,7 @@ def _kernel_asm():
 def _scan(lines):
     """(number of asm MFMAs, list of violations) for an assembly listing."""
     pending = {}           # register -> wait states elapsed since its MFMA write
+    written = {}           # register -> wait states since a compiler VALU wrote it
     in_asm = False
     n_mfma = 0
     bad = []
@@ -75,11 +91,20 @@ def _scan(lines):
         op = l.split()[0]
         if in_asm and op.startswith("v_mfma"):
             n_mfma += 1
-            dst = _regs(l[len(op):].split(",")[0])
+            ops = l[len(op):].split(",")
+            for r in sorted(_any_regs(",".join(ops[1:])) & set(written)):
+                if written[r] < VALU_WAIT:
+                    bad.append(f"line {i}: asm '{l}' reads {r} {written[r]} wait states after "
+                               f"a compiler VALU wrote it")
+            dst = _regs(ops[0])
             for r in list(pending):
                 pending[r] += 1
             for r in dst:
                 pending[r] = 0
+            for r in list(written):
+                written[r] += 1
+                if written[r] >= VALU_WAIT:
+                    del written[r]
             continue
         step = int(l.split()[1]) + 1 if op == "s_nop" else 1
         if not in_asm:
@@ -91,6 +116,14 @@ def _scan(lines):
             pending[r] += step
             if pending[r] >= WAIT:
                 del pending[r]
+        for r in list(written):
+            written[r] += step
+            if written[r] >= VALU_WAIT:
+                del written[r]
+        if not in_asm and op.startswith("v_") and not op.startswith(("v_cmp", "v_readlane",
+                                                                      "v_readfirstlane")):
+            for r in _any_regs(l[len(op):].split(",")[0]):
+                written[r] = 0
     return n_mfma, bad
 
 
@@ -113,6 +146,26 @@ def test_scanner_flags_a_copy_right_after_an_asm_mfma():
 """.splitlines()
     n, bad = _scan(lines)
     assert n == 2 and len(bad) == 2 and "v14" in bad[0] and "v15" in bad[1]
+
+
+def test_scanner_flags_an_operand_written_right_before_an_asm_mfma():
+    """A compiler write of an MFMA source (here the A fragment v178 and the
+    AGPR weight a77) with no wait states before the asm MFMA that reads it."""
+    lines = """\
+\tv_mov_b32_e32 v178, v3
+\tv_accvgpr_write_b32 a77, v4
+\t;;#ASMSTART
+\tv_mfma_f32_32x32x16_bf16 v[0:15], v[178:181], a[76:79], v[0:15]
+\t;;#ASMEND
+\tv_mov_b32_e32 v200, v250
+\ts_nop 4
+\t;;#ASMSTART
+\tv_mfma_f32_32x32x16_bf16 v[32:47], v[198:201], a[76:79], v[32:47]
+\t;;#ASMEND
+""".splitlines()
+    n, bad = _scan(lines)
+    assert n == 2 and len(bad) == 2, bad
+    assert any("reads v178" in b for b in bad) and any("reads a77" in b for b in bad)
 
 
 def test_no_compiler_access_to_asm_mfma_results_without_wait_states():
