@@ -4,7 +4,7 @@
 # whole GPU suite on the working tree.  Usage: r5_rollout_ab.sh TAG [nosuite]
 cd "$(dirname "$0")/../.."
 T=${1:-r5c}; O=gpurun_out/$T; mkdir -p $O
-B=$PWD/scripts/micro/build/lib_base.so
+B=$PWD/scripts/micro/build/lib_${BASE:-base}.so
 export PYTHONPATH=$PWD
 if [ "$2" != "nosuite" ]; then
   timeout -k 10 400 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread > $O/suite.log 2>&1 || { tail -30 $O/suite.log; exit 1; }
