@@ -654,7 +654,16 @@ def ppo_kernel_times(tr, reps=20):
         g = f._g2.view(-1)[:2 * M * 256].view(2, M, 256)
         ws = f._ws2
         iso["gemm_x6_fwd"] = graph_us(lambda: gemm_x6(a0, xw.fwd, a1))
-        iso["gemm_x6_bwd"] = graph_us(lambda: gemm_x6(gz, xw.bwd, g))
+        if getattr(f, "_ximg", None) is not None:
+            # the fused input-gradient GEMM + first-layer backward (its
+            # level-1 partial sums included: the entry's two launches)
+            iso["gemm_x6_bwd_first"] = graph_us(lambda: _lib.check(
+                _lib.lib().dr_gemm_x6_bwd_first(
+                    2, M, 15, gz.data_ptr(), xw.bwd.data_ptr(), a0.data_ptr(),
+                    f._ximg.data_ptr(), f._first.ws.data_ptr(), f._first.ws.numel(),
+                    torch.cuda.current_stream(tr.device).cuda_stream)))
+        else:
+            iso["gemm_x6_bwd"] = graph_us(lambda: gemm_x6(gz, xw.bwd, g))
         # launched on the capturing stream (the current one inside graph_us)
         iso["gemm_x6_wgrad"] = graph_us(lambda: _lib.check(_lib.lib().dr_gemm_x6_wgrad(
             2, M, f.C, gz.data_ptr(), a0.data_ptr(), ws.data_ptr(),
@@ -667,7 +676,8 @@ PPO_KERNEL_NAMES = {"gather_minibatch": "gather_minibatch_kernel",
                     "linear_tanh": "linear_tanh_kernel", "ppo_head": "ppo_head_kernel",
                     "first_layer_bwd": "first_layer_bwd_kernel",
                     "gemm_x6_fwd": "gemm_x6_ws_kernel", "gemm_x6_bwd": "gemm_x6_ws_kernel",
-                    "gemm_x6_wgrad": "gemm_x6_wgrad_kernel", "split_weights": "split_weights_kernel"}
+                    "gemm_x6_wgrad": "gemm_x6_wgrad_kernel", "split_weights": "split_weights_kernel",
+                    "split_x": "split_x_kernel", "gemm_x6_bwd_first": "gemm_x6_fl_kernel"}
 
 
 def rollout_rocprof_k32(path, n, state_dtype):
@@ -728,13 +738,17 @@ def ppo_roofline(cfg, s_per_update, ktimes, rocprof=None, isolated=None, rocprof
     rows = {"gather_minibatch": 2 * (15 + 4 + 3) * 4,
             "linear_tanh": 15 * 4 + 2 * 256 * 4,
             "ppo_head": 2 * 1024 + 2 * 1024 + 44,
-            "first_layer_bwd": 2 * 2 * 1024 + 60}
+            "first_layer_bwd": 2 * 2 * 1024 + 60,
+            "split_x": 15 * 4 + 3136 // 32}            # x in, its three-plane record out
+    # the fused input-gradient GEMM also runs the first layer's weight
+    # gradient (16 x 256 per net and row, features + bias) as x6 MFMA work
+    fl_flop = gemm_flop + 2 * 2 * M * 16 * 256
     kern = {}
     rocprof = rocprof or {}
     isolated = isolated or {}
 
-    def mfma_frac(us):
-        return round(6 * gemm_flop / (us * 1e-6) / 1e12 / BF16_DENSE_PEAK_TFLOPS, 4)
+    def mfma_frac(us, flop=gemm_flop):
+        return round(6 * flop / (us * 1e-6) / 1e12 / BF16_DENSE_PEAK_TFLOPS, 4)
 
     def hbm_frac(name, us):
         return round(rows[name] * M / (us * 1e-6) / 1e9 / HBM_PEAK_GBS, 4)
@@ -746,12 +760,13 @@ def ppo_roofline(cfg, s_per_update, ktimes, rocprof=None, isolated=None, rocprof
             # (rocprofv3; the forward / input-gradient GEMM share one kernel)
             e["rocprof_us"] = round(rp, 2)
         if name.startswith("gemm_x6"):
-            e.update({"bound": "mfma", "prefix_split_frac": mfma_frac(us)})
+            fl = fl_flop if name == "gemm_x6_bwd_first" else gemm_flop
+            e.update({"bound": "mfma", "prefix_split_frac": mfma_frac(us, fl)})
             if name in isolated:
                 e.update({"isolated_us": round(isolated[name], 2),
-                          "isolated_frac": mfma_frac(isolated[name])})
+                          "isolated_frac": mfma_frac(isolated[name], fl)})
             if rp is not None:
-                e["rocprof_frac"] = mfma_frac(rp)
+                e["rocprof_frac"] = mfma_frac(rp, fl)
         elif name in rows:
             e.update({"bound": "hbm", "bytes": rows[name] * M,
                       "prefix_split_frac": hbm_frac(name, us)})

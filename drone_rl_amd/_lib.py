@@ -23,7 +23,7 @@ DR_ERR_HIP = -2
 DR_ERR_NOMEM = -3
 DR_ERR_UNSUPPORTED = -4
 
-ABI_VERSION = 14                # DR_ABI_VERSION in include/dronerl.h
+ABI_VERSION = 15                # DR_ABI_VERSION in include/dronerl.h
 DR_VARIANT_GYM = 0
 DR_VARIANT_VECTORIZED = 1
 DR_VARIANT_MOVING = 2
@@ -140,6 +140,10 @@ SIGNATURES = {
     "dr_gemm_x6_split_weights": (c_int, [c_int64, _P, c_int, _P, _P]),
     "dr_gemm_x6": (c_int, [c_int64, c_int64, _P, _P, _P, _P]),
     "dr_gemm_x6_wgrad": (c_int, [c_int64, c_int64, c_int64, _P, _P, _P, _P]),
+    "dr_gemm_x6_x_bytes": (c_size_t, [c_int64]),
+    "dr_gemm_x6_split_x": (c_int, [c_int64, c_int64, _P, _P, _P]),
+    "dr_gemm_x6_bwd_first": (c_int, [c_int64, c_int64, c_int64, _P, _P, _P, _P, _P, c_size_t,
+                                     _P]),
 }
 
 _lib = None

@@ -691,12 +691,336 @@ __global__ __launch_bounds__(XTHREADS) void gemm_x6_wgrad_kernel(
         }
 }
 
+// ---------------------------------------------------------------------------
+// dr_gemm_x6_bwd_first (round 5): the 256 x 256 layer's input gradient with
+// the first layer's backward fused into its epilogue.  The unfused step wrote
+// grad_h1 = grad_z2 W1 (134 MB for both nets at 65,536 rows) and
+// first_layer_bwd_kernel read it back with h1 (268 MB) to form
+// grad_z1 = grad_h1 (1 - h1^2), the 256 x 15 weight gradient grad_z1^T x and
+// the bias gradient.  Here each output tile's grad_h1 stays in registers:
+// the epilogue loads h1 (the only extra traffic, 134 MB), forms grad_z1,
+// splits it exactly into three bf16 planes (the x6 scheme) and accumulates
+// D2 = X^T grad_z1 on the matrix cores, X the minibatch observations with a
+// constant 1 as a 16th feature (so D2's feature-15 row is the bias gradient).
+// A block writes its D2 once, as one partial row of first_layer_bwd_kernel's
+// partial layout, and the step's existing level-1 / level-2 sums finish it.
+//
+// D2 orientation: the MFMA's A operand is X^T (M = feature, K = rows), its B
+// operand is grad_z1 (K = rows, N = columns).  The main GEMM's accumulator
+// layout gives lane (fr, fh) column fr and rows 8 (r >> 2) + 4 fh + (r & 3),
+// r = 0..15: registers 8 j .. 8 j + 7 are exactly the B fragment of K step j
+// (K index 8 fh + e <-> row 16 j + 4 fh + (e & 3) + 8 (e >> 2)), so grad_z1
+// needs no data movement.  The two column tiles of a wave share one
+// 32 x 32 accumulator: tile 0's features in D2 rows 0..15, tile 1's in rows
+// 16..31 (each tile's A fragment is zero in the other half), 16 registers for
+// the wave's 64 columns x 16 features.
+//
+// Registers: the weights' h and m planes stay in AGPRs as in
+// gemm_x6_ws_kernel, but the l plane is streamed from L2 (one 1-KB fragment
+// per k16 step, two steps ahead) to make room for the epilogue, and the
+// activation rows are register-staged by compiler-tracked loads four split
+// half-units ahead (no LDS-DMA staging: every vector memory op is visible to
+// the compiler's waitcnt pass).  LDS holds only the double-buffered planes.
+constexpr int FL_F = 16;                                // 15 features + the bias column
+constexpr int XREC = 64 + 3 * 2 * 2 * FL_F * 16;         // 3,136 B of X planes per row step
+
+// byte offset in a row step's X record of plane p, K step j, half fh,
+// feature f: the 8 bf16 K values of A-fragment lane (f or 16 + f, fh)
+__host__ __device__ inline int xrec_off(int p, int j, int fh, int f) {
+    return 64 + (((p * 2 + j) * 2 + fh) * FL_F + f) * 16;
+}
+
+// X planes image: one thread per (row step g, K step j, half fh, feature f),
+// the rows 16 j + 4 fh + (e & 3) + 8 (e >> 2), e = 0..7, of feature f of x
+// (m x k f32 row-major; feature 15 is the constant 1), split exactly like
+// the GEMM operands; the record's first 64 B are zero (the A fragment of the
+// other column tile's lanes).
+__global__ __launch_bounds__(256) void split_x_kernel(const float *__restrict__ x, int64_t m,
+                                                      int k, uint8_t *__restrict__ img) {
+    const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    const int64_t g = t >> 6;
+    if (g >= m / WS_RS) return;
+    const int f = (int)(t & 15), fh = (int)((t >> 4) & 1), j = (int)((t >> 5) & 1);
+    uint8_t *rec = img + g * XREC;
+    if ((t & 63) < 4) reinterpret_cast<u32x4_t *>(rec)[t & 3] = (u32x4_t){0u, 0u, 0u, 0u};
+    float v[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+        const int64_t row = g * WS_RS + 16 * j + 4 * fh + (e & 3) + 8 * (e >> 2);
+        v[e] = f < k ? x[row * k + f] : (f == FL_F - 1 ? 1.0f : 0.0f);
+    }
+    u32x4_t h, mm, l;
+    split8(v, h, mm, l);
+    *reinterpret_cast<u32x4_t *>(rec + xrec_off(0, j, fh, f)) = h;
+    *reinterpret_cast<u32x4_t *>(rec + xrec_off(1, j, fh, f)) = mm;
+    *reinterpret_cast<u32x4_t *>(rec + xrec_off(2, j, fh, f)) = l;
+}
+
+__global__ __launch_bounds__(WS_THREADS, 1) void gemm_x6_fl_kernel(
+    const float *__restrict__ A, const uint8_t *__restrict__ img, const float *__restrict__ H,
+    const uint8_t *__restrict__ ximg, float *__restrict__ part, int64_t m, int batch) {
+    __shared__ __attribute__((aligned(16))) uint8_t sh[2 * WS_PSTAGE];
+    const int lane = threadIdx.x & 63;
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int b = (int)blockIdx.x % batch;
+    const int per = (int)gridDim.x / batch;
+    const int j0 = (int)blockIdx.x / batch;
+    const int steps_net = (int)(m / WS_RS);
+    const int R = (steps_net - j0 + per - 1) / per;
+    const float *Ab = A + (int64_t)b * m * XK;
+    const float *Hb = H + (int64_t)b * m * XN;
+    const int fr = lane & 31, fh = lane >> 5;
+
+    // every load goes through a buffer resource (an SGPR base, one per-lane
+    // offset register, the rest in SGPR / immediate offsets): the address
+    // arithmetic of plain loads cost registers this kernel does not have
+    constexpr int kBufFlags = 0x00020000;
+    const __amdgpu_buffer_rsrc_t wrs =
+        __builtin_amdgcn_make_buffer_rsrc((void *)(img + (int64_t)b * W_IMG), 0, (int)W_IMG,
+                                          kBufFlags);
+    const int lane16 = lane * 16;
+    auto wfrag = [&](int t, int s, int p) {
+        return __builtin_bit_cast(
+            bf16x8_t, __builtin_amdgcn_raw_buffer_load_b128(
+                          wrs, lane16, (((w * 2 + t) * 16 + s) * 3 + p) * W_FRAG, 0));
+    };
+    // the weights' h and m planes in AGPRs (gemm_x6_ws_kernel's layout)
+    bf16x8_t Wa[2][16][2];
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int s = 0; s < 16; ++s) {
+            Wa[j][s][0] = wfrag(j, s, 0);
+            Wa[j][s][1] = wfrag(j, s, 1);
+        }
+    // the l plane's fragment of global k16 step g (tile g >> 4, step g & 15):
+    // a ring of 4, loaded two steps ahead
+    auto wl_load = [&](int g) { return wfrag((g >> 4) & 1, g & 15, 2); };
+    bf16x8_t wl[4];
+    wl[0] = wl_load(0);
+    wl[1] = wl_load(1);
+
+    // activation staging: lane L splits row L & 7 of the wave's 8 rows,
+    // chunk 8 u + (L >> 3), half hf ^ (chunk & 1) (the conflict-free split
+    // writes of gemm_x6_ws_kernel), as a float4 register loaded four split
+    // half-units ahead; half-unit q = 2 u + hf of row step k (clamped to the
+    // last step: such rows are split into the unused plane buffer, never read)
+    const int sr = lane & 7, sch = lane >> 3, sodd = sch & 1;
+    // byte offset of the lane's float4 of half-unit hf within the wave's 8 rows
+    const int soff[2] = {sr * 1024 + 32 * sch + 16 * sodd, sr * 1024 + 32 * sch + 16 * (sodd ^ 1)};
+    auto stage_load = [&](int k, int q) {
+        const int kk = k < R ? k : R - 1;
+        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+            (void *)(Ab + ((int64_t)(j0 + kk * per) * WS_RS + 8 * w) * XK), 0, 8 * XK * 4,
+            kBufFlags);
+        return __builtin_bit_cast(
+            float4, __builtin_amdgcn_raw_buffer_load_b128(rs, soff[q & 1], 256 * (q >> 1), 0));
+    };
+    const int wr_base = sch * 512 + (8 * w + sr) * 16;
+    const int wr_half[2] = {wr_base + 8 * sodd, wr_base + 8 * (sodd ^ 1)};
+    auto split_store = [&](int k, int q, const float4 &v) {
+        uint32_t h[2], mm[2], l[2];
+        const float x[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int p = 0; p < 2; ++p) {
+            const float a = x[2 * p], c = x[2 * p + 1];
+            const uint32_t ph = pk_bf16(a, c);
+            const float ra = a - lo_f(ph), rc = c - hi_f(ph);
+            const uint32_t pm = pk_bf16(ra, rc);
+            h[p] = ph;
+            mm[p] = pm;
+            l[p] = pk_bf16(ra - lo_f(pm), rc - hi_f(pm));
+        }
+        uint8_t *dst = sh + (k & 1) * WS_PSTAGE + wr_half[q & 1] + (q >> 1) * 8 * 512;
+        typedef uint32_t u32x2_t __attribute__((ext_vector_type(2)));
+        *reinterpret_cast<u32x2_t *>(dst) = (u32x2_t){h[0], h[1]};
+        *reinterpret_cast<u32x2_t *>(dst + WS_PLANE) = (u32x2_t){mm[0], mm[1]};
+        *reinterpret_cast<u32x2_t *>(dst + 2 * WS_PLANE) = (u32x2_t){l[0], l[1]};
+    };
+    typedef bf16x8_t AFrag[3];
+    const int fr_base = fh * 512 + fr * 16;
+    auto read_frag = [&](int k, int s, AFrag &f) {
+        const uint8_t *src = sh + (k & 1) * WS_PSTAGE + fr_base + s * 1024;
+#pragma unroll
+        for (int p = 0; p < 3; ++p) f[p] = *reinterpret_cast<const bf16x8_t *>(src + p * WS_PLANE);
+    };
+    f32x16_t acc_h[2], acc_l[2];
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+        acc_h[t] = (f32x16_t){};
+        acc_l[t] = (f32x16_t){};
+    }
+    auto finish_tile = [&](int t) {
+        asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
+        acc_h[t] = acc_h[t] + acc_l[t];
+    };
+
+    // ---- the epilogue: grad_z1 of tile tt of row step kk into D2 ----
+    f32x16_t d2 = (f32x16_t){};
+    float hv[16];
+    const int hoff[2] = {(4 * fh * XN + 64 * w + fr) * 4, (4 * fh * XN + 64 * w + 32 + fr) * 4};
+    auto h_load = [&](int kk, int tt, int r) {
+        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+            (void *)(Hb + (int64_t)(j0 + kk * per) * WS_RS * XN), 0, WS_RS * XN * 4, kBufFlags);
+        hv[r] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(
+            rs, hoff[tt], (8 * (r >> 2) + (r & 3)) * XN * 4, 0));
+    };
+    // lane (m = fr, fh) of X^T's fragment: feature fr & 15 of column tile
+    // fr >> 4; the other tile's lanes load from past the record's end, which
+    // the buffer range check returns as zeros
+    const int xoff[2] = {(fr >> 4) == 0 ? xrec_off(0, 0, fh, fr & 15) : 0x7ff00000,
+                         (fr >> 4) == 1 ? xrec_off(0, 0, fh, fr & 15) : 0x7ff00000};
+    auto x_frag = [&](int kk, int tt, int j, bf16x8_t (&xf)[3]) {
+        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+            (void *)(ximg + (int64_t)(j0 + kk * per) * XREC), 0, XREC, kBufFlags);
+#pragma unroll
+        for (int p = 0; p < 3; ++p)
+            xf[p] = __builtin_bit_cast(bf16x8_t, __builtin_amdgcn_raw_buffer_load_b128(
+                                                     rs, xoff[tt], (p * 2 + j) * 512, 0));
+    };
+    // grad_z1 = grad_h1 (1 - h1^2) (first_layer_bwd_kernel's expression) of
+    // registers 8 j .. 8 j + 7 of tile tt, split into the B fragment planes,
+    // and the six x6 products into D2
+    auto d2_kstep = [&](int tt, int j, const bf16x8_t (&xf)[3]) {
+        float gz[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+            const float y = hv[8 * j + e];
+            gz[e] = acc_h[tt][8 * j + e] * (1.0f - y * y);
+        }
+        u32x4_t gh, gm, gl;
+        split8(gz, gh, gm, gl);
+        const bf16x8_t bh = __builtin_bit_cast(bf16x8_t, gh);
+        const bf16x8_t bm = __builtin_bit_cast(bf16x8_t, gm);
+        const bf16x8_t bl = __builtin_bit_cast(bf16x8_t, gl);
+        // one asm statement: D2 stays in VGPRs (the builtin's accumulator
+        // took 16 AGPRs, evicting a weight fragment to VGPRs and a copy back
+        // before each use), and no compiler VALU lands between the MFMAs;
+        // s_nop 4 covers the VALU writes of bh, bm, bl -> SrcB reads
+        asm volatile("s_nop 4\n\t"
+                     "v_mfma_f32_32x32x16_bf16 %0, %1, %4, %0\n\t"
+                     "v_mfma_f32_32x32x16_bf16 %0, %1, %5, %0\n\t"
+                     "v_mfma_f32_32x32x16_bf16 %0, %2, %4, %0\n\t"
+                     "v_mfma_f32_32x32x16_bf16 %0, %1, %6, %0\n\t"
+                     "v_mfma_f32_32x32x16_bf16 %0, %3, %4, %0\n\t"
+                     "v_mfma_f32_32x32x16_bf16 %0, %2, %5, %0"
+                     : "+v"(d2)
+                     : "v"(xf[0]), "v"(xf[1]), "v"(xf[2]), "v"(bh), "v"(bm), "v"(bl));
+    };
+
+    // ---- prologue: step 0's planes, the staging ring for step 1 ----
+    {
+        float4 v0[8];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) v0[q] = stage_load(0, q);
+#pragma unroll
+        for (int q = 0; q < 8; ++q) split_store(0, q, v0[q]);
+    }
+    float4 stg[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) stg[q] = stage_load(1, q);
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    constexpr int NF = 3;                     // fragment sets (two steps ahead)
+    AFrag fb[NF];
+    read_frag(0, 0, fb[0]);
+    read_frag(0, 1, fb[1]);
+    bf16x8_t xf0[3], xf1[3];
+
+    // Row step k, per wave: phase t runs column tile t's 16 k16 steps (96 x6
+    // MFMAs) and the epilogue of the other tile (tile 1 of step k - 1 in
+    // phase 0, tile 0 of step k in phase 1): its h1 rows loaded at k16 steps
+    // 0..7, X fragments of K step 0 at 2 and of K step 1 at 8, grad_z1 and
+    // the D2 MFMAs of K step 0 at 9 and of K step 1 at 13.  Split half-unit
+    // q of step k + 1 at steps 4 q' + 1 (q' = q - 4 t), the staging load of
+    // half-unit q + 4 behind it.  Step 0's phase-0 epilogue is of the zeroed
+    // tile 1: D2 += 0.
+    auto row_step = [&](int k) {
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+            const int tt = 1 - t;
+            const int kk = t == 0 ? (k > 0 ? k - 1 : 0) : k;
+            finish_tile(tt);
+#pragma unroll
+            for (int s = 0; s < 16; ++s) {
+                const int g = 16 * t + s;
+                if (g + 2 < 32) read_frag(k, (g + 2) & 15, fb[(g + 2) % NF]);
+                wl[(g + 2) & 3] = wl_load(g + 2);
+                const AFrag &x = fb[g % NF];
+                mfma_x6_group(s == 0, acc_h[t], acc_l[t], x[0], x[1], x[2], Wa[t][s][0],
+                              Wa[t][s][1], wl[g & 3]);
+                if (s < 8) {
+                    h_load(kk, tt, 2 * s);
+                    h_load(kk, tt, 2 * s + 1);
+                }
+                if (s == 2) x_frag(kk, tt, 0, xf0);
+                if (s == 6) x_frag(kk, tt, 1, xf1);
+                if (s == 9) d2_kstep(tt, 0, xf0);
+                if (s == 13) d2_kstep(tt, 1, xf1);
+                if ((s & 3) == 1) {
+                    const int q = 4 * t + (s >> 2);
+                    split_store(k + 1, q, stg[q & 3]);
+                    stg[q & 3] = stage_load(q + 4 < 8 ? k + 1 : k + 2, (q + 4) & 7);
+                }
+            }
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        read_frag(k + 1, 0, fb[0]);
+        read_frag(k + 1, 1, fb[1]);
+    };
+    for (int k = 0; k < R; ++k) row_step(k);
+    // tile 1 of the last row step
+    if (R > 0) {
+        finish_tile(1);
+#pragma unroll
+        for (int r = 0; r < 16; ++r) h_load(R - 1, 1, r);
+        x_frag(R - 1, 1, 0, xf0);
+        x_frag(R - 1, 1, 1, xf1);
+        d2_kstep(1, 0, xf0);
+        d2_kstep(1, 1, xf1);
+    }
+    // D2 -> this block's partial row (first_layer_bwd_kernel's layout:
+    // [feature * 256 + column], row j0 * batch + b)
+    float *out = part + ((int64_t)j0 * batch + b) * (FL_F * XN);
+    asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");   // D2's asm MFMA writes
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        const int mrow = 8 * (r >> 2) + 4 * fh + (r & 3);
+        out[(mrow & 15) * XN + 64 * w + 32 * (mrow >> 4) + fr] = d2[r];
+    }
+}
+
 int fail_g(int code, const std::string &msg) {
     set_global_error(msg);
     return code;
 }
 
 }  // namespace
+
+// Launchers of the fused input-gradient + first-layer backward (the C ABI
+// entry dr_gemm_x6_bwd_first in ppo_kernels.hip adds the level-1 partial sum
+// in the first-layer workspace layout).
+size_t gemm_x6_x_bytes(int64_t m) { return m < WS_RS ? 0 : (size_t)(m / WS_RS) * XREC; }
+
+int gemm_x6_split_x_launch(int64_t m, int k, const float *x, void *ximg, hipStream_t st) {
+    const int64_t threads = (m / WS_RS) * 64;
+    hipLaunchKernelGGL(split_x_kernel, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, st,
+                       x, m, k, static_cast<uint8_t *>(ximg));
+    return hipGetLastError() == hipSuccess ? DR_OK : DR_ERR_HIP;
+}
+
+// returns the blocks per net (the partial rows written), or -1
+int gemm_x6_fl_launch(int batch, int64_t m, const float *gz, const void *img, const float *h,
+                      const void *ximg, float *part, hipStream_t st) {
+    const int n_cu = device_cu_count();
+    const int units = (int)(batch * (m / WS_RS));
+    int grid = units < n_cu ? units : n_cu;
+    grid -= grid % batch;
+    hipLaunchKernelGGL(gemm_x6_fl_kernel, dim3(grid), dim3(WS_THREADS), 0, st, gz,
+                       static_cast<const uint8_t *>(img), h, static_cast<const uint8_t *>(ximg),
+                       part, m, batch);
+    return hipGetLastError() == hipSuccess ? grid / batch : -1;
+}
+
 }  // namespace dr
 
 using namespace dr;

@@ -2327,6 +2327,68 @@ static int launch_first_bwd(const char *who, int nets, int64_t m, int64_t k, int
     return check_launch(who);
 }
 
+extern "C++" {
+namespace dr {   // gemm_x6.hip
+size_t gemm_x6_x_bytes(int64_t m);
+int gemm_x6_split_x_launch(int64_t m, int k, const float *x, void *ximg, hipStream_t st);
+int gemm_x6_fl_launch(int batch, int64_t m, const float *gz, const void *img, const float *h,
+                      const void *ximg, float *part, hipStream_t st);
+}  // namespace dr
+}
+
+size_t dr_gemm_x6_x_bytes(int64_t m) { return gemm_x6_x_bytes(m); }
+
+int dr_gemm_x6_split_x(int64_t m, int64_t k, const float *x, void *ximg, void *stream) {
+    if (m < 128 || m % 128 || m > (int64_t(1) << 26) || k < 1 || k > 15 || !x || !ximg ||
+        (((uintptr_t)ximg) & 15))
+        return fail0(DR_ERR_INVALID, "dr_gemm_x6_split_x: bad arguments (m a positive multiple "
+                                     "of 128, 1 <= k <= 15, ximg 16-byte aligned)");
+    if (gemm_x6_split_x_launch(m, (int)k, x, ximg, as_stream(stream)))
+        return fail0(DR_ERR_HIP, std::string("dr_gemm_x6_split_x: ") +
+                                     hipGetErrorString(hipGetLastError()));
+    return DR_OK;
+}
+
+// grad_h1 = grad_z W (the 256 x 256 layer's input gradient, both nets) never
+// stored: the first layer's backward (grad_z1 = grad_h1 (1 - h1^2), its
+// weight and bias gradients) fused into the GEMM's epilogue, leaving in
+// `workspace` exactly what dr_first_layer_backward2(..., defer = 1) leaves
+// there (the level-1 grouped partials) for dr_grad_finish.
+int dr_gemm_x6_bwd_first(int64_t batch, int64_t m, int64_t k, const float *grad_z,
+                         const void *img, const float *h, const void *ximg, void *workspace,
+                         size_t workspace_bytes, void *stream) {
+    const int64_t n = 256;
+    if (batch != 2 || m < 128 || m % 128 || m > (int64_t(1) << 26) || k < 1 || k > 15 ||
+        !grad_z || !img || !h || !ximg || !workspace ||
+        ((((uintptr_t)grad_z) | ((uintptr_t)img) | ((uintptr_t)h) | ((uintptr_t)ximg)) & 15))
+        return fail0(DR_ERR_INVALID, "dr_gemm_x6_bwd_first: bad arguments (batch 2, m a positive "
+                                     "multiple of 128, 1 <= k <= 15, 16-byte aligned pointers)");
+    if (workspace_bytes < first_ws_bytes(2, m, k, n))
+        return fail0(DR_ERR_INVALID, "dr_gemm_x6_bwd_first: workspace too small");
+    hipStream_t st = as_stream(stream);
+    // the fused kernel writes 16 x 256 partials per net (features 0 .. 14,
+    // the bias at 15); the workspace's per-net stride is (k + 1) x 256, so
+    // k < 15 is laid out by the features it has
+    if (k != 15)
+        return fail0(DR_ERR_UNSUPPORTED, "dr_gemm_x6_bwd_first: k must be 15 (the drone obs)");
+    const int nb_fl = first_blocks(m);
+    const int P = (int)(2 * (k + 1) * n);
+    float *part = static_cast<float *>(workspace);
+    float *part2 = reinterpret_cast<float *>(static_cast<char *>(workspace) +
+                                             align_up(sizeof(float) * (size_t)(nb_fl * P)));
+    const int per = gemm_x6_fl_launch(2, m, grad_z, img, h, ximg, part, st);
+    if (per < 1 || per > nb_fl)
+        return fail0(DR_ERR_HIP, std::string("dr_gemm_x6_bwd_first: ") +
+                                     hipGetErrorString(hipGetLastError()));
+    // level 1 into the group count dr_grad_finish expects of this m
+    const int gsize_fl = (nb_fl + kHeadGroups - 1) / kHeadGroups;
+    const int ng = (nb_fl + gsize_fl - 1) / gsize_fl;
+    const int gsize = (per + ng - 1) / ng;
+    hipLaunchKernelGGL(colsum_groups_kernel, dim3((P + kBlock - 1) / kBlock, ng), dim3(kBlock),
+                       0, st, per, P, gsize, part, part2);
+    return check_launch("dr_gemm_x6_bwd_first");
+}
+
 int dr_first_layer_backward(int64_t m, int64_t k, int64_t n, const float *grad_h,
                             const float *h, const float *x, const int32_t *rows, float *grad_w,
                             float *grad_b, void *workspace, size_t workspace_bytes,

@@ -127,6 +127,10 @@ class ActorCritic:
         # (fp32-accurate bf16 MFMA) where it applies;
         # DRONERL_GEMM_X6=0: the f32 library GEMMs
         self.gemm_x6 = os.environ.get("DRONERL_GEMM_X6", "1") != "0"
+        # the layer's input gradient with the first layer's backward fused
+        # into its epilogue (dr_gemm_x6_bwd_first, round 5) on the deferred-
+        # finish path; DRONERL_X6_FL=0: dr_gemm_x6 + dr_first_layer_backward2
+        self.gemm_x6_fl = os.environ.get("DRONERL_X6_FL", "1") != "0"
         self._x6 = None
         self.flat = torch.zeros(off, dtype=torch.float32, device=self.device)
         self.reset_parameters(seed, log_std_init)
@@ -413,6 +417,25 @@ class FusedTrainStep:
                 on_ready(self.first_layer_end(), self.grad.numel())
             g = self._g2.view(-1)[:2 * M * n_in].view(2, M, n_in)
             xw = x6_weights(pol, M) if k == 1 else None
+            if (xw is not None and defer_finish and rows is None and pol.gemm_x6_fl and
+                    pol.obs_dim == 15 and n_in == 256):
+                # grad_h1 never stored: the first layer's backward in the
+                # GEMM's epilogue, its partials left in the first-layer
+                # workspace for the deferred finish (dr_gemm_x6_bwd_first)
+                from . import _lib
+                if getattr(self, "_ximg", None) is None:
+                    self._ximg = torch.empty(_lib.lib().dr_gemm_x6_x_bytes(M), dtype=torch.uint8,
+                                             device=pol.device)
+                st = torch.cuda.current_stream(pol.device).cuda_stream
+                _lib.check(_lib.lib().dr_gemm_x6_split_x(M, 15, obs.data_ptr(),
+                                                         self._ximg.data_ptr(), st))
+                mark("split_x")
+                _lib.check(_lib.lib().dr_gemm_x6_bwd_first(
+                    2, M, 15, gz.data_ptr(), xw.bwd.data_ptr(), x.data_ptr(),
+                    self._ximg.data_ptr(), self._first.ws.data_ptr(), self._first.ws.numel(),
+                    st))
+                mark("gemm_x6_bwd_first")
+                continue
             if xw is not None:
                 gemm_x6(gz, xw.bwd, g)       # images refreshed by hidden_forward
             else:

@@ -39,7 +39,7 @@
 extern "C" {
 #endif
 
-#define DR_ABI_VERSION 14
+#define DR_ABI_VERSION 15
 
 enum dr_status {
     DR_OK = 0,
@@ -553,6 +553,30 @@ int dr_gemm_x6(int64_t batch, int64_t m, const float *a, const void *img, float 
    Deterministic.  (ABI v10.) */
 int dr_gemm_x6_wgrad(int64_t batch, int64_t m, int64_t chunks, const float *g, const float *h,
                      float *ws, void *stream);
+
+/* The first-layer operand image of dr_gemm_x6_bwd_first: the minibatch
+   observations x (m x k f32 row-major, k <= 15) with a constant 1 as the
+   16th feature, split exactly into three bf16 planes in the MFMA fragment
+   order (dr_gemm_x6_x_bytes(m) bytes, 16-byte aligned).  (ABI v15.) */
+size_t dr_gemm_x6_x_bytes(int64_t m);
+int dr_gemm_x6_split_x(int64_t m, int64_t k, const float *x, void *ximg, void *stream);
+
+/* The 256 x 256 layer's input gradient with the first layer's backward
+   fused into its epilogue (replaces dr_gemm_x6(2, m, grad_z, img W-form,
+   grad_h) followed by dr_first_layer_backward2(..., defer = 1); PPO.train's
+   backward through SB3's MlpExtractor, /root/reference/train.py:36-43):
+   grad_h1 = grad_z W per net stays in registers, grad_z1 = grad_h1 (1 - h^2)
+   with h (2, m, 256) the first layer's activations, and the first layer's
+   weight and bias gradients accumulate on the matrix cores against ximg
+   (dr_gemm_x6_split_x of the same minibatch's x, k = 15).  `workspace` is
+   dr_first_layer_backward2's (>= dr_first_layer_backward2_workspace_bytes(m,
+   15, 256)) and is left exactly as its defer = 1 form leaves it: the next
+   dr_grad_finish / dr_grad_finish_clip_adam with first_workspace =
+   workspace writes the gradients.  batch 2, m a positive multiple of 128,
+   pointers 16-byte aligned.  Deterministic.  (ABI v15.) */
+int dr_gemm_x6_bwd_first(int64_t batch, int64_t m, int64_t k, const float *grad_z,
+                         const void *img, const float *h, const void *ximg, void *workspace,
+                         size_t workspace_bytes, void *stream);
 
 #ifdef __cplusplus
 }

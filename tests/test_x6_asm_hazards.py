@@ -22,7 +22,8 @@ import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 SRC = os.path.join(ROOT, "drone_rl_amd", "csrc", "gemm_x6.hip")
-KERNEL = "gemm_x6_ws_kernel"
+# the weight-stationary GEMM and (round 5) its first-layer-backward form
+KERNELS = ("gemm_x6_ws_kernel", "gemm_x6_fl_kernel")
 # XDL (v_mfma_f32_32x32x16_bf16, 8 passes on gfx950) write VGPR -> VALU, VMEM
 # or LDS access of it: 11 wait states on gfx940-class parts; checked with margin
 WAIT = 18
@@ -51,7 +52,21 @@ def _any_regs(text):
     return _regs(text, _VREG, "v") | _regs(text, _AREG, "a")
 
 
-def _kernel_asm():
+_ASM = {}
+
+
+def _kernel_asm(kernel):
+    if "s" not in _ASM:
+        _ASM["s"] = _compile()
+    s = _ASM["s"]
+    name = next(l.split(":")[0] for l in s.splitlines()
+                if kernel in l.split(":")[0] and re.match(r"^[_A-Za-z0-9]+:", l))
+    a = s.index(name + ":")
+    b = s.index(".Lfunc_end", a)
+    return s[a:b].splitlines()
+
+
+def _compile():
     hipcc = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
     if not os.path.exists(hipcc):
         pytest.skip("hipcc not available")
@@ -63,12 +78,7 @@ def _kernel_asm():
              "--cuda-device-only", "-S", SRC, "-o", asm],
             capture_output=True, text=True, timeout=300)
         assert out.returncode == 0, out.stderr[-2000:]
-        s = open(asm).read()
-    name = next(l.split(":")[0] for l in s.splitlines()
-                if KERNEL in l.split(":")[0] and re.match(r"^[_A-Za-z0-9]+:", l))
-    a = s.index(name + ":")
-    b = s.index(".Lfunc_end", a)
-    return s[a:b].splitlines()
+        return open(asm).read()
 
 
 def _scan(lines):
@@ -168,7 +178,8 @@ def test_scanner_flags_an_operand_written_right_before_an_asm_mfma():
     assert any("reads v178" in b for b in bad) and any("reads a77" in b for b in bad)
 
 
-def test_no_compiler_access_to_asm_mfma_results_without_wait_states():
-    n_mfma, bad = _scan(_kernel_asm())
+@pytest.mark.parametrize("kernel", KERNELS)
+def test_no_compiler_access_to_asm_mfma_results_without_wait_states(kernel):
+    n_mfma, bad = _scan(_kernel_asm(kernel))
     assert n_mfma >= 192, f"expected the kernel's asm MFMAs, found {n_mfma}"
     assert not bad, "\n".join(bad[:20])
