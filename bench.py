@@ -661,6 +661,7 @@ def ppo_kernel_times(tr, reps=20):
                 _lib.lib().dr_gemm_x6_bwd_first(
                     2, M, 15, gz.data_ptr(), xw.bwd.data_ptr(), a0.data_ptr(),
                     f._ximg.data_ptr(), f._first.ws.data_ptr(), f._first.ws.numel(),
+                    int(pol.gemm_x6_fl_direct),
                     torch.cuda.current_stream(tr.device).cuda_stream)))
         else:
             iso["gemm_x6_bwd"] = graph_us(lambda: gemm_x6(gz, xw.bwd, g))

@@ -56,7 +56,7 @@ class dr_grad_finish(ctypes.Structure):
                 ("first_n", c_int64),
                 ("g_w0", c_void_p), ("g_b0", c_void_p), ("g_w1", c_void_p), ("g_b1", c_void_p),
                 ("chunks", c_void_p), ("chunk_groups", c_int64), ("chunk_count", c_int64),
-                ("chunk_size", c_int64), ("chunk_dst", c_void_p)]
+                ("chunk_size", c_int64), ("chunk_dst", c_void_p), ("first_rows", c_int64)]
 
 
 class DroneRLError(RuntimeError):
@@ -143,7 +143,8 @@ SIGNATURES = {
     "dr_gemm_x6_x_bytes": (c_size_t, [c_int64]),
     "dr_gemm_x6_split_x": (c_int, [c_int64, c_int64, _P, _P, _P]),
     "dr_gemm_x6_bwd_first": (c_int, [c_int64, c_int64, c_int64, _P, _P, _P, _P, _P, c_size_t,
-                                     _P]),
+                                     c_int, _P]),
+    "dr_gemm_x6_bwd_first_rows": (c_int64, [c_int64]),
 }
 
 _lib = None

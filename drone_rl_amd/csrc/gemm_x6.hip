@@ -796,9 +796,17 @@ __global__ __launch_bounds__(WS_THREADS, 1) void gemm_x6_fl_kernel(
     // the l plane's fragment of global k16 step g (tile g >> 4, step g & 15):
     // a ring of 4, loaded two steps ahead
     auto wl_load = [&](int g) { return wfrag((g >> 4) & 1, g & 15, 2); };
-    bf16x8_t wl[4];
-    wl[0] = wl_load(0);
-    wl[1] = wl_load(1);
+// the l plane's fragments are loaded FL_WL_AHEAD k16 steps ahead: every
+// vector-memory wait is in issue order, so a fragment load queued behind the
+// HBM loads of h1 / the staging rows waits for them too (2 ahead: 127 us per
+// call, 6 ahead: 118, scripts/micro/r5_flvar.sh, round 5)
+#ifndef FL_WL_AHEAD
+#define FL_WL_AHEAD 6
+#endif
+    constexpr int WLA = FL_WL_AHEAD, WLR = WLA < 4 ? 4 : 8;
+    bf16x8_t wl[WLR];
+#pragma unroll
+    for (int g = 0; g < WLA; ++g) wl[g] = wl_load(g);
 
     // activation staging: lane L splits row L & 7 of the wave's 8 rows,
     // chunk 8 u + (L >> 3), half hf ^ (chunk & 1) (the conflict-free split
@@ -857,13 +865,26 @@ __global__ __launch_bounds__(WS_THREADS, 1) void gemm_x6_fl_kernel(
 
     // ---- the epilogue: grad_z1 of tile tt of row step kk into D2 ----
     f32x16_t d2 = (f32x16_t){};
-    float hv[16];
+    // FL_H_EARLY (A/B knob): the epilogue's h1 rows loaded one phase ahead,
+    // tile t's in hb[t] (loaded while tile t's MFMAs run, read by the next
+    // phase).  Round 5: 123-125 vs 125-127 us alone, 117-121 vs 115-118 us
+    // beside FL_WL_AHEAD 6 -- no gain, off
+#ifndef FL_H_EARLY
+#define FL_H_EARLY 0
+#endif
+    float hb[FL_H_EARLY ? 2 : 1][16];
     const int hoff[2] = {(4 * fh * XN + 64 * w + fr) * 4, (4 * fh * XN + 64 * w + 32 + fr) * 4};
     auto h_load = [&](int kk, int tt, int r) {
+        float *hv = hb[FL_H_EARLY ? tt : 0];
         const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
             (void *)(Hb + (int64_t)(j0 + kk * per) * WS_RS * XN), 0, WS_RS * XN * 4, kBufFlags);
+#ifdef FL_NO_H
+        (void)rs;
+        hv[r] = 0.5f;
+#else
         hv[r] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(
             rs, hoff[tt], (8 * (r >> 2) + (r & 3)) * XN * 4, 0));
+#endif
     };
     // lane (m = fr, fh) of X^T's fragment: feature fr & 15 of column tile
     // fr >> 4; the other tile's lanes load from past the record's end, which
@@ -882,10 +903,13 @@ __global__ __launch_bounds__(WS_THREADS, 1) void gemm_x6_fl_kernel(
     // registers 8 j .. 8 j + 7 of tile tt, split into the B fragment planes,
     // and the six x6 products into D2
     auto d2_kstep = [&](int tt, int j, const bf16x8_t (&xf)[3]) {
+#ifdef FL_NO_D2
+        return;
+#endif
         float gz[8];
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
-            const float y = hv[8 * j + e];
+            const float y = hb[FL_H_EARLY ? tt : 0][8 * j + e];
             gz[e] = acc_h[tt][8 * j + e] * (1.0f - y * y);
         }
         u32x4_t gh, gm, gl;
@@ -920,6 +944,11 @@ __global__ __launch_bounds__(WS_THREADS, 1) void gemm_x6_fl_kernel(
 #pragma unroll
     for (int q = 0; q < 4; ++q) stg[q] = stage_load(1, q);
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    if (FL_H_EARLY) {
+        // row step 0's phase-0 epilogue is of the zeroed tile 1: finite rows
+#pragma unroll
+        for (int r = 0; r < 16; ++r) h_load(0, 1, r);
+    }
     constexpr int NF = 3;                     // fragment sets (two steps ahead)
     AFrag fb[NF];
     read_frag(0, 0, fb[0]);
@@ -944,13 +973,18 @@ __global__ __launch_bounds__(WS_THREADS, 1) void gemm_x6_fl_kernel(
             for (int s = 0; s < 16; ++s) {
                 const int g = 16 * t + s;
                 if (g + 2 < 32) read_frag(k, (g + 2) & 15, fb[(g + 2) % NF]);
-                wl[(g + 2) & 3] = wl_load(g + 2);
+                wl[(g + WLA) % WLR] = wl_load(g + WLA);
                 const AFrag &x = fb[g % NF];
                 mfma_x6_group(s == 0, acc_h[t], acc_l[t], x[0], x[1], x[2], Wa[t][s][0],
-                              Wa[t][s][1], wl[g & 3]);
+                              Wa[t][s][1], wl[g % WLR]);
                 if (s < 8) {
-                    h_load(kk, tt, 2 * s);
-                    h_load(kk, tt, 2 * s + 1);
+                    if (FL_H_EARLY) {
+                        h_load(k, t, 2 * s);          // the next phase's epilogue
+                        h_load(k, t, 2 * s + 1);
+                    } else {
+                        h_load(kk, tt, 2 * s);
+                        h_load(kk, tt, 2 * s + 1);
+                    }
                 }
                 if (s == 2) x_frag(kk, tt, 0, xf0);
                 if (s == 6) x_frag(kk, tt, 1, xf1);
@@ -972,7 +1006,8 @@ __global__ __launch_bounds__(WS_THREADS, 1) void gemm_x6_fl_kernel(
     if (R > 0) {
         finish_tile(1);
 #pragma unroll
-        for (int r = 0; r < 16; ++r) h_load(R - 1, 1, r);
+        for (int r = 0; r < 16; ++r)
+            if (!FL_H_EARLY) h_load(R - 1, 1, r);
         x_frag(R - 1, 1, 0, xf0);
         x_frag(R - 1, 1, 1, xf1);
         d2_kstep(1, 0, xf0);
@@ -1009,12 +1044,18 @@ int gemm_x6_split_x_launch(int64_t m, int k, const float *x, void *ximg, hipStre
 }
 
 // returns the blocks per net (the partial rows written), or -1
-int gemm_x6_fl_launch(int batch, int64_t m, const float *gz, const void *img, const float *h,
-                      const void *ximg, float *part, hipStream_t st) {
+// blocks per net of gemm_x6_fl_kernel at m rows (its partial rows)
+int gemm_x6_fl_rows(int batch, int64_t m) {
     const int n_cu = device_cu_count();
     const int units = (int)(batch * (m / WS_RS));
     int grid = units < n_cu ? units : n_cu;
     grid -= grid % batch;
+    return grid / batch;
+}
+
+int gemm_x6_fl_launch(int batch, int64_t m, const float *gz, const void *img, const float *h,
+                      const void *ximg, float *part, hipStream_t st) {
+    const int grid = gemm_x6_fl_rows(batch, m) * batch;
     hipLaunchKernelGGL(gemm_x6_fl_kernel, dim3(grid), dim3(WS_THREADS), 0, st, gz,
                        static_cast<const uint8_t *>(img), h, static_cast<const uint8_t *>(ximg),
                        part, m, batch);

@@ -1431,6 +1431,41 @@ __device__ inline float first_finish_part(int bx, int ng, int n, int K, int nets
     return s * s;
 }
 
+// The same finish from `rows` level-1 partial rows (dr_gemm_x6_bwd_first's
+// per-block rows, no grouping launch): a block takes 64 entries, its four
+// waves a quarter of the rows each (8 accumulators, 32 loads in flight per
+// lane at 128 rows), combined in LDS in a fixed order.
+__device__ inline float first_finish_direct(int bx, int rows, int n, int K, int nets,
+                                            const float *__restrict__ part, const FirstBwdOut &o) {
+    __shared__ float red[4][64];
+    const int P1 = (K + 1) * n;
+    const int P = nets * P1;
+    const int col = threadIdx.x & 63, q = threadIdx.x >> 6;
+    const int pp = bx * 64 + col;
+    float s = 0.f;
+    if (pp < P) {
+        const int lo = q * rows / 4, hi = (q + 1) * rows / 4;
+        float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+        int r = lo;
+        for (; r + 8 <= hi; r += 8) {
+#pragma unroll
+            for (int u = 0; u < 8; ++u) acc[u] += part[(int64_t)(r + u) * P + pp];
+        }
+        for (; r < hi; ++r) acc[0] += part[(int64_t)r * P + pp];
+        s = ((acc[0] + acc[1]) + (acc[2] + acc[3])) + ((acc[4] + acc[5]) + (acc[6] + acc[7]));
+    }
+    red[q][col] = s;
+    __syncthreads();
+    if (q != 0 || pp >= P) return 0.f;
+    const float t = (red[0][col] + red[1][col]) + (red[2][col] + red[3][col]);
+    const int net = pp >= P1 ? 1 : 0;
+    const int p = pp - net * P1;
+    const int k = p / n, c = p - k * n;
+    if (k < K) o.gw[net][c * K + k] = t;
+    else o.gb[net][c] = t;
+    return t * t;
+}
+
 __global__ __launch_bounds__(kBlock) void first_layer_finish_kernel(int ng, int n, int K,
                                                                     int nets,
                                                                     const float *__restrict__ part,
@@ -1613,8 +1648,8 @@ struct FinishArgs {
     const float *h_part2, *h_adv_ms, *log_std;
     float ent_coef, vf_coef;
     HeadOut ho;
-    // first layer
-    int f_ng, f_n, f_K, f_nets;
+    // first layer (f_direct > 0: that many level-1 rows, summed here)
+    int f_ng, f_n, f_K, f_nets, f_direct;
     const float *f_part2;
     FirstBwdOut fo;
     // split-K chunks
@@ -1633,7 +1668,9 @@ __global__ __launch_bounds__(kBlock) void grad_finish_kernel(FinishArgs a) {
         sq = head_finish_part(b, a.h_ng, a.h_P, a.h_hd, a.h_m, a.h_part2, a.h_adv_ms, a.log_std,
                               a.ent_coef, a.vf_coef, a.ho);
     } else if ((b -= a.bh) < a.bf) {
-        sq = first_finish_part(b, a.f_ng, a.f_n, a.f_K, a.f_nets, a.f_part2, a.fo);
+        sq = a.f_direct ? first_finish_direct(b, a.f_direct, a.f_n, a.f_K, a.f_nets, a.f_part2,
+                                              a.fo)
+                        : first_finish_part(b, a.f_ng, a.f_n, a.f_K, a.f_nets, a.f_part2, a.fo);
     } else {
         b -= a.bf;
         sq = chunk_sum_part(b, a.c_groups, a.c_count, a.c_size, a.chunks, a.c_dst);
@@ -1948,7 +1985,10 @@ static int first_blocks(int64_t m);
 // Block counts of grad_finish_kernel's three segments.
 static void finish_blocks(const dr_grad_finish *f, int &bh, int &bf, int &bc) {
     bh = f->head_workspace ? (int)((kHeadFixed + 7 * f->head_hd + kBlock - 1) / kBlock) : 0;
-    bf = f->first_workspace ? (int)((2 * (f->first_k + 1) * f->first_n + kBlock - 1) / kBlock) : 0;
+    const int64_t fP = 2 * (f->first_k + 1) * f->first_n;
+    bf = !f->first_workspace ? 0
+         : f->first_rows > 0 ? (int)((fP + 63) / 64)     // first_finish_direct: 64 per block
+                             : (int)((fP + kBlock - 1) / kBlock);
     bc = f->chunks ? (int)((f->chunk_groups * f->chunk_size + kBlock - 1) / kBlock) : 0;
 }
 
@@ -1991,7 +2031,8 @@ static int launch_grad_finish(const dr_grad_finish *f, void *workspace, size_t w
                               !f->stats))
         return fail0(DR_ERR_INVALID, "dr_grad_finish: bad head arguments");
     if (f->first_workspace && (f->first_m < 1 || f->first_n < 4 || f->first_n > 256 ||
-                               f->first_k < 1 || !f->g_w0 || !f->g_b0 || !f->g_w1 || !f->g_b1))
+                               f->first_k < 1 || !f->g_w0 || !f->g_b0 || !f->g_w1 || !f->g_b1 ||
+                               f->first_rows < 0 || f->first_rows > first_blocks(f->first_m)))
         return fail0(DR_ERR_INVALID, "dr_grad_finish: bad first-layer arguments");
     if (f->chunks && (f->chunk_groups < 1 || f->chunk_count < 1 || f->chunk_size < 1 ||
                       !f->chunk_dst))
@@ -2035,6 +2076,10 @@ static int launch_grad_finish(const dr_grad_finish *f, void *workspace, size_t w
         a.f_part2 = reinterpret_cast<const float *>(static_cast<const char *>(f->first_workspace) +
                                                     align_up(sizeof(float) * (size_t)(nb * P)));
         a.fo = FirstBwdOut{{f->g_w0, f->g_w1}, {f->g_b0, f->g_b1}};
+        if (f->first_rows > 0) {
+            a.f_direct = (int)f->first_rows;
+            a.f_part2 = static_cast<const float *>(f->first_workspace);
+        }
     }
     if (f->chunks) {
         a.c_groups = f->chunk_groups;
@@ -2333,6 +2378,7 @@ size_t gemm_x6_x_bytes(int64_t m);
 int gemm_x6_split_x_launch(int64_t m, int k, const float *x, void *ximg, hipStream_t st);
 int gemm_x6_fl_launch(int batch, int64_t m, const float *gz, const void *img, const float *h,
                       const void *ximg, float *part, hipStream_t st);
+int gemm_x6_fl_rows(int batch, int64_t m);
 }  // namespace dr
 }
 
@@ -2354,9 +2400,14 @@ int dr_gemm_x6_split_x(int64_t m, int64_t k, const float *x, void *ximg, void *s
 // weight and bias gradients) fused into the GEMM's epilogue, leaving in
 // `workspace` exactly what dr_first_layer_backward2(..., defer = 1) leaves
 // there (the level-1 grouped partials) for dr_grad_finish.
+int64_t dr_gemm_x6_bwd_first_rows(int64_t m) {
+    if (m < 128 || m % 128 || m > (int64_t(1) << 26)) return 0;
+    return gemm_x6_fl_rows(2, m);
+}
+
 int dr_gemm_x6_bwd_first(int64_t batch, int64_t m, int64_t k, const float *grad_z,
                          const void *img, const float *h, const void *ximg, void *workspace,
-                         size_t workspace_bytes, void *stream) {
+                         size_t workspace_bytes, int direct, void *stream) {
     const int64_t n = 256;
     if (batch != 2 || m < 128 || m % 128 || m > (int64_t(1) << 26) || k < 1 || k > 15 ||
         !grad_z || !img || !h || !ximg || !workspace ||
@@ -2380,6 +2431,9 @@ int dr_gemm_x6_bwd_first(int64_t batch, int64_t m, int64_t k, const float *grad_
     if (per < 1 || per > nb_fl)
         return fail0(DR_ERR_HIP, std::string("dr_gemm_x6_bwd_first: ") +
                                      hipGetErrorString(hipGetLastError()));
+    // direct: the per-block rows stay at the workspace start for a finish
+    // with first_rows = dr_gemm_x6_bwd_first_rows(m) (no level-1 launch)
+    if (direct) return DR_OK;
     // level 1 into the group count dr_grad_finish expects of this m
     const int gsize_fl = (nb_fl + kHeadGroups - 1) / kHeadGroups;
     const int ng = (nb_fl + gsize_fl - 1) / gsize_fl;

@@ -1,7 +1,9 @@
 // Exact three-plane bf16 split of f32 values for the bf16 matrix cores (the
 // x6 GEMM scheme of gemm_x6.hip: x = h + m + l, each plane RNE of the
 // remainder, x - h and (x - h) - m exact in f32, the last remainder a bf16),
-// shared by the 256 x 256 layer GEMMs and the first layer (ppo_kernels.hip).
+// used by the weight-image split, the weight-gradient GEMM's operands and the
+// fused first-layer backward's grad_z1 / observation planes (all in
+// gemm_x6.hip).
 #pragma once
 
 #include <cstdint>

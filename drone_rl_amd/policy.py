@@ -131,6 +131,8 @@ class ActorCritic:
         # into its epilogue (dr_gemm_x6_bwd_first, round 5) on the deferred-
         # finish path; DRONERL_X6_FL=0: dr_gemm_x6 + dr_first_layer_backward2
         self.gemm_x6_fl = os.environ.get("DRONERL_X6_FL", "1") != "0"
+        # its per-block rows summed by the deferred finish (no grouping launch)
+        self.gemm_x6_fl_direct = os.environ.get("DRONERL_X6_FL_DIRECT", "1") != "0"
         self._x6 = None
         self.flat = torch.zeros(off, dtype=torch.float32, device=self.device)
         self.reset_parameters(seed, log_std_init)
@@ -390,6 +392,7 @@ class FusedTrainStep:
         if defer_finish and (not self.can_defer() or on_ready is not None):
             raise ValueError("defer_finish needs a 2-hidden-layer net and no on_ready")
         mark = self.mark or _no_mark
+        self._first_rows = 0
         hs = hidden_forward(pol, obs, self._acts, self._acts2, rows, top_preact=preact,
                             mark=self.mark)
         gz = self._gz2[top]
@@ -430,10 +433,13 @@ class FusedTrainStep:
                 _lib.check(_lib.lib().dr_gemm_x6_split_x(M, 15, obs.data_ptr(),
                                                          self._ximg.data_ptr(), st))
                 mark("split_x")
+                direct = int(pol.gemm_x6_fl_direct)
                 _lib.check(_lib.lib().dr_gemm_x6_bwd_first(
                     2, M, 15, gz.data_ptr(), xw.bwd.data_ptr(), x.data_ptr(),
                     self._ximg.data_ptr(), self._first.ws.data_ptr(), self._first.ws.numel(),
-                    st))
+                    direct, st))
+                if direct:
+                    self._first_rows = _lib.lib().dr_gemm_x6_bwd_first_rows(M)
                 mark("gemm_x6_bwd_first")
                 continue
             if xw is not None:
@@ -473,6 +479,7 @@ class FusedTrainStep:
         d.stats = stats.data_ptr()
         d.first_workspace = self._first.ws.data_ptr()
         d.first_m, d.first_k, d.first_n = M, pol.obs_dim, pol.net_arch[0]
+        d.first_rows = self._first_rows
         d.g_w0, d.g_b0, d.g_w1, d.g_b1 = gp("pi0.w"), gp("pi0.b"), gp("vf0.w"), gp("vf0.b")
         out = pol.p2(1, "w", self.grad)                        # (2, N, K), contiguous
         N, Kd = out.shape[1], out.shape[2]

@@ -469,6 +469,11 @@ typedef struct dr_grad_finish {
     const float *chunks;
     int64_t chunk_groups, chunk_count, chunk_size;
     float *chunk_dst;
+    /* 0: first_workspace holds dr_first_layer_backward2's level-1 groups;
+       > 0: that many per-block rows at its start, left by
+       dr_gemm_x6_bwd_first(..., direct = 1) (= dr_gemm_x6_bwd_first_rows(m);
+       summed by the finish, no grouping launch).  (ABI v15.) */
+    int64_t first_rows;
 } dr_grad_finish;
 
 /* dr_clip_adam fused with the deferred gradient finish: one launch reduces
@@ -572,11 +577,17 @@ int dr_gemm_x6_split_x(int64_t m, int64_t k, const float *x, void *ximg, void *s
    dr_first_layer_backward2's (>= dr_first_layer_backward2_workspace_bytes(m,
    15, 256)) and is left exactly as its defer = 1 form leaves it: the next
    dr_grad_finish / dr_grad_finish_clip_adam with first_workspace =
-   workspace writes the gradients.  batch 2, m a positive multiple of 128,
-   pointers 16-byte aligned.  Deterministic.  (ABI v15.) */
+   workspace writes the gradients.  With direct != 0 the kernel's per-block
+   rows are left at the workspace start instead (no grouping launch) for a
+   finish with first_rows = dr_gemm_x6_bwd_first_rows(m).  batch 2, m a
+   positive multiple of 128, pointers 16-byte aligned.  Deterministic.
+   (ABI v15.) */
 int dr_gemm_x6_bwd_first(int64_t batch, int64_t m, int64_t k, const float *grad_z,
                          const void *img, const float *h, const void *ximg, void *workspace,
-                         size_t workspace_bytes, void *stream);
+                         size_t workspace_bytes, int direct, void *stream);
+/* The number of per-block rows dr_gemm_x6_bwd_first(..., direct = 1) leaves
+   at m rows on the current device (0 for an invalid m). */
+int64_t dr_gemm_x6_bwd_first_rows(int64_t m);
 
 #ifdef __cplusplus
 }

@@ -79,7 +79,7 @@ def test_bwd_first_matches_f64_within_fp32_bound(m):
     wsb = L.dr_first_layer_backward2_workspace_bytes(m, 15, 256)
     ws_f = torch.zeros(wsb, dtype=torch.uint8, device="cuda")
     check(L.dr_gemm_x6_bwd_first(2, m, 15, ptr(gz), ptr(img), ptr(h), ptr(ximg), ptr(ws_f), wsb,
-                                 s))
+                                 0, s))
     # the unfused path into a second workspace
     gh = torch.empty(2, m, 256, device="cuda")
     check(L.dr_gemm_x6(2, m, ptr(gz), ptr(img), ptr(gh), s))
@@ -102,15 +102,25 @@ def test_bwd_first_matches_f64_within_fp32_bound(m):
     env_b = env1.sum(1).numpy()
     n_chain = 256 + 3 + 1024 + 64      # dot product, elementwise, row sum, groups (generous)
     gam = n_chain * U / (1 - n_chain * U)
-    for name, ws in (("fused", ws_f), ("unfused", ws_u)):
-        w_, b_ = _level1_total(ws, m)
+    # direct: the per-block rows at the workspace start
+    ws_d = torch.zeros(wsb, dtype=torch.uint8, device="cuda")
+    check(L.dr_gemm_x6_bwd_first(2, m, 15, ptr(gz), ptr(img), ptr(h), ptr(ximg), ptr(ws_d), wsb,
+                                 1, s))
+    torch.cuda.synchronize()
+    rows = L.dr_gemm_x6_bwd_first_rows(m)
+    assert 1 <= rows <= min(-(-m // 16), 256)
+    P = 2 * 16 * 256
+    drows = ws_d.view(torch.float32)[:rows * P].double().cpu().view(rows, 2, 16, 256).sum(0)
+    direct = (drows[:, :15, :].transpose(1, 2).numpy(), drows[:, 15, :].numpy())
+    for name, ws in (("fused", ws_f), ("unfused", ws_u), ("direct", None)):
+        w_, b_ = _level1_total(ws, m) if ws is not None else direct
         ew = np.abs(w_ - ref_w) / np.maximum(env_w, 1e-30)
         eb = np.abs(b_ - ref_b) / np.maximum(env_b, 1e-30)
         assert ew.max() <= gam and eb.max() <= gam, (name, ew.max(), eb.max(), gam)
     # deterministic: a second run gives the same bytes
     ws_2 = torch.zeros_like(ws_f)
     check(L.dr_gemm_x6_bwd_first(2, m, 15, ptr(gz), ptr(img), ptr(h), ptr(ximg), ptr(ws_2), wsb,
-                                 s))
+                                 0, s))
     torch.cuda.synchronize()
     assert torch.equal(ws_f, ws_2)
 
@@ -124,22 +134,25 @@ def test_bwd_first_argument_errors():
     img = torch.zeros(L.dr_gemm_x6_weights_bytes(2), dtype=torch.uint8, device="cuda")
     xi = torch.zeros(L.dr_gemm_x6_x_bytes(128), dtype=torch.uint8, device="cuda")
     assert L.dr_gemm_x6_bwd_first(2, 100, 15, ptr(a), ptr(img), ptr(a), ptr(xi), ptr(ws),
-                                  ws.numel(), s) == _lib.DR_ERR_INVALID
+                                  ws.numel(), 0, s) == _lib.DR_ERR_INVALID
     assert L.dr_gemm_x6_bwd_first(2, 128, 15, ptr(a), ptr(img), ptr(a), ptr(xi), ptr(ws), 16,
-                                  s) == _lib.DR_ERR_INVALID
+                                  0, s) == _lib.DR_ERR_INVALID
+    assert L.dr_gemm_x6_bwd_first_rows(100) == 0 and L.dr_gemm_x6_bwd_first_rows(128) >= 1
     assert L.dr_gemm_x6_split_x(128, 16, ptr(a), ptr(xi), s) == _lib.DR_ERR_INVALID
 
 
 def test_trainer_step_fused_equals_unfused_within_bound(monkeypatch):
     """One FusedTrainStep on the deferred-finish path with the fused kernel
-    and without it (DRONERL_X6_FL=0): the first-layer gradients agree within
-    the fp32 bound, every other gradient entry is bitwise the same."""
+    (its rows summed by the finish directly, and through the grouping launch)
+    and without it (DRONERL_X6_FL=0): the first-layer gradients agree, every
+    other gradient entry is bitwise the same."""
     from drone_rl_amd import ppo_kernels as K
     from drone_rl_amd.policy import ActorCritic, FusedTrainStep
     m = 8192
     grads = []
-    for fl in ("1", "0"):
+    for fl, direct in (("1", "1"), ("1", "0"), ("0", "1")):
         monkeypatch.setenv("DRONERL_X6_FL", fl)
+        monkeypatch.setenv("DRONERL_X6_FL_DIRECT", direct)
         pol = ActorCritic(15, 4, (256, 256), seed=3, device="cuda")
         fs = FusedTrainStep(pol, m)
         g = torch.Generator().manual_seed(11)
@@ -153,10 +166,11 @@ def test_trainer_step_fused_equals_unfused_within_bound(monkeypatch):
         torch.cuda.synchronize()
         grads.append((grad.clone(), {k: fs.gview(k).clone() for k in
                                       ("pi0.w", "pi0.b", "vf0.w", "vf0.b")}))
-    (gf, first_f), (gu, first_u) = grads
+    gu, first_u = grads[-1]
     lo = pol.offsets["pi1.w"][0]                 # the first layer's entries come first
-    assert torch.equal(gf[lo:], gu[lo:])
-    for k in first_f:
-        a, b = first_f[k].double(), first_u[k].double()
-        scale = b.abs().max().item() + 1e-30
-        assert (a - b).abs().max().item() <= 1e-4 * scale, k
+    for gf, first_f in grads[:-1]:
+        assert torch.equal(gf[lo:], gu[lo:])
+        for k in first_f:
+            a, b = first_f[k].double(), first_u[k].double()
+            scale = b.abs().max().item() + 1e-30
+            assert (a - b).abs().max().item() <= 1e-4 * scale, k
