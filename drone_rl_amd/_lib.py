@@ -56,7 +56,8 @@ class dr_grad_finish(ctypes.Structure):
                 ("first_n", c_int64),
                 ("g_w0", c_void_p), ("g_b0", c_void_p), ("g_w1", c_void_p), ("g_b1", c_void_p),
                 ("chunks", c_void_p), ("chunk_groups", c_int64), ("chunk_count", c_int64),
-                ("chunk_size", c_int64), ("chunk_dst", c_void_p), ("first_rows", c_int64)]
+                ("chunk_size", c_int64), ("chunk_dst", c_void_p), ("first_rows", c_int64),
+                ("head_direct", c_int64)]
 
 
 class DroneRLError(RuntimeError):

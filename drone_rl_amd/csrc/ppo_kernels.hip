@@ -1480,13 +1480,7 @@ struct HeadOut {
 
 // Fixed-order column sums of row groups: out[g][p] = sum of in[b][p] over
 // b in [g*gsize, (g+1)*gsize); 8 independent accumulators per thread.
-__global__ __launch_bounds__(kBlock) void colsum_groups_kernel(int nb, int P, int gsize,
-                                                               const float *__restrict__ in,
-                                                               float *__restrict__ out) {
-    const int p = blockIdx.x * kBlock + threadIdx.x;
-    if (p >= P) return;
-    const int b0 = blockIdx.y * gsize;
-    const int b1 = min(nb, b0 + gsize);
+__device__ inline float colsum_range(const float *__restrict__ in, int P, int p, int b0, int b1) {
     float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
     int b = b0;
     for (; b + 7 < b1; b += 8) {
@@ -1494,7 +1488,72 @@ __global__ __launch_bounds__(kBlock) void colsum_groups_kernel(int nb, int P, in
         for (int u = 0; u < 8; ++u) s[u] += in[(int64_t)(b + u) * P + p];
     }
     for (; b < b1; ++b) s[0] += in[(int64_t)b * P + p];
-    out[(int64_t)blockIdx.y * P + p] = ((s[0] + s[1]) + (s[2] + s[3])) + ((s[4] + s[5]) + (s[6] + s[7]));
+    return ((s[0] + s[1]) + (s[2] + s[3])) + ((s[4] + s[5]) + (s[6] + s[7]));
+}
+
+__global__ __launch_bounds__(kBlock) void colsum_groups_kernel(int nb, int P, int gsize,
+                                                               const float *__restrict__ in,
+                                                               float *__restrict__ out) {
+    const int p = blockIdx.x * kBlock + threadIdx.x;
+    if (p >= P) return;
+    const int b0 = blockIdx.y * gsize;
+    out[(int64_t)blockIdx.y * P + p] = colsum_range(in, P, p, b0, min(nb, b0 + gsize));
+}
+
+// first-level row groups of the partial sums (32 / 64 measured 6.62-6.69 vs
+// 6.67-6.72 PPO updates/s, round 4)
+constexpr int kHeadGroups = 16;
+
+// Entry p of the head's reduced partials to its output (the loss terms to
+// `loss`); returns its square for the norm.
+__device__ inline float head_store(int p, float s, int hd, float *loss, const HeadOut &o) {
+    if (p < kLossK) {
+        loss[p] = s;
+        return 0.f;
+    }
+    if (p < 13) {
+        o.g_b_act[p - 9] = s;
+    } else if (p == 13) {
+        o.g_b_val[0] = s;
+    } else {
+        const int q = p - kHeadFixed;
+        if (q < hd) o.g_b_pi[q] = s;
+        else if (q < 2 * hd) o.g_b_vf[q - hd] = s;
+        else if (q < 6 * hd) o.g_w_act[q - 2 * hd] = s;
+        else o.g_w_val[q - 6 * hd] = s;
+    }
+    return s * s;
+}
+
+// Block 0's tail: the loss statistics and the log_std gradient (their
+// squares for the norm, from thread 0).
+__device__ inline float head_stats(const float *loss, int64_t m, const float *__restrict__ adv_ms,
+                                   const float *__restrict__ log_std, float ent_coef,
+                                   float vf_coef, const HeadOut &o) {
+    float sq = 0.f;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const float inv_m = 1.0f / (float)m;
+        const float pl = loss[0] * inv_m;
+        const float vl = loss[1] * inv_m;
+        float H = 0.f;
+        for (int j = 0; j < 4; ++j) H += 0.5f + kLogSqrt2Pi + log_std[j];
+        const float el = -H;
+        for (int j = 0; j < 4; ++j) {
+            const float g = loss[4 + j] - ent_coef;
+            o.g_log_std[j] = g;
+            sq += g * g;
+        }
+        o.stats[0] = pl + ent_coef * el + vf_coef * vl;
+        o.stats[1] = pl;
+        o.stats[2] = vl;
+        o.stats[3] = el;
+        o.stats[4] = loss[2] * inv_m;
+        o.stats[5] = loss[3] * inv_m;
+        o.stats[6] = adv_ms[0];
+        o.stats[7] = adv_ms[1];
+    }
+    return sq;
 }
 
 // One thread's share of the head-gradient finish: the level-2 sum of the
@@ -1519,48 +1578,60 @@ __device__ inline float head_finish_part(int bx, int nb, int P, int hd, int64_t 
             s3 += part[(int64_t)(b + 3) * P + p];
         }
         for (; b < nb; ++b) s0 += part[(int64_t)b * P + p];
-        const float s = ((s0 + s1) + s2) + s3;
-        if (p < kLossK) {
-            loss[p] = s;
+        sq = head_store(p, ((s0 + s1) + s2) + s3, hd, loss, o);
+    }
+    if (bx == 0) sq += head_stats(loss, m, adv_ms, log_std, ent_coef, vf_coef, o);
+    return sq;
+}
+
+// The head finish from the kernel's nb per-block rows (no grouping launch):
+// a block takes 16 entries, its 16 row slices the level-1 groups of the
+// grouped path (colsum_range over the same rows), and slice 0 the level-2
+// sum in head_finish_part's order: bitwise the grouped path's values.
+__device__ inline float head_finish_direct(int bx, int nb, int P, int hd, int64_t m,
+                                           const float *__restrict__ part,
+                                           const float *__restrict__ adv_ms,
+                                           const float *__restrict__ log_std, float ent_coef,
+                                           float vf_coef, const HeadOut &o) {
+    __shared__ float loss[kLossK];
+    __shared__ float red[kHeadGroups][16];
+    const int col = threadIdx.x & 15, q = threadIdx.x >> 4;
+    const int p = bx * 16 + col;
+    const int gsize = (nb + kHeadGroups - 1) / kHeadGroups;
+    const int ng = (nb + gsize - 1) / gsize;
+    if (p < P && q < ng) {
+        const int b0 = q * gsize, b1 = min(nb, b0 + gsize);
+        if (b1 - b0 == 64) {
+            // the full 64-row group (65,536-row minibatches): every load
+            // issued before the sums, which keep colsum_range's order
+            float v[64];
+#pragma unroll
+            for (int r = 0; r < 64; ++r) v[r] = part[(int64_t)(b0 + r) * P + p];
+            float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int i = 0; i < 8; ++i)
+#pragma unroll
+                for (int u = 0; u < 8; ++u) s[u] += v[8 * i + u];
+            red[q][col] = ((s[0] + s[1]) + (s[2] + s[3])) + ((s[4] + s[5]) + (s[6] + s[7]));
         } else {
-            sq = s * s;
-            if (p < 13) {
-                o.g_b_act[p - 9] = s;
-            } else if (p == 13) {
-                o.g_b_val[0] = s;
-            } else {
-                const int q = p - kHeadFixed;
-                if (q < hd) o.g_b_pi[q] = s;
-                else if (q < 2 * hd) o.g_b_vf[q - hd] = s;
-                else if (q < 6 * hd) o.g_w_act[q - 2 * hd] = s;
-                else o.g_w_val[q - 6 * hd] = s;
-            }
+            red[q][col] = colsum_range(part, P, p, b0, b1);
         }
     }
-    if (bx == 0) {
-        __syncthreads();
-        if (threadIdx.x == 0) {
-            const float inv_m = 1.0f / (float)m;
-            const float pl = loss[0] * inv_m;
-            const float vl = loss[1] * inv_m;
-            float H = 0.f;
-            for (int j = 0; j < 4; ++j) H += 0.5f + kLogSqrt2Pi + log_std[j];
-            const float el = -H;
-            for (int j = 0; j < 4; ++j) {
-                const float g = loss[4 + j] - ent_coef;
-                o.g_log_std[j] = g;
-                sq += g * g;
-            }
-            o.stats[0] = pl + ent_coef * el + vf_coef * vl;
-            o.stats[1] = pl;
-            o.stats[2] = vl;
-            o.stats[3] = el;
-            o.stats[4] = loss[2] * inv_m;
-            o.stats[5] = loss[3] * inv_m;
-            o.stats[6] = adv_ms[0];
-            o.stats[7] = adv_ms[1];
+    __syncthreads();
+    float sq = 0.f;
+    if (q == 0 && p < P) {
+        float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+        int b = 0;
+        for (; b + 3 < ng; b += 4) {
+            s0 += red[b + 0][col];
+            s1 += red[b + 1][col];
+            s2 += red[b + 2][col];
+            s3 += red[b + 3][col];
         }
+        for (; b < ng; ++b) s0 += red[b][col];
+        sq = head_store(p, ((s0 + s1) + s2) + s3, hd, loss, o);
     }
+    if (bx == 0) sq += head_stats(loss, m, adv_ms, log_std, ent_coef, vf_coef, o);
     return sq;
 }
 
@@ -1572,9 +1643,6 @@ __global__ __launch_bounds__(kBlock) void ppo_head_finish_kernel(
                            o);
 }
 
-// first-level row groups of the partial sums (32 / 64 measured 6.62-6.69 vs
-// 6.67-6.72 PPO updates/s, round 4)
-constexpr int kHeadGroups = 16;
 
 inline int head_blocks(int64_t m) {
     const int64_t b = (m + 4 * kHeadTile - 1) / (4 * kHeadTile);  // >= 1 tile per wave
@@ -1642,8 +1710,8 @@ __device__ inline float chunk_sum_part(int bx, int64_t groups, int count, int64_
 // sum and the norm pass: 4 launches).
 struct FinishArgs {
     int bh, bf, bc;
-    // head
-    int h_ng, h_P, h_hd;
+    // head (h_direct: h_ng per-block rows at h_part2, summed in the finish)
+    int h_ng, h_P, h_hd, h_direct;
     int64_t h_m;
     const float *h_part2, *h_adv_ms, *log_std;
     float ent_coef, vf_coef;
@@ -1665,8 +1733,10 @@ __global__ __launch_bounds__(kBlock) void grad_finish_kernel(FinishArgs a) {
     int b = blockIdx.x;
     float sq;
     if (b < a.bh) {
-        sq = head_finish_part(b, a.h_ng, a.h_P, a.h_hd, a.h_m, a.h_part2, a.h_adv_ms, a.log_std,
-                              a.ent_coef, a.vf_coef, a.ho);
+        sq = a.h_direct ? head_finish_direct(b, a.h_ng, a.h_P, a.h_hd, a.h_m, a.h_part2,
+                                             a.h_adv_ms, a.log_std, a.ent_coef, a.vf_coef, a.ho)
+                        : head_finish_part(b, a.h_ng, a.h_P, a.h_hd, a.h_m, a.h_part2, a.h_adv_ms,
+                                           a.log_std, a.ent_coef, a.vf_coef, a.ho);
     } else if ((b -= a.bh) < a.bf) {
         sq = a.f_direct ? first_finish_direct(b, a.f_direct, a.f_n, a.f_K, a.f_nets, a.f_part2,
                                               a.fo)
@@ -1984,7 +2054,10 @@ static int first_blocks(int64_t m);
 
 // Block counts of grad_finish_kernel's three segments.
 static void finish_blocks(const dr_grad_finish *f, int &bh, int &bf, int &bc) {
-    bh = f->head_workspace ? (int)((kHeadFixed + 7 * f->head_hd + kBlock - 1) / kBlock) : 0;
+    const int64_t hP = kHeadFixed + 7 * f->head_hd;
+    bh = !f->head_workspace ? 0
+         : f->head_direct ? (int)((hP + 15) / 16)         // head_finish_direct: 16 per block
+                          : (int)((hP + kBlock - 1) / kBlock);
     const int64_t fP = 2 * (f->first_k + 1) * f->first_n;
     bf = !f->first_workspace ? 0
          : f->first_rows > 0 ? (int)((fP + 63) / 64)     // first_finish_direct: 64 per block
@@ -2059,6 +2132,11 @@ static int launch_grad_finish(const dr_grad_finish *f, void *workspace, size_t w
         a.h_part2 = reinterpret_cast<const float *>(reinterpret_cast<const char *>(part) +
                                                     align_up(sizeof(float) * (size_t)(nb * P + 2)));
         a.h_adv_ms = part + (int64_t)nb * P;
+        if (f->head_direct) {
+            a.h_direct = 1;
+            a.h_ng = nb;
+            a.h_part2 = part;
+        }
         a.log_std = f->log_std;
         a.ent_coef = f->ent_coef;
         a.vf_coef = f->vf_coef;
@@ -2282,6 +2360,8 @@ int dr_ppo_head_loss_backward(int64_t m, int64_t hd, int preact, const float *h_
     hipLaunchKernelGGL(ppo_head_kernel, dim3(nb), dim3(kBlock), sizeof(float) * 4 * P, st, a);
     int rc = check_launch("dr_ppo_head_loss_backward");
     if (rc) return rc;
+    // defer 2: the per-block rows are summed by the finish (head_direct)
+    if (defer == 2) return DR_OK;
     // two-level fixed-order reduction of the nb x P partials
     float *part2 = reinterpret_cast<float *>(
         reinterpret_cast<char *>(part) + align_up(sizeof(float) * (size_t)(nb * P + 2)));

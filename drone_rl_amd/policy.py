@@ -133,6 +133,8 @@ class ActorCritic:
         self.gemm_x6_fl = os.environ.get("DRONERL_X6_FL", "1") != "0"
         # its per-block rows summed by the deferred finish (no grouping launch)
         self.gemm_x6_fl_direct = os.environ.get("DRONERL_X6_FL_DIRECT", "1") != "0"
+        # the head kernel's per-block rows summed by the deferred finish too
+        self.head_direct = os.environ.get("DRONERL_HEAD_DIRECT", "1") != "0"
         self._x6 = None
         self.flat = torch.zeros(off, dtype=torch.float32, device=self.device)
         self.reset_parameters(seed, log_std_init)
@@ -402,7 +404,10 @@ class FusedTrainStep:
                      self.gview("action.b"), self.gview("value.w"), self.gview("value.b"),
                      self.gview(f"pi{top}.b"), self.gview(f"vf{top}.b"),
                      self.gview("log_std"), rows, preact=preact, adv_ready=adv_ready,
-                     stats_out=stats_out, defer=defer_finish, **top_bias(pol, self._acts2))
+                     stats_out=stats_out,
+                     defer=(2 if pol.head_direct else 1) if defer_finish else 0,
+                     **top_bias(pol, self._acts2))
+        self._head_direct = bool(defer_finish and pol.head_direct)
         mark("ppo_head")
         if depth == 1:                        # the head kernel gave grad_z of layer 0
             if rows is not None:
@@ -480,6 +485,7 @@ class FusedTrainStep:
         d.first_workspace = self._first.ws.data_ptr()
         d.first_m, d.first_k, d.first_n = M, pol.obs_dim, pol.net_arch[0]
         d.first_rows = self._first_rows
+        d.head_direct = int(self._head_direct)
         d.g_w0, d.g_b0, d.g_w1, d.g_b1 = gp("pi0.w"), gp("pi0.b"), gp("vf0.w"), gp("vf0.b")
         out = pol.p2(1, "w", self.grad)                        # (2, N, K), contiguous
         N, Kd = out.shape[1], out.shape[2]

@@ -336,7 +336,8 @@ class HeadLossBackward:
         (adv_part=self.adv_part) for this minibatch; stats_out (8 f32)
         receives the stats instead of self.stats; zb_pi / zb_vf as
         policy_heads.  With defer the gradient / stats outputs are written
-        later by ClipAdam.step_finish (GradFinish)."""
+        later by ClipAdam.step_finish (GradFinish); defer=2 leaves the
+        per-block rows unreduced for a finish with head_direct = 1."""
         assert h_pi.shape == (self.m, self.hd) and aux.shape[1] == 3
         assert rows is not None or aux.shape[0] == self.m
         stats = self.stats if stats_out is None else stats_out
@@ -349,7 +350,7 @@ class HeadLossBackward:
             ptr(_f32(actions)), ptr(_f32(aux)), _rows(rows), float(self.clip), float(self.ent),
             float(self.vf), norm, ptr(gz_pi), ptr(gz_vf), ptr(g_w_act), ptr(g_b_act),
             ptr(g_w_val), ptr(g_b_val), ptr(g_b_pi), ptr(g_b_vf), ptr(g_log_std),
-            ptr(stats), int(bool(defer)), ptr(self.ws), self.ws.numel(), _s(h_pi)))
+            ptr(stats), int(defer), ptr(self.ws), self.ws.numel(), _s(h_pi)))
         return stats
 
 

@@ -394,7 +394,8 @@ int dr_policy_heads(int64_t m, int64_t hd, int preact, const float *h_pi,
    normalize_advantage: 0 off, 1 on, 2 on with the advantage partials
    already written to the head of `workspace` by dr_gather_minibatch.
    defer != 0: the gradient / stats outputs are NOT written here; the
-   reduced partials stay in `workspace` for dr_grad_finish_clip_adam. */
+   reduced partials stay in `workspace` for dr_grad_finish_clip_adam (defer
+   2: unreduced, for a finish with head_direct = 1; no grouping launch). */
 size_t dr_ppo_head_workspace_bytes(int64_t m, int64_t hd);
 int dr_ppo_head_loss_backward(int64_t m, int64_t hd, int preact, const float *h_pi,
                               const float *h_vf, const float *zb_pi,
@@ -474,6 +475,11 @@ typedef struct dr_grad_finish {
        dr_gemm_x6_bwd_first(..., direct = 1) (= dr_gemm_x6_bwd_first_rows(m);
        summed by the finish, no grouping launch).  (ABI v15.) */
     int64_t first_rows;
+    /* 0: head_workspace holds the level-1 groups; 1: the head kernel's
+       per-block rows, left by dr_ppo_head_loss_backward(..., defer = 2)
+       (summed by the finish in the grouped order: bitwise the same).
+       (ABI v15.) */
+    int64_t head_direct;
 } dr_grad_finish;
 
 /* dr_clip_adam fused with the deferred gradient finish: one launch reduces
