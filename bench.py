@@ -741,6 +741,10 @@ def ppo_roofline(cfg, s_per_update, ktimes, rocprof=None, isolated=None, rocprof
             "ppo_head": 2 * 1024 + 2 * 1024 + 44,
             "first_layer_bwd": 2 * 2 * 1024 + 60,
             "split_x": 15 * 4 + 3136 // 32}            # x in, its three-plane record out
+    if "gemm_x6_bwd_first" in ktimes and "split_x" not in ktimes:
+        # dr_linear_tanh2_x6: the observation image (98 B per row) and the
+        # weight images (2 MB per launch, 32 B per row at 65,536) as well
+        rows["linear_tanh"] += 3136 // 32 + 32
     # the fused input-gradient GEMM also runs the first layer's weight
     # gradient (16 x 256 per net and row, features + bias) as x6 MFMA work
     fl_flop = gemm_flop + 2 * 2 * M * 16 * 256

@@ -146,6 +146,8 @@ SIGNATURES = {
     "dr_gemm_x6_bwd_first": (c_int, [c_int64, c_int64, c_int64, _P, _P, _P, _P, _P, c_size_t,
                                      c_int, _P]),
     "dr_gemm_x6_bwd_first_rows": (c_int64, [c_int64]),
+    "dr_linear_tanh2_x6": (c_int, [c_int64, c_int64, c_int64, _P, _P, _P, _P, _P, _P, _P, _P,
+                                   _P, _P, _P, _P]),
 }
 
 _lib = None

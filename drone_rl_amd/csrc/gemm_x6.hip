@@ -43,47 +43,16 @@
 namespace dr {
 namespace {
 
-constexpr int XK = 256;                 // reduction length (hidden width)
-constexpr int XN = 256;                 // output columns
 #define X6_S2(x) #x
 #define X6_S(x) X6_S2(x)
 constexpr int XWAVES = 8;               // waves of the weight-gradient kernel
 constexpr int XTHREADS = 64 * XWAVES;
-constexpr int64_t W_IMG = (int64_t)3 * XN * XK * 2;   // 384 KB per net: 3 bf16 planes
 
-// Weight image of `batch` nets in the weight-stationary kernel's register
-// order: img[b][w][j][s][p][lane][16 B] is the MFMA B fragment of plane p of
-// Bt (= W for transpose 0, W^T for transpose 1; W (256, 256) row-major per
-// net) for wave w's column tile j and k16 step s: lane = fr + 32 fh holds
-// Bt[n = 64 w + 32 j + fr][k = 16 s + 8 fh .. + 7], so each fragment is one
-// coalesced 1-KB load.  One thread per (b, n, 8-k chunk).
-__device__ inline int64_t wimg_off(int n, int k0) {
-    const int w = n >> 6, j = (n >> 5) & 1, fr = n & 31, s = k0 >> 4, fh = (k0 >> 3) & 1;
-    return ((int64_t)((w * 2 + j) * 16 + s) * 3 * 64 + fr + 32 * fh) * 16;
-}
-constexpr int64_t W_FRAG = 64 * 16;     // one plane fragment: 1 KB
+// the weight image (wimg_off, x6_split.h), one thread per (b, n, 8-k chunk)
 __global__ __launch_bounds__(256) void split_weights_kernel(const float *__restrict__ w,
                                                             int transpose, int batch,
                                                             uint8_t *__restrict__ img) {
-    const int t = blockIdx.x * 256 + threadIdx.x;
-    if (t >= batch * XN * (XK / 8)) return;
-    if (transpose == 2) {      // both images: blockIdx.y 0 -> W^T form, 1 -> W form
-        transpose = (int)blockIdx.y;
-        img += (int64_t)blockIdx.y * batch * W_IMG;
-    }
-    const int c = t & 31, n = (t >> 5) & (XN - 1), b = t >> 13;
-    const float *wb = w + (int64_t)b * XN * XK;
-    const int k0 = c * 8;
-    float x[8];
-#pragma unroll
-    for (int j = 0; j < 8; ++j)
-        x[j] = transpose ? wb[(int64_t)(k0 + j) * XN + n] : wb[(int64_t)n * XK + k0 + j];
-    u32x4_t h, m, l;
-    split8(x, h, m, l);
-    uint8_t *base = img + (int64_t)b * W_IMG + wimg_off(n, k0);
-    *reinterpret_cast<u32x4_t *>(base) = h;
-    *reinterpret_cast<u32x4_t *>(base + W_FRAG) = m;
-    *reinterpret_cast<u32x4_t *>(base + 2 * W_FRAG) = l;
+    split_weights_item(w, transpose, batch, img, blockIdx.x * 256 + threadIdx.x, blockIdx.y);
 }
 
 // global_load_lds_dwordx4 by inline asm (the saddr form: a wave-uniform
@@ -152,7 +121,7 @@ __device__ inline uint32_t lds_addr(const uint8_t *p) {
 // split VALU into the MFMA asm (so it issues in the MFMAs' shadow) needs ~10
 // more VGPRs than the 512-register budget leaves (weights 384 + accumulators
 // 64 + fragments 36 + split): the allocator spilled the weights.
-constexpr int WS_RS = 32;                            // rows per row step
+constexpr int WS_RS = X6_RS;                         // rows per row step
 constexpr int WS_PLANE = WS_RS * XK * 2;             // 16 KB: one plane of a row step
 constexpr int WS_PSTAGE = 3 * WS_PLANE;              // 48 KB
 constexpr int WS_FSLOT = WS_RS * XK * 4;             // 32 KB: f32 rows of a row step
@@ -721,39 +690,10 @@ __global__ __launch_bounds__(XTHREADS) void gemm_x6_wgrad_kernel(
 // activation rows are register-staged by compiler-tracked loads four split
 // half-units ahead (no LDS-DMA staging: every vector memory op is visible to
 // the compiler's waitcnt pass).  LDS holds only the double-buffered planes.
-constexpr int FL_F = 16;                                // 15 features + the bias column
-constexpr int XREC = 64 + 3 * 2 * 2 * FL_F * 16;         // 3,136 B of X planes per row step
-
-// byte offset in a row step's X record of plane p, K step j, half fh,
-// feature f: the 8 bf16 K values of A-fragment lane (f or 16 + f, fh)
-__host__ __device__ inline int xrec_off(int p, int j, int fh, int f) {
-    return 64 + (((p * 2 + j) * 2 + fh) * FL_F + f) * 16;
-}
-
-// X planes image: one thread per (row step g, K step j, half fh, feature f),
-// the rows 16 j + 4 fh + (e & 3) + 8 (e >> 2), e = 0..7, of feature f of x
-// (m x k f32 row-major; feature 15 is the constant 1), split exactly like
-// the GEMM operands; the record's first 64 B are zero (the A fragment of the
-// other column tile's lanes).
+// the X planes image (xrec_off, x6_split.h)
 __global__ __launch_bounds__(256) void split_x_kernel(const float *__restrict__ x, int64_t m,
                                                       int k, uint8_t *__restrict__ img) {
-    const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    const int64_t g = t >> 6;
-    if (g >= m / WS_RS) return;
-    const int f = (int)(t & 15), fh = (int)((t >> 4) & 1), j = (int)((t >> 5) & 1);
-    uint8_t *rec = img + g * XREC;
-    if ((t & 63) < 4) reinterpret_cast<u32x4_t *>(rec)[t & 3] = (u32x4_t){0u, 0u, 0u, 0u};
-    float v[8];
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {
-        const int64_t row = g * WS_RS + 16 * j + 4 * fh + (e & 3) + 8 * (e >> 2);
-        v[e] = f < k ? x[row * k + f] : (f == FL_F - 1 ? 1.0f : 0.0f);
-    }
-    u32x4_t h, mm, l;
-    split8(v, h, mm, l);
-    *reinterpret_cast<u32x4_t *>(rec + xrec_off(0, j, fh, f)) = h;
-    *reinterpret_cast<u32x4_t *>(rec + xrec_off(1, j, fh, f)) = mm;
-    *reinterpret_cast<u32x4_t *>(rec + xrec_off(2, j, fh, f)) = l;
+    split_x_item(x, nullptr, m, k, img, (int64_t)blockIdx.x * 256 + threadIdx.x);
 }
 
 __global__ __launch_bounds__(WS_THREADS, 1) void gemm_x6_fl_kernel(
@@ -1102,6 +1042,8 @@ int dr_gemm_x6(int64_t batch, int64_t m, const float *a, const void *img, float 
     int grid = units < n_cu ? units : n_cu;
     grid -= grid % (int)batch;
     // plain stores: the next kernel reads C back from the Infinity Cache
+    // (round 5: the streamed-l-plane form of gemm_x6_fl_kernel without its
+    // epilogue, 112-113 vs 103-109 us for this kernel, bitwise the same C)
     hipLaunchKernelGGL(gemm_x6_ws_kernel, dim3(grid), dim3(WS_THREADS), 0,
                        static_cast<hipStream_t>(stream), a, static_cast<const uint8_t *>(img), c,
                        m, (int)batch);

@@ -17,6 +17,7 @@
 #include <string>
 
 #include "common.h"
+#include "x6_split.h"
 
 #pragma clang fp contract(off)
 
@@ -866,6 +867,30 @@ struct LayerPair {
     float *h[2];
 };
 
+// The x6 GEMMs' operand images built by extra blocks of the first-layer
+// forward launch (linear_tanh_kernel<K, true>, its last grid row): the
+// 256 x 256 layer's weight images in both forms (split_weights_kernel's
+// items) and, with ximg, the minibatch observation image of the fused
+// input-gradient GEMM (split_x_kernel's items) -- two launches fewer per
+// optimizer step, the same bytes.
+struct X6Aux {
+    const float *w256;         // (2, 256, 256): both nets' weights
+    uint8_t *img;              // 2 x 2 x W_IMG: W^T forms, then W forms
+    uint8_t *ximg;             // nullable
+};
+constexpr int kAuxWBlocks = 2 * XN * (XK / 8) / kBlock;    // per weight form
+
+__device__ inline void x6_aux_block(int bx, int64_t m, int k, const float *__restrict__ x,
+                                    const int32_t *__restrict__ rows, const X6Aux &aux) {
+    if (bx < 2 * kAuxWBlocks) {
+        split_weights_item(aux.w256, 2, 2, aux.img, (bx % kAuxWBlocks) * kBlock + threadIdx.x,
+                           bx / kAuxWBlocks);
+        return;
+    }
+    bx -= 2 * kAuxWBlocks;
+    if (aux.ximg) split_x_item(x, rows, m, k, aux.ximg, (int64_t)bx * kBlock + threadIdx.x);
+}
+
 // (round 3 A/B, removed in round 4: two rows per wave and iteration measured
 // 38.1 vs 37.6-37.8 us per call; the input row through per-lane loads and
 // readlanes instead of scalar loads, slower)
@@ -884,11 +909,17 @@ struct LayerPair {
 #ifndef DR_LT_MAXB
 #define DR_LT_MAXB 1024
 #endif
-template <int K>
+template <int K, bool AUX>
 __global__ __launch_bounds__(kBlock) void linear_tanh_kernel(int64_t m, int n,
                                                              const float *__restrict__ x,
                                                              const int32_t *__restrict__ rows,
-                                                             LayerPair lp) {
+                                                             LayerPair lp, X6Aux aux) {
+    if constexpr (AUX) {
+        if (blockIdx.y == gridDim.y - 1) {
+            x6_aux_block(blockIdx.x, m, K, x, rows, aux);
+            return;
+        }
+    }
     const float *__restrict__ w = lp.w[blockIdx.y];
     const float *__restrict__ b = lp.b[blockIdx.y];
     float *__restrict__ h = lp.h[blockIdx.y];
@@ -2258,8 +2289,8 @@ static int launch_linear_tanh(const char *who, int nets, int64_t m, int64_t k, i
     switch (k) {
 #define DR_LT_CASE(K)                                                                      \
     case K:                                                                                \
-        hipLaunchKernelGGL(linear_tanh_kernel<K>, dim3(nb, nets), dim3(kBlock), 0, st, m,   \
-                           (int)n, x, rows, lp);                                           \
+        hipLaunchKernelGGL((linear_tanh_kernel<K, false>), dim3(nb, nets), dim3(kBlock), 0, st, \
+                           m, (int)n, x, rows, lp, X6Aux{});                               \
         break;
         DR_LT_CASE(4) DR_LT_CASE(8) DR_LT_CASE(12) DR_LT_CASE(15) DR_LT_CASE(16)
         DR_LT_CASE(18) DR_LT_CASE(24) DR_LT_CASE(32)
@@ -2282,6 +2313,30 @@ int dr_linear_tanh2(int64_t m, int64_t k, int64_t n, const float *x, const int32
                     const float *b1, float *h1, void *stream) {
     const LayerPair lp{{w0, w1}, {b0, b1}, {h0, h1}};
     return launch_linear_tanh("dr_linear_tanh2", 2, m, k, n, x, rows, lp, stream);
+}
+
+int dr_linear_tanh2_x6(int64_t m, int64_t k, int64_t n, const float *x, const int32_t *rows,
+                       const float *w0, const float *b0, float *h0, const float *w1,
+                       const float *b1, float *h1, const float *w256, void *img, void *ximg,
+                       void *stream) {
+    const char *who = "dr_linear_tanh2_x6";
+    if (m < 1 || !x || n != 256 || k != 15 || !w0 || !b0 || !h0 || !w1 || !b1 || !h1 ||
+        !w256 || !img || ((((uintptr_t)h0) | ((uintptr_t)h1) | ((uintptr_t)w0) |
+                           ((uintptr_t)w1) | ((uintptr_t)img) | ((uintptr_t)ximg)) & 15))
+        return fail0(DR_ERR_INVALID, std::string(who) +
+                                         ": bad arguments (k 15, n 256, 16-byte aligned "
+                                         "outputs, weights and images)");
+    if (ximg && (m % 128 || m > (int64_t(1) << 26)))
+        return fail0(DR_ERR_INVALID, std::string(who) + ": ximg needs m a multiple of 128");
+    const LayerPair lp{{w0, w1}, {b0, b1}, {h0, h1}};
+    const int64_t nbl = (m + DR_LT_RPB - 1) / DR_LT_RPB;
+    const int nb = (int)(nbl < DR_LT_MAXB ? nbl : DR_LT_MAXB);
+    const int64_t naux = 2 * kAuxWBlocks + (ximg ? (2 * m + kBlock - 1) / kBlock : 0);
+    const int gx = (int)(naux > nb ? naux : nb);
+    hipLaunchKernelGGL((linear_tanh_kernel<15, true>), dim3(gx, 3), dim3(kBlock), 0,
+                       as_stream(stream), m, 256, x, rows, lp,
+                       X6Aux{w256, static_cast<uint8_t *>(img), static_cast<uint8_t *>(ximg)});
+    return check_launch(who);
 }
 
 int dr_policy_heads(int64_t m, int64_t hd, int preact, const float *h_pi, const float *h_vf,

@@ -2,8 +2,8 @@
 // x6 GEMM scheme of gemm_x6.hip: x = h + m + l, each plane RNE of the
 // remainder, x - h and (x - h) - m exact in f32, the last remainder a bf16),
 // used by the weight-image split, the weight-gradient GEMM's operands and the
-// fused first-layer backward's grad_z1 / observation planes (all in
-// gemm_x6.hip).
+// fused first-layer backward's grad_z1 / observation planes (gemm_x6.hip),
+// and the operand images below (also built by ppo_kernels.hip).
 #pragma once
 
 #include <cstdint>
@@ -36,6 +36,89 @@ __device__ inline void split8(const float x[8], u32x4_t &h, u32x4_t &m, u32x4_t 
         m[q] = pm;
         l[q] = pk_bf16(sa, sb);
     }
+}
+
+// ---------------------------------------------------------------------------
+// Operand images of the x6 GEMMs (gemm_x6.hip), built by split_weights_kernel
+// / split_x_kernel and by the first-layer forward's auxiliary blocks
+// (ppo_kernels.hip linear_tanh_kernel<K, true>): the same items, so every
+// producer writes the same bytes.
+constexpr int XK = 256;                 // reduction length (hidden width)
+constexpr int XN = 256;                 // output columns
+constexpr int X6_RS = 32;               // rows per row step of the GEMM kernels
+constexpr int64_t W_IMG = (int64_t)3 * XN * XK * 2;   // 384 KB per net: 3 bf16 planes
+constexpr int64_t W_FRAG = 64 * 16;     // one plane fragment: 1 KB
+
+// Weight image of `batch` nets in the weight-stationary kernel's register
+// order: img[b][w][j][s][p][lane][16 B] is the MFMA B fragment of plane p of
+// Bt (= W for transpose 0, W^T for transpose 1; W (256, 256) row-major per
+// net) for wave w's column tile j and k16 step s: lane = fr + 32 fh holds
+// Bt[n = 64 w + 32 j + fr][k = 16 s + 8 fh .. + 7], so each fragment is one
+// coalesced 1-KB load.
+__host__ __device__ inline int64_t wimg_off(int n, int k0) {
+    const int w = n >> 6, j = (n >> 5) & 1, fr = n & 31, s = k0 >> 4, fh = (k0 >> 3) & 1;
+    return ((int64_t)((w * 2 + j) * 16 + s) * 3 * 64 + fr + 32 * fh) * 16;
+}
+
+// Item t (b, n, 8-k chunk) of the weight image; transpose 2 builds both forms
+// (y 0: the W^T form at img, y 1: the W form after it).
+__device__ inline void split_weights_item(const float *__restrict__ w, int transpose, int batch,
+                                          uint8_t *__restrict__ img, int t, int y) {
+    if (t >= batch * XN * (XK / 8)) return;
+    if (transpose == 2) {
+        transpose = y;
+        img += (int64_t)y * batch * W_IMG;
+    }
+    const int c = t & 31, n = (t >> 5) & (XN - 1), b = t >> 13;
+    const float *wb = w + (int64_t)b * XN * XK;
+    const int k0 = c * 8;
+    float x[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+        x[j] = transpose ? wb[(int64_t)(k0 + j) * XN + n] : wb[(int64_t)n * XK + k0 + j];
+    u32x4_t h, m, l;
+    split8(x, h, m, l);
+    uint8_t *base = img + (int64_t)b * W_IMG + wimg_off(n, k0);
+    *reinterpret_cast<u32x4_t *>(base) = h;
+    *reinterpret_cast<u32x4_t *>(base + W_FRAG) = m;
+    *reinterpret_cast<u32x4_t *>(base + 2 * W_FRAG) = l;
+}
+
+// The first-layer observation image of the fused input-gradient GEMM
+// (gemm_x6_fl_kernel): per row step a 3,136-B record of X^T's A fragments.
+constexpr int FL_F = 16;                                // 15 features + the bias column
+constexpr int XREC = 64 + 3 * 2 * 2 * FL_F * 16;         // 3,136 B of X planes per row step
+
+// byte offset in a row step's X record of plane p, K step j, half fh,
+// feature f: the 8 bf16 K values of A-fragment lane (f or 16 + f, fh)
+__host__ __device__ inline int xrec_off(int p, int j, int fh, int f) {
+    return 64 + (((p * 2 + j) * 2 + fh) * FL_F + f) * 16;
+}
+
+// Item t = (row step g, K step j, half fh, feature f): the rows 16 j + 4 fh +
+// (e & 3) + 8 (e >> 2), e = 0..7, of feature f of x (m x k f32 row-major,
+// row r read as x[rows[r]] when rows is given; feature 15 is the constant
+// 1), split exactly like the GEMM operands; the record's first 64 B are zero
+// (the A fragment of the other column tile's lanes).
+__device__ inline void split_x_item(const float *__restrict__ x, const int32_t *__restrict__ rows,
+                                    int64_t m, int k, uint8_t *__restrict__ img, int64_t t) {
+    const int64_t g = t >> 6;
+    if (g >= m / X6_RS) return;
+    const int f = (int)(t & 15), fh = (int)((t >> 4) & 1), j = (int)((t >> 5) & 1);
+    uint8_t *rec = img + g * XREC;
+    if ((t & 63) < 4) reinterpret_cast<u32x4_t *>(rec)[t & 3] = (u32x4_t){0u, 0u, 0u, 0u};
+    float v[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+        const int64_t row = g * X6_RS + 16 * j + 4 * fh + (e & 3) + 8 * (e >> 2);
+        const int64_t src = rows ? (int64_t)rows[row] : row;
+        v[e] = f < k ? x[src * k + f] : (f == FL_F - 1 ? 1.0f : 0.0f);
+    }
+    u32x4_t h, mm, l;
+    split8(v, h, mm, l);
+    *reinterpret_cast<u32x4_t *>(rec + xrec_off(0, j, fh, f)) = h;
+    *reinterpret_cast<u32x4_t *>(rec + xrec_off(1, j, fh, f)) = mm;
+    *reinterpret_cast<u32x4_t *>(rec + xrec_off(2, j, fh, f)) = l;
 }
 
 }  // namespace dr

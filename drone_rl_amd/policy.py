@@ -133,6 +133,9 @@ class ActorCritic:
         self.gemm_x6_fl = os.environ.get("DRONERL_X6_FL", "1") != "0"
         # its per-block rows summed by the deferred finish (no grouping launch)
         self.gemm_x6_fl_direct = os.environ.get("DRONERL_X6_FL_DIRECT", "1") != "0"
+        # the x6 operand images built by the first layer's forward launch
+        # (dr_linear_tanh2_x6) instead of their own launches
+        self.x6_fused_images = os.environ.get("DRONERL_X6_FUSED_IMAGES", "1") != "0"
         # the head kernel's per-block rows summed by the deferred finish too
         self.head_direct = os.environ.get("DRONERL_HEAD_DIRECT", "1") != "0"
         self._x6 = None
@@ -395,8 +398,18 @@ class FusedTrainStep:
             raise ValueError("defer_finish needs a 2-hidden-layer net and no on_ready")
         mark = self.mark or _no_mark
         self._first_rows = 0
+        # the fused input-gradient GEMM + first-layer backward
+        # (dr_gemm_x6_bwd_first): its observation image is built by the
+        # first layer's forward launch
+        fl = (defer_finish and rows is None and pol.gemm_x6_fl and pol.obs_dim == 15 and
+              pol.net_arch == (256, 256) and x6_weights(pol, M) is not None)
+        if fl and getattr(self, "_ximg", None) is None:
+            from . import _lib
+            self._ximg = torch.empty(_lib.lib().dr_gemm_x6_x_bytes(M), dtype=torch.uint8,
+                                     device=pol.device)
+        fused_img = fl and pol.x6_fused_images
         hs = hidden_forward(pol, obs, self._acts, self._acts2, rows, top_preact=preact,
-                            mark=self.mark)
+                            mark=self.mark, ximg=self._ximg if fused_img else None)
         gz = self._gz2[top]
         stats = head(hs["pi"][top], hs["vf"][top], pol.p("action.w"), pol.p("action.b"),
                      pol.p("value.w"), pol.p("value.b"), pol.log_std, actions, aux,
@@ -425,19 +438,16 @@ class FusedTrainStep:
                 on_ready(self.first_layer_end(), self.grad.numel())
             g = self._g2.view(-1)[:2 * M * n_in].view(2, M, n_in)
             xw = x6_weights(pol, M) if k == 1 else None
-            if (xw is not None and defer_finish and rows is None and pol.gemm_x6_fl and
-                    pol.obs_dim == 15 and n_in == 256):
+            if k == 1 and fl:
                 # grad_h1 never stored: the first layer's backward in the
                 # GEMM's epilogue, its partials left in the first-layer
                 # workspace for the deferred finish (dr_gemm_x6_bwd_first)
                 from . import _lib
-                if getattr(self, "_ximg", None) is None:
-                    self._ximg = torch.empty(_lib.lib().dr_gemm_x6_x_bytes(M), dtype=torch.uint8,
-                                             device=pol.device)
                 st = torch.cuda.current_stream(pol.device).cuda_stream
-                _lib.check(_lib.lib().dr_gemm_x6_split_x(M, 15, obs.data_ptr(),
-                                                         self._ximg.data_ptr(), st))
-                mark("split_x")
+                if not fused_img:
+                    _lib.check(_lib.lib().dr_gemm_x6_split_x(M, 15, obs.data_ptr(),
+                                                             self._ximg.data_ptr(), st))
+                    mark("split_x")
                 direct = int(pol.gemm_x6_fl_direct)
                 _lib.check(_lib.lib().dr_gemm_x6_bwd_first(
                     2, M, 15, gz.data_ptr(), xw.bwd.data_ptr(), x.data_ptr(),
@@ -559,7 +569,7 @@ def fusable(pol: ActorCritic) -> bool:
 
 @torch.no_grad()
 def hidden_forward(pol: ActorCritic, obs, acts, acts2=None, rows=None, top_preact=False,
-                   mark=None):
+                   mark=None, ximg=None):
     """Hidden activations of the pi and vf MLPs into preallocated buffers
     acts[pre][k] (M, net_arch[k]); with acts2 (the (2, M, n) buffers that
     acts views) each layer's tanh runs once over both MLPs; with rows the
@@ -568,19 +578,34 @@ def hidden_forward(pol: ActorCritic, obs, acts, acts2=None, rows=None, top_preac
     the head kernel, adds the bias and applies tanh on load (top_bias(pol)
     gives the pointers), so the (M, n) tanh pass is skipped and both MLPs'
     top GEMMs run as ONE batched GEMM (no bias epilogue; 125 us against
-    2 x 74 us for two addmm at M = 65,536, MI355X-tuned solutions)."""
+    2 x 74 us for two addmm at M = 65,536, MI355X-tuned solutions).
+    On the x6 path the first layer's launch also re-splits the 256 x 256
+    weights into their images (they may have changed since) and, with ximg,
+    builds the fused input-gradient GEMM's observation image
+    (dr_linear_tanh2_x6)."""
     from . import ppo_kernels as K
     mark = mark or _no_mark
     top = len(pol.net_arch) - 1
-    K.linear_tanh2(obs, pol.p("pi0.w"), pol.p("pi0.b"), acts["pi"][0],
-                   pol.p("vf0.w"), pol.p("vf0.b"), acts["vf"][0], rows)
+    xw = (x6_weights(pol, acts2[0].shape[1])
+          if (top_preact and top == 1 and acts2 is not None and pol.obs_dim == 15 and
+              pol.x6_fused_images) else None)
+    if xw is not None:
+        K.linear_tanh2_x6(obs, pol.p("pi0.w"), pol.p("pi0.b"), acts["pi"][0],
+                          pol.p("vf0.w"), pol.p("vf0.b"), acts["vf"][0], pol.p2(1, "w"),
+                          xw.img, ximg, rows)
+    else:
+        assert ximg is None
+        K.linear_tanh2(obs, pol.p("pi0.w"), pol.p("pi0.b"), acts["pi"][0],
+                       pol.p("vf0.w"), pol.p("vf0.b"), acts["vf"][0], rows)
     mark("linear_tanh")
     for k in range(1, len(pol.net_arch)):
         if top_preact and k == top and acts2 is not None:
-            xw = x6_weights(pol, acts2[k - 1].shape[1]) if k == 1 else None
+            if k == 1 and xw is None:
+                xw = x6_weights(pol, acts2[k - 1].shape[1])
+                if xw is not None:
+                    xw.refresh()             # the weights may have changed since
+                    mark("split_weights")
             if xw is not None:
-                xw.refresh()                 # the weights may have changed since
-                mark("split_weights")
                 gemm_x6(acts2[k - 1], xw.fwd, acts2[k])
                 mark("gemm_x6_fwd")
             else:

@@ -278,6 +278,20 @@ def linear_tanh2(x, w0, b0, h0, w1, b1, h1, rows=None):
     return h0, h1
 
 
+def linear_tanh2_x6(x, w0, b0, h0, w1, b1, h1, w256, img, ximg=None, rows=None):
+    """linear_tanh2 (k 15, n 256) with the 256 x 256 layer's x6 weight images
+    (both forms, from w256 (2, 256, 256)) into img and, with ximg, the
+    observation image of dr_gemm_x6_bwd_first built in the same launch."""
+    k = x.shape[1]
+    m, n = h0.shape
+    assert h1.shape == (m, n) and w0.shape == w1.shape == (n, k)
+    assert w256.shape == (2, 256, 256) and w256.is_contiguous()
+    check(_lib.lib().dr_linear_tanh2_x6(m, k, n, ptr(_f32(x)), _rows(rows), ptr(_f32(w0)),
+                                        ptr(_f32(b0)), ptr(h0), ptr(_f32(w1)), ptr(_f32(b1)),
+                                        ptr(h1), ptr(w256), ptr(img), ptr(ximg), _s(x)))
+    return h0, h1
+
+
 def gather_minibatch(idx, obs, actions, aux, obs_out, actions_out, aux_out, adv_part=None):
     """obs_out / actions_out / aux_out = rows idx of obs (., d) / actions
     (., 4) / aux (., 3), one launch; with adv_part (a HeadLossBackward's

@@ -595,6 +595,18 @@ int dr_gemm_x6_bwd_first(int64_t batch, int64_t m, int64_t k, const float *grad_
    at m rows on the current device (0 for an invalid m). */
 int64_t dr_gemm_x6_bwd_first_rows(int64_t m);
 
+/* dr_linear_tanh2 (k = 15, n = 256) with the x6 GEMMs' operand images built
+   by extra blocks of the same launch: both weight forms of the 256 x 256
+   layer into img (dr_gemm_x6_split_weights(2, w256, 2, img) -- w256 the
+   (2, 256, 256) weights of both nets) and, with ximg non-null, the
+   observation image of dr_gemm_x6_bwd_first (dr_gemm_x6_split_x of x, read
+   through rows when given; m a multiple of 128).  The same bytes as the
+   separate launches.  (ABI v15.) */
+int dr_linear_tanh2_x6(int64_t m, int64_t k, int64_t n, const float *x, const int32_t *rows,
+                       const float *w0, const float *b0, float *h0, const float *w1,
+                       const float *b1, float *h1, const float *w256, void *img, void *ximg,
+                       void *stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -174,3 +174,47 @@ def test_trainer_step_fused_equals_unfused_within_bound(monkeypatch):
             a, b = first_f[k].double(), first_u[k].double()
             scale = b.abs().max().item() + 1e-30
             assert (a - b).abs().max().item() <= 1e-4 * scale, k
+
+
+@pytest.mark.parametrize("m,with_rows", [(128, False), (65536, False), (4096, True)])
+def test_linear_tanh2_x6_builds_the_same_images(m, with_rows):
+    """dr_linear_tanh2_x6: h0 / h1 bitwise dr_linear_tanh2's, the weight
+    images bitwise dr_gemm_x6_split_weights(transpose 2)'s and the
+    observation image bitwise dr_gemm_x6_split_x's (of x[rows] with rows)."""
+    L = _lib.lib()
+    s = torch.cuda.current_stream().cuda_stream
+    g = torch.Generator().manual_seed(m + int(with_rows))
+    total = 3 * m if with_rows else m
+    x = torch.randn(total, 15, generator=g).cuda()
+    rows = (torch.randperm(total, generator=g)[:m].to(torch.int32).cuda() if with_rows
+            else None)
+    w0, w1 = (torch.randn(256, 15, generator=g).cuda() * 0.3 for _ in range(2))
+    b0, b1 = (torch.randn(256, generator=g).cuda() * 0.1 for _ in range(2))
+    w256 = (torch.randn(2, 256, 256, generator=g) * 0.06).cuda()
+    h = [torch.empty(m, 256, device="cuda") for _ in range(4)]
+    nb = L.dr_gemm_x6_weights_bytes(2)
+    img_a = torch.zeros(2 * nb, dtype=torch.uint8, device="cuda")
+    img_b = torch.zeros(2 * nb, dtype=torch.uint8, device="cuda")
+    xi_a = torch.zeros(L.dr_gemm_x6_x_bytes(m), dtype=torch.uint8, device="cuda")
+    xi_b = torch.zeros_like(xi_a)
+    rp = ptr(rows)
+    check(L.dr_linear_tanh2(m, 15, 256, ptr(x), rp, ptr(w0), ptr(b0), ptr(h[0]), ptr(w1),
+                            ptr(b1), ptr(h[1]), s))
+    check(L.dr_gemm_x6_split_weights(2, ptr(w256), 2, ptr(img_a), s))
+    xg = x[rows.long()].contiguous() if with_rows else x
+    check(L.dr_gemm_x6_split_x(m, 15, ptr(xg), ptr(xi_a), s))
+    check(L.dr_linear_tanh2_x6(m, 15, 256, ptr(x), rp, ptr(w0), ptr(b0), ptr(h[2]), ptr(w1),
+                               ptr(b1), ptr(h[3]), ptr(w256), ptr(img_b), ptr(xi_b), s))
+    torch.cuda.synchronize()
+    assert torch.equal(h[0], h[2]) and torch.equal(h[1], h[3])
+    assert torch.equal(img_a, img_b)
+    assert torch.equal(xi_a, xi_b)
+    # without the observation image: the weight images alone
+    img_c = torch.zeros_like(img_a)
+    check(L.dr_linear_tanh2_x6(m, 15, 256, ptr(x), rp, ptr(w0), ptr(b0), ptr(h[2]), ptr(w1),
+                               ptr(b1), ptr(h[3]), ptr(w256), ptr(img_c), None, s))
+    torch.cuda.synchronize()
+    assert torch.equal(img_a, img_c) and torch.equal(h[0], h[2])
+    assert L.dr_linear_tanh2_x6(m, 16, 256, ptr(x), rp, ptr(w0), ptr(b0), ptr(h[2]), ptr(w1),
+                                ptr(b1), ptr(h[3]), ptr(w256), ptr(img_c), None,
+                                s) == _lib.DR_ERR_INVALID
