@@ -1,7 +1,13 @@
 #!/bin/bash
-# PMC passes over scripts/micro/gemm_x6_bench.py (one counter group per run).
+# PMC passes over scripts/micro/gemm_x6_bench.py (one counter group per run);
+# with FL=1 over scripts/micro/fl_bench.py instead (the fused input-gradient
+# GEMM + first-layer backward, round 5), into gpurun_out/pmc_fl.
 cd "$(dirname "$0")/../.."
-OUT=$PWD/gpurun_out/pmc_gx6
+if [ "${FL:-0}" = 1 ]; then
+  OUT=$PWD/gpurun_out/pmc_fl; PROG="$PWD/scripts/micro/fl_bench.py"; export REPS=10
+else
+  OUT=$PWD/gpurun_out/pmc_gx6; PROG="$PWD/scripts/micro/gemm_x6_bench.py --reps 10"
+fi
 mkdir -p "$OUT"
 export TMPDIR=/tmp
 i=0
@@ -10,7 +16,7 @@ for grp in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY 
            "FETCH_SIZE" "WRITE_SIZE"; do
   i=$((i+1))
   timeout -s KILL 90 rocprofv3 --pmc $grp --output-format csv -d "$OUT/p$i" -o run \
-      -- python3 "$PWD/scripts/micro/gemm_x6_bench.py" --reps 10 "$@" > "$OUT/p$i.log" 2>&1
+      -- python3 $PROG "$@" > "$OUT/p$i.log" 2>&1
   rc=$?; echo "pass $i rc=$rc"
   if [ $rc -ne 0 ]; then tail -5 "$OUT/p$i.log"; exit $rc; fi
 done
@@ -22,12 +28,15 @@ res = {"workload": "scripts/micro/gemm_x6_bench.py --reps 10 (both nets, 65,536 
                    "inputs), rocprofv3 --pmc, two passes (scripts/micro/gemm_x6_pmc.sh); "
                    "per-dispatch averages per kernel"}
 for key, pat in (("gemm_x6_ws_kernel", r"gemm_x6_ws_kernel"),
-                 ("gemm_x6_wgrad_kernel", r"gemm_x6_wgrad_kernel")):
+                 ("gemm_x6_wgrad_kernel", r"gemm_x6_wgrad_kernel"),
+                 ("gemm_x6_fl_kernel", r"gemm_x6_fl_kernel")):
     acc = collections.defaultdict(list)
     for f in glob.glob(out + "/p*/run_counter_collection.csv"):
         for r in csv.DictReader(open(f)):
             if re.search(pat, r["Kernel_Name"]):
                 acc[r["Counter_Name"]].append(float(r["Counter_Value"]))
+    if not acc:
+        continue
     m = {k: sum(v) / len(v) for k, v in acc.items()}
     d = {"counters_per_dispatch": {k: round(v, 1) for k, v in sorted(m.items())},
          "dispatches": max((len(v) for v in acc.values()), default=0)}
