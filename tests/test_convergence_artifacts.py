@@ -52,7 +52,9 @@ def _anchor_at(a, eps):
 # configs[2] GPU runs at a fixed curriculum level (every env starts at eps;
 # the per-env 2000-episode bump never fires in these runs), scripts/c3_matched.sh
 C3_AT_EPS = {0.0: ["r01_ppo_c3_converge.jsonl", "r02_ppo_c3_eps0_x6_s0.jsonl",
-                   "r02_ppo_c3_eps0_x6_s1.jsonl", "r02_ppo_c3_eps0_x6_s2.jsonl"],
+                   "r02_ppo_c3_eps0_x6_s1.jsonl", "r02_ppo_c3_eps0_x6_s2.jsonl",
+                   # round 5's kernels (fused first-layer backward, direct finishes)
+                   "r05_ppo_c3_eps0_s0.jsonl"],
              0.5: ["r02_ppo_c3_eps0.5_s0.jsonl", "r02_ppo_c3_eps0.5_s1.jsonl",
                    "r02_ppo_c3_eps0.5_s2.jsonl"],
              1.0: ["r02_ppo_c3_eps1.0_s0.jsonl", "r02_ppo_c3_eps1.0_s1.jsonl",
