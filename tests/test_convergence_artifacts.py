@@ -104,7 +104,9 @@ def test_anchor_and_fixed_eps_runs_crash_early_no_learning_claim():
 # configs[2] with the staged curriculum (eps 0 -> 1.0 by +0.05 every 20
 # updates from update 300) and ent_coef 0.01, three seeds
 STAGED = ["r03_ppo_c3_staged_ent01_s0", "r03_ppo_c3_staged_ent01_s1",
-          "r03_ppo_c3_staged_ent01_s2"]
+          "r03_ppo_c3_staged_ent01_s2",
+          # round 5's kernels (fused first-layer backward, direct finishes)
+          "r05_ppo_c3_staged_ent01_s0", "r05_ppo_c3_staged_ent01_s1"]
 
 
 def _eval(name):
