@@ -302,6 +302,11 @@ class FusedTrainStep:
         self._ws = torch.empty(self.C * wmax * max(dims), **f32)
         self.tanh_ws = torch.empty(
             max(K.tanh_backward_workspace_bytes(m, n) for n in policy.net_arch) // 4 + 1, **f32)
+        # the fused input-gradient + first-layer kernel right after the head,
+        # ahead of the weight gradient: it reads grad_z2 and h1 first, while
+        # grad_z2 is fresh in the Infinity Cache (7.32 vs 7.27 updates/s
+        # in-process, one box; DRONERL_FL_FIRST=0 for the other order)
+        self.fl_first = os.environ.get("DRONERL_FL_FIRST", "1") != "0"
         # optional instrumentation: mark(name) is called on the host right
         # after each kernel of the fused step is enqueued (bench.py records a
         # HIP event there to time every kernel on the stream)
@@ -428,9 +433,33 @@ class FusedTrainStep:
             for j, pre in enumerate(("pi", "vf")):
                 self._wgrad(gz[j], obs, self.gview(f"{pre}0.w"))
             return self.grad, stats
+        def fused_first(x):
+            # grad_h1 never stored: the first layer's backward in the GEMM's
+            # epilogue, its partials left in the first-layer workspace for the
+            # deferred finish (dr_gemm_x6_bwd_first)
+            from . import _lib
+            xw = x6_weights(pol, M)
+            st = torch.cuda.current_stream(pol.device).cuda_stream
+            if not fused_img:
+                _lib.check(_lib.lib().dr_gemm_x6_split_x(M, 15, obs.data_ptr(),
+                                                         self._ximg.data_ptr(), st))
+                mark("split_x")
+            direct = int(pol.gemm_x6_fl_direct)
+            _lib.check(_lib.lib().dr_gemm_x6_bwd_first(
+                2, M, 15, gz.data_ptr(), xw.bwd.data_ptr(), x.data_ptr(),
+                self._ximg.data_ptr(), self._first.ws.data_ptr(), self._first.ws.numel(),
+                direct, st))
+            if direct:
+                self._first_rows = _lib.lib().dr_gemm_x6_bwd_first_rows(M)
+            mark("gemm_x6_bwd_first")
+
         for k in reversed(range(1, depth)):
             x = self._acts2[k - 1]
             n_in = x.shape[2]
+            # fl_first: the fused kernel ahead of the weight gradient
+            # (independent outputs: the same bytes either way)
+            if k == 1 and fl and self.fl_first:
+                fused_first(x)
             self._wgrad2(gz, x, pol.p2(k, "w", self.grad), defer=defer_finish)
             mark("gemm_x6_wgrad")
             if k == 1 and on_ready is not None:
@@ -439,23 +468,8 @@ class FusedTrainStep:
             g = self._g2.view(-1)[:2 * M * n_in].view(2, M, n_in)
             xw = x6_weights(pol, M) if k == 1 else None
             if k == 1 and fl:
-                # grad_h1 never stored: the first layer's backward in the
-                # GEMM's epilogue, its partials left in the first-layer
-                # workspace for the deferred finish (dr_gemm_x6_bwd_first)
-                from . import _lib
-                st = torch.cuda.current_stream(pol.device).cuda_stream
-                if not fused_img:
-                    _lib.check(_lib.lib().dr_gemm_x6_split_x(M, 15, obs.data_ptr(),
-                                                             self._ximg.data_ptr(), st))
-                    mark("split_x")
-                direct = int(pol.gemm_x6_fl_direct)
-                _lib.check(_lib.lib().dr_gemm_x6_bwd_first(
-                    2, M, 15, gz.data_ptr(), xw.bwd.data_ptr(), x.data_ptr(),
-                    self._ximg.data_ptr(), self._first.ws.data_ptr(), self._first.ws.numel(),
-                    direct, st))
-                if direct:
-                    self._first_rows = _lib.lib().dr_gemm_x6_bwd_first_rows(M)
-                mark("gemm_x6_bwd_first")
+                if not self.fl_first:
+                    fused_first(x)
                 continue
             if xw is not None:
                 gemm_x6(gz, xw.bwd, g)       # images refreshed by hidden_forward
