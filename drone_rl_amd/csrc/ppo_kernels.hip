@@ -21,6 +21,18 @@
 
 #pragma clang fp contract(off)
 
+// DR_LOSS_RCP 1 (default since round 5): the Gaussian log-prob's and the PPO
+// row's divisions by var, 2 var and the advantage std are products with
+// reciprocals formed once per thread (an IEEE f32 division is ~10 VALU, and
+// the policy rows run on 4 lanes of 64 in the head kernel: the issue cost is
+// the whole wave's; its loss block 244 -> 120 VALU per 4-row tile); each term
+// within an ulp or so of the quotient.  7.19-7.21 vs 7.14-7.15 PPO updates/s,
+// three alternating pairs on one box (profiles/r05_loss_rcp_ab.json).  0: the
+// quotients (round 1-4 bits).
+#ifndef DR_LOSS_RCP
+#define DR_LOSS_RCP 1
+#endif
+
 namespace dr {
 namespace {
 
@@ -106,7 +118,11 @@ __global__ __launch_bounds__(kBlock) void policy_sample_kernel(
         a[j] = m[j] + sd * z[j];
         const float d = a[j] - m[j];
         const float var = sd * sd;
+#if DR_LOSS_RCP  // the same reciprocal as RowLossConst::inv_2var (the first epoch's ratio stays 1)
+        lp += (-(d * d) * (1.0f / (2.0f * var)) - logf(sd)) - kLogSqrt2Pi;
+#else
         lp += (-(d * d) / (2.0f * var) - logf(sd)) - kLogSqrt2Pi;
+#endif
     }
     if (a_raw) a_raw[i] = make_float4(a[0], a[1], a[2], a[3]);
     if (a_clip)
@@ -624,7 +640,8 @@ constexpr int kLossK = 9;  // pl, vl, clipcnt, kl, g_ls[4], (spare)
 // fused head kernel so both compute bit-identical rows.
 struct RowLossConst {
     float var[4], logsd[4];
-    float lo, hi, clip, inv_m, vf_coef, amean, astd;
+    float inv_var[4], inv_2var[4];
+    float lo, hi, clip, inv_m, vf_coef, amean, astd, inv_astd;
     int normalize;
 };
 
@@ -637,6 +654,8 @@ __device__ inline RowLossConst row_loss_const(const float *log_std, float clip, 
         const float sd = expf(log_std[j]);
         c.var[j] = sd * sd;
         c.logsd[j] = logf(sd);
+        c.inv_var[j] = 1.0f / c.var[j];
+        c.inv_2var[j] = 1.0f / (2.0f * c.var[j]);
     }
     c.lo = 1.0f - clip;
     c.hi = 1.0f + clip;
@@ -645,6 +664,7 @@ __device__ inline RowLossConst row_loss_const(const float *log_std, float clip, 
     c.vf_coef = vf_coef;
     c.amean = amean;
     c.astd = astd;
+    c.inv_astd = 1.0f / (astd + 1e-8f);
     c.normalize = normalize;
     return c;
 }
@@ -661,10 +681,19 @@ __device__ inline void ppo_row(const RowLossConst &c, const float mu[4], const f
     for (int j = 0; j < 4; ++j) {
         const float d = ac[j] - mu[j];
         dd[j] = d;
+#if DR_LOSS_RCP
+        zz[j] = d * c.inv_var[j];         // d logp / d mu_j
+        lp += (-(d * d) * c.inv_2var[j] - c.logsd[j]) - kLogSqrt2Pi;
+#else
         zz[j] = d / c.var[j];             // d logp / d mu_j
         lp += (-(d * d) / (2.0f * c.var[j]) - c.logsd[j]) - kLogSqrt2Pi;
+#endif
     }
+#if DR_LOSS_RCP
+    if (c.normalize) A = (A - c.amean) * c.inv_astd;
+#else
     if (c.normalize) A = (A - c.amean) / (c.astd + 1e-8f);
+#endif
     const float logr = lp - old_lp;
     const float r = expf(logr);
     const float rc = fminf(fmaxf(r, c.lo), c.hi);
@@ -683,7 +712,11 @@ __device__ inline void ppo_row(const RowLossConst &c, const float mu[4], const f
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
         gm[j] = dlp * zz[j];
+#if DR_LOSS_RCP
+        acc[4 + j] += dlp * ((dd[j] * dd[j]) * c.inv_var[j] - 1.0f);  // d/dlog_std_j
+#else
         acc[4 + j] += dlp * ((dd[j] * dd[j]) / c.var[j] - 1.0f);  // d/dlog_std_j
+#endif
     }
 }
 
@@ -698,10 +731,19 @@ __device__ inline void ppo_row_policy(const RowLossConst &c, const float mu[4],
     for (int j = 0; j < 4; ++j) {
         const float d = ac[j] - mu[j];
         dd[j] = d;
+#if DR_LOSS_RCP
+        zz[j] = d * c.inv_var[j];
+        lp += (-(d * d) * c.inv_2var[j] - c.logsd[j]) - kLogSqrt2Pi;
+#else
         zz[j] = d / c.var[j];
         lp += (-(d * d) / (2.0f * c.var[j]) - c.logsd[j]) - kLogSqrt2Pi;
+#endif
     }
+#if DR_LOSS_RCP
+    if (c.normalize) A = (A - c.amean) * c.inv_astd;
+#else
     if (c.normalize) A = (A - c.amean) / (c.astd + 1e-8f);
+#endif
     const float logr = lp - old_lp;
     const float r = expf(logr);
     const float rc = fminf(fmaxf(r, c.lo), c.hi);
@@ -717,7 +759,11 @@ __device__ inline void ppo_row_policy(const RowLossConst &c, const float mu[4],
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
         gm[j] = dlp * zz[j];
+#if DR_LOSS_RCP
+        acc[4 + j] += dlp * ((dd[j] * dd[j]) * c.inv_var[j] - 1.0f);
+#else
         acc[4 + j] += dlp * ((dd[j] * dd[j]) / c.var[j] - 1.0f);
+#endif
     }
 }
 

@@ -1,9 +1,12 @@
 #!/bin/bash
 # PMC passes over scripts/micro/gemm_x6_bench.py (one counter group per run);
 # with FL=1 over scripts/micro/fl_bench.py instead (the fused input-gradient
-# GEMM + first-layer backward, round 5), into gpurun_out/pmc_fl.
+# GEMM + first-layer backward, round 5), into gpurun_out/pmc_fl; with HEAD=1
+# over scripts/micro/head_bench.py (ppo_head_kernel), into gpurun_out/pmc_head.
 cd "$(dirname "$0")/../.."
-if [ "${FL:-0}" = 1 ]; then
+if [ "${HEAD:-0}" = 1 ]; then
+  OUT=$PWD/gpurun_out/pmc_head; PROG="$PWD/scripts/micro/head_bench.py"; export REPS=10
+elif [ "${FL:-0}" = 1 ]; then
   OUT=$PWD/gpurun_out/pmc_fl; PROG="$PWD/scripts/micro/fl_bench.py"; export REPS=10
 else
   OUT=$PWD/gpurun_out/pmc_gx6; PROG="$PWD/scripts/micro/gemm_x6_bench.py --reps 10"
@@ -29,7 +32,8 @@ res = {"workload": "scripts/micro/gemm_x6_bench.py --reps 10 (both nets, 65,536 
                    "per-dispatch averages per kernel"}
 for key, pat in (("gemm_x6_ws_kernel", r"gemm_x6_ws_kernel"),
                  ("gemm_x6_wgrad_kernel", r"gemm_x6_wgrad_kernel"),
-                 ("gemm_x6_fl_kernel", r"gemm_x6_fl_kernel")):
+                 ("gemm_x6_fl_kernel", r"gemm_x6_fl_kernel"),
+                 ("ppo_head_kernel", r"ppo_head_kernel")):
     acc = collections.defaultdict(list)
     for f in glob.glob(out + "/p*/run_counter_collection.csv"):
         for r in csv.DictReader(open(f)):
@@ -54,6 +58,12 @@ for key, pat in (("gemm_x6_ws_kernel", r"gemm_x6_ws_kernel"),
     if "FETCH_SIZE" in m and "WRITE_SIZE" in m:
         # KiB; FETCH_SIZE x 2 on gfx950 (MI355X_MICROARCH.md, HBM / rocprofv3)
         d["hbm_bytes_per_dispatch"] = round(m["FETCH_SIZE"] * 2048 + m["WRITE_SIZE"] * 1024)
+    if "SQ_ACTIVE_INST_VALU" in m and "GRBM_GUI_ACTIVE" in m:
+        # VALU issue cycles summed over the 1,024 SIMDs, against the busy clock
+        d["active_inst_valu_per_simd_over_gui_active"] = round(
+            m["SQ_ACTIVE_INST_VALU"] / 1024.0 / (m["GRBM_GUI_ACTIVE"] / 8.0), 3)
+        if w:
+            d["valu_active_frac_of_wave_cycles"] = round(m["SQ_ACTIVE_INST_VALU"] / w, 3)
     if "SQ_LDS_BANK_CONFLICT" in m:
         d["lds_bank_conflict_cycles"] = m["SQ_LDS_BANK_CONFLICT"]
     res[key] = d
