@@ -54,7 +54,7 @@ def _anchor_at(a, eps):
 C3_AT_EPS = {0.0: ["r01_ppo_c3_converge.jsonl", "r02_ppo_c3_eps0_x6_s0.jsonl",
                    "r02_ppo_c3_eps0_x6_s1.jsonl", "r02_ppo_c3_eps0_x6_s2.jsonl",
                    # round 5's kernels (fused first-layer backward, direct finishes)
-                   "r05_ppo_c3_eps0_s0.jsonl"],
+                   "r05_ppo_c3_eps0_s0.jsonl", "r05_ppo_c3_eps0_s0_final.jsonl"],
              0.5: ["r02_ppo_c3_eps0.5_s0.jsonl", "r02_ppo_c3_eps0.5_s1.jsonl",
                    "r02_ppo_c3_eps0.5_s2.jsonl"],
              1.0: ["r02_ppo_c3_eps1.0_s0.jsonl", "r02_ppo_c3_eps1.0_s1.jsonl",
