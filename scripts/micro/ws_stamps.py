@@ -49,3 +49,14 @@ for k, v in d.items():
           f"   per step k (wave-median): {[int(x) for x in np.median(v.reshape(32, R), 0)]}")
 print(f"row step (loop top -> next loop top) median {np.median(step):.0f}; MFMA-only 192 x 32 = 6144")
 print(f"whole wave (kernel start -> last barrier) median {np.median(tot):.0f}")
+# with the realtime stamps (23, 2) / (23, 3) (s_memrealtime, 100 MHz) and
+# (23, 4) (s_memtime after the last row step): the shader clock and the
+# waves' start / end spread in microseconds
+rt0, rt1 = st[:, :, 23, 2], st[:, :, 23, 3]
+if rt0.min() > 0 and rt1.min() > 0:
+    loop = st[:, :, 23, 4] - st[:, :, 23, 0]
+    us = (rt1 - rt0) / 100.0
+    print(f"wave lifetime {np.median(us):.2f} us median (s_memrealtime); shader clock "
+          f"{np.median(loop / us) / 1e3:.3f} GHz; prologue {np.median(pro) / np.median(loop / us):.2f} us")
+    print(f"wave starts spread {(rt0.max() - rt0.min()) / 100.0:.2f} us, ends spread "
+          f"{(rt1.max() - rt1.min()) / 100.0:.2f} us (blocks 0-7)")
