@@ -57,6 +57,9 @@ HBM_PEAK_GBS = 8000.0      # MI355X HBM3E spec (MI355X_MICROARCH.md)
 # tree's (committed_profile): reported in the line's committed_artefacts
 # block, labelled stale, never inside a live block
 ARTEFACTS = {}
+# the headline's node timing at world > 1 (node_timing's rank figures),
+# reported in the line beside the value
+HEADLINE_NODE = {}
 
 
 def _atoi(v):
@@ -195,18 +198,45 @@ def parse():
     return ap.parse_args()
 
 
-def timed_region(work, sync, world, clock=time.monotonic_ns):
+# Start alignment at world > 1: after the barrier and the device
+# synchronize, the ranks agree on a common CLOCK_MONOTONIC deadline (the
+# latest rank's ready time + this margin, one all_reduce MAX, still before
+# t0) and spin until it, so that the barrier's release skew between the
+# ranks' host threads does not enter the node wall max(t1) - min(t0).
+START_MARGIN_NS = int(os.environ.get("DRONERL_START_MARGIN_NS", "2000000"))
+
+
+def start_deadline(ready_ns, world, device=None, margin_ns=START_MARGIN_NS):
+    """The common start time: max over ranks of ready_ns, plus margin_ns
+    (one all_reduce MAX of an int64, on the device under RCCL)."""
+    if world == 1:
+        return ready_ns
+    import torch
+    import torch.distributed as dist
+    dev = device if (device is not None and dist.get_backend() == "nccl") else "cpu"
+    t = torch.tensor([ready_ns], dtype=torch.int64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return int(t.item()) + margin_ns
+
+
+def timed_region(work, sync, world, clock=time.monotonic_ns, device=None, align=True):
     """The timing rule of every bench leg: a barrier
-    and a device synchronize come BEFORE t0; then the work and a device
-    synchronize; then t1.  No torch.distributed call runs between t0 and t1
-    (at --steps 20 the timed region is one ~29 us launch, which an RCCL
-    barrier across 8 GPUs would rival).  Returns (t0, t1) in ns of
-    CLOCK_MONOTONIC, the clock every process of one node shares, so the
-    ranks' spans can be compared after the timer (node_timing)."""
+    and a device synchronize come BEFORE t0; at world > 1 the ranks then
+    agree on a common start deadline and spin until it (start_deadline,
+    also before t0); then t0, the work, a device synchronize and t1.  No
+    torch.distributed call runs between t0 and t1 (at --steps 20 the timed
+    region is one ~38 us launch, which an RCCL barrier across 8 GPUs would
+    rival).  Returns (t0, t1) in ns of CLOCK_MONOTONIC, the clock every
+    process of one node shares, so the ranks' spans can be compared after
+    the timer (node_timing)."""
     if world > 1:
         import torch.distributed as dist
         dist.barrier()
     sync()
+    if world > 1 and align:
+        deadline = start_deadline(clock(), world, device)
+        while clock() < deadline:
+            pass
     t0 = clock()
     work()
     sync()
@@ -244,6 +274,7 @@ def node_timing(spans):
     return {"wall_s": (t1 - t0) / 1e9,
             "max_rank_s": max(s[1] - s[0] for s in spans) / 1e9,
             "gpu_ms": max(s[2] for s in spans) / 1e6,
+            "start_skew_us": (max(s[0] for s in spans) - t0) / 1e3,
             "ranks": len(spans)}
 
 
@@ -336,7 +367,7 @@ def time_env(args, dtype_name, n_envs, rank, world, device, steps, warmup, varia
             for t in range(warmup, total):
                 b.step(acts[t])
         ev1.record(stream)
-    span = timed_region(work, torch.cuda.synchronize, world)
+    span = timed_region(work, torch.cuda.synchronize, world, device=device)
     tm = node_timing(gather_spans((*span, round(ev0.elapsed_time(ev1) * 1e6)), world, device))
     elapsed, gpu_ms = tm["wall_s"], tm["gpu_ms"]
     # sanity: the env is alive (episodes end and reset under a random policy)
@@ -454,15 +485,21 @@ def time_headline(args, n_envs, rank, world, device, steps, warmup, kmax):
         # have a 37-39 us median (scripts/micro/host_wait.py); with this
         # rehearsal and the no-argument torch.cuda.synchronize (no device-
         # guard switch around it) it reads 38.1-39.2 us (3 runs, one box)
-        timed_region(work, torch.cuda.synchronize, world)
+        timed_region(work, torch.cuda.synchronize, world, device=device)
     gc.disable()
-    span = timed_region(work, torch.cuda.synchronize, world)
+    span = timed_region(work, torch.cuda.synchronize, world, device=device)
     gc.enable()
     if g is None and any(rcs):
         from drone_rl_amd._lib import check
         check(next(r for r in rcs if r), b.handle)
     tm = node_timing(gather_spans((*span, round(ev0.elapsed_time(ev1) * 1e6)), world, device))
     elapsed, gpu_ms = tm["wall_s"], tm["gpu_ms"]
+    if world > 1:
+        HEADLINE_NODE.update({"wall_us": round(tm["wall_s"] * 1e6, 2),
+                              "slowest_rank_span_us": round(tm["max_rank_s"] * 1e6, 2),
+                              "start_skew_us": round(tm["start_skew_us"], 2),
+                              "start_alignment": "common CLOCK_MONOTONIC deadline agreed "
+                                                 "before t0 (bench.start_deadline)"})
     ep =b.get("ep_num").float().mean().item()
     b.close()
     graphed = g is not None
@@ -827,7 +864,7 @@ def time_ppo(args, rank, world, device, force_dp=False, dp_graph=False, profile=
     def work():
         for _ in range(K):
             last[:] = [tr.learn_step()]
-    span = timed_region(work, torch.cuda.synchronize, world)
+    span = timed_region(work, torch.cuda.synchronize, world, device=device)
     el = node_timing(gather_spans((*span, 0), world, device))["wall_s"]
     st = last[0]
     es =tr.episode_stats()
@@ -1107,6 +1144,8 @@ def main():
         "single_step": single,
         "mean_ep_num": round(ep, 2),
     }
+    if HEADLINE_NODE:
+        out["node_timing"] = dict(HEADLINE_NODE)
     if world == 1 and not args.no_companion:
         # cache-busting companion of the headline: the same
         # kernel at 4,194,304 envs, where the step is HBM-bound, not launch-

@@ -24,12 +24,17 @@ def test_node_timing_is_max_end_minus_min_start():
     assert t["max_rank_s"] == 7_000 / 1e9
     assert t["gpu_ms"] == 7.0
     assert t["ranks"] == 3
+    assert t["start_skew_us"] == (2_000 - 1_000) / 1e3
     one = bench.node_timing([(10, 20, 1_000_000)])
     assert one["wall_s"] == one["max_rank_s"] == 10 / 1e9 and one["gpu_ms"] == 1.0
     with pytest.raises(ValueError):
         bench.node_timing([])
     with pytest.raises(ValueError):
         bench.node_timing([(5, 4, 0)])
+
+
+def test_start_deadline_world1_is_the_ready_time():
+    assert bench.start_deadline(12345, 1) == 12345
 
 
 def test_timed_region_single_rank_orders_sync_and_clock():
@@ -99,3 +104,7 @@ def test_no_collective_inside_the_timed_region_gloo_world2():
         assert tm["wall_s"] == (max(s[1] for s in spans) - min(s[0] for s in spans)) / 1e9
         assert tm["gpu_ms"] == 2.0
         assert tm["wall_s"] >= tm["max_rank_s"] >= 0.08
+        # the start deadline (one all_reduce MAX before t0) lines the ranks'
+        # t0 up: the skew is scheduling jitter, far below the barrier's
+        assert any(n == "all_reduce" and b <= t0 for n, a, b in calls)
+        assert 0 <= tm["start_skew_us"] < 5_000, tm
