@@ -23,7 +23,12 @@ The JSON line also carries
   roofline      the headline kernel: algorithmic bytes per launch (per env-
                 step 81 B of actions / obs / reward / done, plus the f64 state
                 read and written once per launch: 224 B / K)
-                over its average per-launch GPU time from HIP events on the
+                over its per-launch GPU time: for a direct launch (the
+                driver's --steps 20) the dispatch-packet timestamps of the
+                same launches repeated right before the timed region (the
+                value's region holds the launches alone; an instrumented
+                region with a HIP event pair around them is timed first and
+                reported beside it), for a graph replay HIP events on the
                 launch stream across the timed region;
   single_step   the same envs through one dr_step launch per step (305 B per
                 env-step in f64), with its own roofline block;
@@ -60,6 +65,8 @@ ARTEFACTS = {}
 # the headline's node timing at world > 1 (node_timing's rank figures),
 # reported in the line beside the value
 HEADLINE_NODE = {}
+# the headline's walls with and without the HIP event pair (direct launches)
+HEADLINE_WALLS = {}
 
 
 def _atoi(v):
@@ -206,6 +213,16 @@ def parse():
 START_MARGIN_NS = int(os.environ.get("DRONERL_START_MARGIN_NS", "2000000"))
 
 
+def single_node(world):
+    """Whether all `world` ranks share this node's CLOCK_MONOTONIC: torchrun's
+    LOCAL_WORLD_SIZE equals WORLD_SIZE (spawn_ranks sets both; absent = one
+    process).  Across nodes the monotonic clocks are unrelated, so the start
+    alignment and the node wall max(t1) - min(t0) apply on one node only
+    (advisor r05)."""
+    lw = os.environ.get("LOCAL_WORLD_SIZE")
+    return world <= 1 or lw is None or _atoi(lw) == world
+
+
 def start_deadline(ready_ns, world, device=None, margin_ns=START_MARGIN_NS):
     """The common start time: max over ranks of ready_ns, plus margin_ns
     (one all_reduce MAX of an int64, on the device under RCCL)."""
@@ -233,10 +250,12 @@ def timed_region(work, sync, world, clock=time.monotonic_ns, device=None, align=
         import torch.distributed as dist
         dist.barrier()
     sync()
-    if world > 1 and align:
+    if world > 1 and align and single_node(world):
         deadline = start_deadline(clock(), world, device)
-        while clock() < deadline:
-            pass
+        # bounded: a deadline far ahead means the clocks are not shared
+        if deadline - clock() <= 100 * START_MARGIN_NS:
+            while clock() < deadline:
+                pass
     t0 = clock()
     work()
     sync()
@@ -271,6 +290,12 @@ def node_timing(spans):
     t1 = max(s[1] for s in spans)
     if any(s[1] < s[0] for s in spans):
         raise ValueError("a span ends before it starts")
+    if not single_node(len(spans)):
+        # ranks on several nodes: no shared clock, the slowest rank's span
+        slow = max(s[1] - s[0] for s in spans) / 1e9
+        return {"wall_s": slow, "max_rank_s": slow,
+                "gpu_ms": max(s[2] for s in spans) / 1e6, "start_skew_us": None,
+                "ranks": len(spans), "clock": "per-rank spans (multi-node)"}
     return {"wall_s": (t1 - t0) / 1e9,
             "max_rank_s": max(s[1] - s[0] for s in spans) / 1e9,
             "gpu_ms": max(s[2] for s in spans) / 1e6,
@@ -473,7 +498,7 @@ def time_headline(args, n_envs, rank, world, device, steps, warmup, kmax):
             if rep > 0:
                 reps.append(pk0.elapsed_time(pk1))
         packet_ms = sorted(reps)[len(reps) // 2]
-    def work():
+    def work_events():
         ev0.record(stream)
         timed()
         ev1.record(stream)
@@ -485,19 +510,39 @@ def time_headline(args, n_envs, rank, world, device, steps, warmup, kmax):
         # have a 37-39 us median (scripts/micro/host_wait.py); with this
         # rehearsal and the no-argument torch.cuda.synchronize (no device-
         # guard switch around it) it reads 38.1-39.2 us (3 runs, one box)
-        timed_region(work, torch.cuda.synchronize, world, device=device)
+        timed_region(work_events, torch.cuda.synchronize, world, device=device)
     gc.disable()
-    span = timed_region(work, torch.cuda.synchronize, world, device=device)
+    span_ev = timed_region(work_events, torch.cuda.synchronize, world, device=device)
     gc.enable()
+    tm_ev = node_timing(gather_spans((*span_ev, round(ev0.elapsed_time(ev1) * 1e6)), world,
+                                     device))
+    HEADLINE_WALLS.clear()
+    if g is None:
+        # The value's own region (round 6, verdict r05 item 7): the launches
+        # alone between t0 and t1 -- the HIP event pair above cost ~3 us of
+        # queue time inside its region (profiles/r05_host_events.json).  The
+        # GPU time of these launches is the packet-timestamped repetitions'
+        # median measured right before (the same launches and arguments);
+        # the instrumented region's wall and event time are reported beside.
+        timed_region(timed, torch.cuda.synchronize, world, device=device)   # rehearsal
+        gc.disable()
+        span = timed_region(timed, torch.cuda.synchronize, world, device=device)
+        gc.enable()
+        tm = node_timing(gather_spans((*span, round(packet_ms * 1e6)), world, device))
+        HEADLINE_WALLS.update({"wall_us": round(tm["wall_s"] * 1e6, 2),
+                               "wall_us_with_event_pair": round(tm_ev["wall_s"] * 1e6, 2),
+                               "event_pair_gpu_us": round(tm_ev["gpu_ms"] * 1e3, 3)})
+    else:
+        tm = tm_ev
     if g is None and any(rcs):
         from drone_rl_amd._lib import check
         check(next(r for r in rcs if r), b.handle)
-    tm = node_timing(gather_spans((*span, round(ev0.elapsed_time(ev1) * 1e6)), world, device))
     elapsed, gpu_ms = tm["wall_s"], tm["gpu_ms"]
     if world > 1:
         HEADLINE_NODE.update({"wall_us": round(tm["wall_s"] * 1e6, 2),
                               "slowest_rank_span_us": round(tm["max_rank_s"] * 1e6, 2),
-                              "start_skew_us": round(tm["start_skew_us"], 2),
+                              "start_skew_us": (None if tm["start_skew_us"] is None
+                                                else round(tm["start_skew_us"], 2)),
                               "start_alignment": "common CLOCK_MONOTONIC deadline agreed "
                                                  "before t0 (bench.start_deadline)"})
     ep =b.get("ep_num").float().mean().item()
@@ -756,6 +801,16 @@ def rocprof_averages(path):
     return out
 
 
+def dominant_ppo_kernel(kern):
+    """The optimizer step's kernel with the largest time per step (verdict
+    r05 item 4): by rocprof_us when any entry carries it (the committed
+    rocprofv3 summary matches the tree), else by the live prefix split.
+    Only entries with a roofline bound compete."""
+    key = "rocprof_us" if any("rocprof_us" in e for e in kern.values()) else "prefix_split_us"
+    cands = {n: e[key] for n, e in kern.items() if key in e and "bound" in e}
+    return max(cands, key=cands.get) if cands else None
+
+
 def ppo_roofline(cfg, s_per_update, ktimes, rocprof=None, isolated=None, rocprof_source=None):
     """The ppo block's roofline.  Whole update: fp32-equivalent FLOP per
     second, reported against the f32 matrix peak only as
@@ -768,8 +823,8 @@ def ppo_roofline(cfg, s_per_update, ktimes, rocprof=None, isolated=None, rocprof
     DESIGN.md 3) against HBM (`prefix_split_frac`); the GEMMs also timed
     alone (`isolated_us`, live); `rocprof_us` / `rocprof_frac` from a
     committed rocprofv3 summary that matches the current kernel sources
-    (`rocprof_source`).  The dominant kernel (the forward x6 GEMM) takes its
-    fraction from its live isolated launches."""
+    (`rocprof_source`).  The dominant kernel is the one with the largest time
+    per optimizer step (dominant_ppo_kernel)."""
     M, NT, E = cfg.batch_size, cfg.num_envs * cfg.n_steps, cfg.n_epochs
     flop_update = NT * PPO_FWD_FLOP * (1 + 3 * E)
     gemm_flop = 2 * 2 * M * 256 * 256            # both nets, one fp32 GEMM
@@ -826,17 +881,30 @@ def ppo_roofline(cfg, s_per_update, ktimes, rocprof=None, isolated=None, rocprof
                     "fractions are in kernels_per_minibatch and dominant_kernel)",
            "rocprof_source": rocprof_source,
            "kernels_per_minibatch": kern}
-    if "gemm_x6_fwd" in isolated:
-        us = isolated["gemm_x6_fwd"]
-        d = {"kernel": "gemm_x6_ws_kernel (forward, both nets, 65,536 rows)", "bound": "mfma",
-             "achieved": round(6 * gemm_flop / (us * 1e-6) / 1e12, 1),
-             "peak": BF16_DENSE_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": mfma_frac(us),
-             "us": round(us, 2),
-             "timing": "live: 20 back-to-back launches on the trainer's buffers in one "
-                       "hipGraph, HIP events"}
-        rp = rocprof.get("gemm_x6_ws_kernel")
-        if rp is not None:
-            d.update({"rocprof_us": round(rp, 2), "rocprof_frac": mfma_frac(rp)})
+    dom = dominant_ppo_kernel(kern)
+    if dom is not None:
+        e = kern[dom]
+        basis = next(k for k in ("rocprof_us", "isolated_us", "prefix_split_us") if k in e)
+        us = e[basis]
+        if e["bound"] == "mfma":
+            flop = 6 * (fl_flop if dom == "gemm_x6_bwd_first" else gemm_flop)
+            ach, peak, unit = flop / (us * 1e-6) / 1e12, BF16_DENSE_PEAK_TFLOPS, "TFLOP/s"
+        else:
+            ach, peak, unit = rows[dom] * M / (us * 1e-6) / 1e9, HBM_PEAK_GBS, "GB/s"
+        d = {"step": dom, "kernel": PPO_KERNEL_NAMES.get(dom, dom), "bound": e["bound"],
+             "achieved": round(ach, 1), "peak": peak, "unit": unit,
+             "frac": round(ach / peak, 4), "us": round(us, 2),
+             "timing": {"rocprof_us": "the kernel's own rocprofv3 average in whole training "
+                                      "steps (" + str(rocprof_source) + ")",
+                        "isolated_us": "live: 20 back-to-back launches on the trainer's "
+                                       "buffers in one hipGraph, HIP events",
+                        "prefix_split_us": "live prefix split (kernel_timing)"}[basis],
+             "selection": "the step's kernel with the largest time per optimizer step "
+                          "(rocprof_us when the committed summary matches the tree, else "
+                          "prefix_split_us)"}
+        for k in ("isolated_us", "isolated_frac", "rocprof_us", "rocprof_frac"):
+            if k in e and k != basis:
+                d[k] = e[k]
         out["dominant_kernel"] = d
     return out
 
@@ -1080,6 +1148,11 @@ def main():
                                "launch and env the f64 state read (124 B) and written (100 B) "
                                "once",
                 "avg_launch_us": round(per_launch_s * 1e6, 3),
+                "avg_launch_us_source": ("dispatch-packet timestamps (median of 5 "
+                                         "repetitions of the timed launches, right before "
+                                         "the timed region)" if packet_ms and not graphed
+                                         else "HIP events on the launch stream across the "
+                                              "timed region"),
                 # the same algorithmic bytes over the timed region's host wall
                 # (launch + synchronize included; the value's own clock)
                 "frac_wall": round(N * K * bpe / elapsed / 1e9 / HBM_PEAK_GBS, 4),
@@ -1095,6 +1168,15 @@ def main():
                 # event records' queue time
                 "avg_launch_us_packet": (round(packet_ms / launches * 1e3, 3)
                                          if packet_ms else None),
+                # the instrumented region (HIP event pair around the launches):
+                # its wall and the events' GPU time
+                **({"walls": dict(HEADLINE_WALLS,
+                                  frac_wall_with_event_pair=round(
+                                      N * K * bpe / (HEADLINE_WALLS["wall_us_with_event_pair"]
+                                                     * 1e-6) / 1e9 / HBM_PEAK_GBS, 4),
+                                  avg_launch_us_events=round(
+                                      HEADLINE_WALLS["event_pair_gpu_us"] / launches, 3))}
+                   if HEADLINE_WALLS else {}),
                 "limiter": "the f64 step, split by data over two waves per SIMD "
                            "(translation / rotation; memory waves stream the outputs beside "
                            "them; with no physics the stream alone takes ~30 us per 32 "

@@ -449,6 +449,246 @@ __global__ __launch_bounds__(WS_THREADS, 1) void gemm_x6_ws_kernel(
 }
 
 // ---------------------------------------------------------------------------
+// gemm_x6_ws16_kernel (round 6, X6_MFMA16): gemm_x6_ws_kernel on
+// v_mfma_f32_16x16x32_bf16.  Under DVFS give-back the 16x16x32 form held a
+// higher clock than 32x32x16 at equal cycles per FLOP (MI355X_MICROARCH.md,
+// DVFS give-back item 7), and its 16-row A fragments let a phase be a ROW
+// tile: phase t runs rows 16 t .. + 15 of the row step against all four of
+// the wave's 16-column tiles, so each activation fragment is read from LDS
+// once per row step (48 ds_read_b128 instead of 96).  Same block shape,
+// staging, split and LDS planes as gemm_x6_ws_kernel; the weights in the
+// X6_MFMA16 image order (wimg_off): wave w's column tile ct, k32 step s.
+// Per SIMD and row step: 384 MFMAs of 16 cycles (the same 6,144 pipe cycles,
+// 3,072 of issue), 48 fragment reads, 32 stores, 8 DMA pieces.
+// Accumulators D[m][n] of a 16 x 16 tile: column n = lane & 15, row
+// m = 4 (lane >> 4) + r, r = 0..3.
+typedef float f32x4_t __attribute__((ext_vector_type(4)));
+
+__device__ inline void mfma16_a(f32x4_t &d, const bf16x8_t &x, const bf16x8_t &w) {
+    asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+v"(d) : "v"(x), "a"(w));
+}
+__device__ inline void mfma16_v(f32x4_t &d, const bf16x8_t &x, const bf16x8_t &w) {
+    asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+v"(d) : "v"(x), "v"(w));
+}
+__device__ inline void mfma16_first(f32x4_t &d, const bf16x8_t &x, const bf16x8_t &w) {
+    asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, 0" : "=&v"(d) : "v"(x), "a"(w));
+}
+
+__global__ __launch_bounds__(WS_THREADS, 1) void gemm_x6_ws16_kernel(
+    const float *__restrict__ A, const uint8_t *__restrict__ img, float *__restrict__ C,
+    int64_t m, int batch) {
+    __shared__ __attribute__((aligned(16))) uint8_t sh[WS_LDS];
+    const int lane = threadIdx.x & 63;
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int b = (int)blockIdx.x % batch;
+    const int per = (int)gridDim.x / batch;
+    const int j0 = (int)blockIdx.x / batch;
+    const int steps_net = (int)(m / WS_RS);
+    const int R = (steps_net - j0 + per - 1) / per;
+    const float *Ab = A + (int64_t)b * m * XK;
+    float *Cb = C + (int64_t)b * m * XN;
+    const int fc = lane & 15, fq = lane >> 4;
+
+    // the weights: wave w's 4 column tiles x 8 k32 steps x 3 planes as B
+    // fragments (lane: column 64 w + 16 ct + fc, k 32 s + 8 fq .. + 7); h, m
+    // planes in AGPRs (read there by the asm MFMAs), l in VGPRs
+    bf16x8_t Wa[4][8][2], Wv[4][8];
+    {
+        const uint8_t *ib = img + (int64_t)b * W_IMG + lane * 16;
+#pragma unroll
+        for (int ct = 0; ct < 4; ++ct)
+#pragma unroll
+            for (int s = 0; s < 8; ++s) {
+                const uint8_t *src = ib + ((w * 4 + ct) * 8 + s) * 3 * W_FRAG;
+                Wa[ct][s][0] = *reinterpret_cast<const bf16x8_t *>(src);
+                Wa[ct][s][1] = *reinterpret_cast<const bf16x8_t *>(src + W_FRAG);
+                Wv[ct][s] = *reinterpret_cast<const bf16x8_t *>(src + 2 * W_FRAG);
+            }
+    }
+
+    // staging and split: gemm_x6_ws_kernel's, unchanged
+    const int sr = lane & 7, sc = (lane >> 3) & 3, shf = lane >> 5;
+    const uint32_t voff_f = (uint32_t)(sr * 1024 + 32 * sc + 16 * (shf ^ (sc & 1)));
+    auto issue_rows = [&](int k) {
+        const float *r0 = Ab + ((int64_t)(j0 + k * per) * WS_RS + 8 * w) * XK;
+        uint8_t *dst = sh + WS_LDS_F + (k & 1) * WS_FSLOT + w * 8 * 1024;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) glds16_s(r0 + 32 * i, voff_f, lds_addr(dst + i * 1024));
+    };
+    const int rd_base = WS_LDS_F + w * 8 * 1024 + (lane >> 5) * 1024 + (lane & 31) * 16;
+    auto split_read = [&](int k, int u, int hf, float4 &v) {
+        v = *reinterpret_cast<const float4 *>(sh + rd_base + (k & 1) * WS_FSLOT + u * 2048 +
+                                              hf * 512);
+    };
+    const int wr_base = (lane >> 3) * 512 + (8 * w + sr) * 16;
+    const int wr_odd = (lane >> 3) & 1;
+    const int wr_half[2] = {wr_base + 8 * wr_odd, wr_base + 8 * (wr_odd ^ 1)};
+    auto split_store = [&](int k, int u, int hf, uint32_t h0, uint32_t h1, uint32_t m0,
+                           uint32_t m1, uint32_t l0, uint32_t l1) {
+        uint8_t *dst = sh + (k & 1) * WS_PSTAGE + wr_half[hf] + u * 8 * 512;
+        typedef uint32_t u32x2_t __attribute__((ext_vector_type(2)));
+        *reinterpret_cast<u32x2_t *>(dst) = (u32x2_t){h0, h1};
+        *reinterpret_cast<u32x2_t *>(dst + WS_PLANE) = (u32x2_t){m0, m1};
+        *reinterpret_cast<u32x2_t *>(dst + 2 * WS_PLANE) = (u32x2_t){l0, l1};
+    };
+    auto split_rw = [&](int k, int u, int hf) {
+        float4 v;
+        split_read(k, u, hf, v);
+        const uint32_t h0 = pk_bf16(v.x, v.y);
+        float ra = v.x - lo_f(h0), rb = v.y - hi_f(h0);
+        const uint32_t m0 = pk_bf16(ra, rb);
+        const uint32_t l0 = pk_bf16(ra - lo_f(m0), rb - hi_f(m0));
+        const uint32_t h1 = pk_bf16(v.z, v.w);
+        ra = v.z - lo_f(h1), rb = v.w - hi_f(h1);
+        const uint32_t m1 = pk_bf16(ra, rb);
+        const uint32_t l1 = pk_bf16(ra - lo_f(m1), rb - hi_f(m1));
+        split_store(k, u, hf, h0, h1, m0, m1, l0, l1);
+    };
+    // activation fragments of global k32 step g of a row step (row tile
+    // g >> 3, k32 step g & 7; MFMA A operand): row 16 (g >> 3) + fc, k
+    // 32 (g & 7) + 8 fq .. + 7 = chunk 4 (g & 7) + fq.  A 16-lane group
+    // reads 16 consecutive rows of one chunk: 256 contiguous bytes
+    typedef bf16x8_t AFrag[3];
+    const int fr_base = fq * 512 + fc * 16;
+    auto read_frag = [&](int k, int g, AFrag &f) {
+        const uint8_t *src = sh + (k & 1) * WS_PSTAGE + fr_base + (g >> 3) * 256 + (g & 7) * 2048;
+#pragma unroll
+        for (int p = 0; p < 3; ++p) f[p] = *reinterpret_cast<const bf16x8_t *>(src + p * WS_PLANE);
+    };
+    // accumulators [row tile][column tile]: hi (h.h) and lo (the five small
+    // products)
+    f32x4_t acc_h[2][4], acc_l[2][4];
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int ct = 0; ct < 4; ++ct) acc_h[t][ct] = acc_l[t][ct] = (f32x4_t){};
+    // output i = 4 ct + r of row tile t: row 16 t + 4 fq + r, column
+    // 64 w + 16 ct + fc (four 64-B row segments per store)
+    const int st_off = (4 * fq * XN + fc) * 4;
+    auto store_one = [&](int k, int t, int i) {
+        const int ct = i >> 2, r = i & 3;
+        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+            Cb + (int64_t)(j0 + k * per) * WS_RS * XN, 0, k < 0 ? 0 : WS_RS * XN * 4,
+            0x00020000);
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(acc_h[t][ct][r]), rs, st_off,
+                                              ((16 * t + r) * XN + 64 * w + 16 * ct) * 4, 0);
+    };
+    // the accumulators are operands of the wait-state pad, so the compiler
+    // cannot hoist the adds above it (next to the MFMAs that write them)
+    auto finish_tile = [&](int t) {
+        asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7"
+                     : "+v"(acc_h[t][0]), "+v"(acc_h[t][1]), "+v"(acc_h[t][2]),
+                       "+v"(acc_h[t][3]), "+v"(acc_l[t][0]), "+v"(acc_l[t][1]),
+                       "+v"(acc_l[t][2]), "+v"(acc_l[t][3])::"memory");
+#pragma unroll
+        for (int ct = 0; ct < 4; ++ct) acc_h[t][ct] = acc_h[t][ct] + acc_l[t][ct];
+    };
+    // the six products of row tile t, k32 step s, for the four column tiles
+    // (h += xh.wh; l += xh.wm, xm.wh, xh.wl, xl.wh, xm.wm: per output the
+    // order of gemm_x6_ws_kernel), interleaved over the column tiles
+    auto mfma_group = [&](bool first, int t, int s, const AFrag &x) {
+#pragma unroll
+        for (int ct = 0; ct < 4; ++ct) {
+            if (first) mfma16_first(acc_h[t][ct], x[0], Wa[ct][s][0]);
+            else mfma16_a(acc_h[t][ct], x[0], Wa[ct][s][0]);
+        }
+#pragma unroll
+        for (int ct = 0; ct < 4; ++ct) {
+            if (first) mfma16_first(acc_l[t][ct], x[0], Wa[ct][s][1]);
+            else mfma16_a(acc_l[t][ct], x[0], Wa[ct][s][1]);
+        }
+#pragma unroll
+        for (int ct = 0; ct < 4; ++ct) mfma16_a(acc_l[t][ct], x[1], Wa[ct][s][0]);
+#pragma unroll
+        for (int ct = 0; ct < 4; ++ct) mfma16_v(acc_l[t][ct], x[0], Wv[ct][s]);
+#pragma unroll
+        for (int ct = 0; ct < 4; ++ct) mfma16_a(acc_l[t][ct], x[2], Wa[ct][s][0]);
+#pragma unroll
+        for (int ct = 0; ct < 4; ++ct) mfma16_a(acc_l[t][ct], x[1], Wa[ct][s][1]);
+    };
+
+    if (R > 0) issue_rows(0);
+    if (R > 1) issue_rows(1);
+    __builtin_amdgcn_sched_barrier(0);
+    if (R > 1)
+        asm volatile("s_waitcnt vmcnt(8)" ::: "memory");     // weights + rows of step 0
+    else
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+    for (int q = 0; q < 8; ++q) split_rw(0, q >> 1, q & 1);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");       // staging slot 0 read
+    issue_rows(R > 2 ? 2 : R - 1);                           // clamped: never split
+    asm volatile("s_waitcnt vmcnt(8)" ::: "memory");         // step 1's staging
+    asm volatile("s_barrier" ::: "memory");                  // planes of step 0
+    AFrag fb[WS_NF];
+    read_frag(0, 0, fb[0]);
+    read_frag(0, 1, fb[1]);
+    // Row step k, per wave: phase t = row tile t's 8 k32 steps (4 column
+    // tiles x 6 products = 24 MFMAs each) with the other row tile's 16
+    // output stores beside them (t = 0: row tile 1 of step k - 1); fragments
+    // two k32 steps ahead; split half-unit q = 4 t + (s >> 1) of row step
+    // k + 1 read at even s, split and written at odd s, and behind each
+    // unit's second half the DMA of its two staging pieces for step k + 3;
+    // then lgkmcnt(0) + barrier.  No data-dependent branch (the same edge
+    // handling as gemm_x6_ws_kernel).
+    auto row_step = [&](int k) {
+        __builtin_amdgcn_sched_barrier(0);
+        asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+            const int ko = t == 1 ? k : k - 1;
+            finish_tile(1 - t);
+            float4 v;
+#pragma unroll
+            for (int s = 0; s < 8; ++s) {
+                const int g = 8 * t + s;
+                constexpr int D = WS_NF - 1;
+                if (g + D < 16) read_frag(k, g + D, fb[(g + D) % WS_NF]);
+                const int q = 4 * t + (s >> 1);
+                if ((s & 1) == 0) split_read(k + 1, q >> 1, q & 1, v);
+                mfma_group(s == 0, t, s, fb[g % WS_NF]);
+                store_one(ko, 1 - t, 2 * s);
+                store_one(ko, 1 - t, 2 * s + 1);
+                if ((s & 1) == 1) {
+                    const uint32_t h0 = pk_bf16(v.x, v.y);
+                    float ra = v.x - lo_f(h0), rb = v.y - hi_f(h0);
+                    const uint32_t m0 = pk_bf16(ra, rb);
+                    const uint32_t l0 = pk_bf16(ra - lo_f(m0), rb - hi_f(m0));
+                    const uint32_t h1 = pk_bf16(v.z, v.w);
+                    ra = v.z - lo_f(h1), rb = v.w - hi_f(h1);
+                    const uint32_t m1 = pk_bf16(ra, rb);
+                    const uint32_t l1 = pk_bf16(ra - lo_f(m1), rb - hi_f(m1));
+                    split_store(k + 1, q >> 1, q & 1, h0, h1, m0, m1, l0, l1);
+                    if (q & 1) {
+                        // unit q >> 1's staging pieces consumed: refill them
+                        // with step k + 3 (clamped: such rows are never split)
+                        const int u = q >> 1;
+                        const int k3 = k + 3 >= R ? R - 1 : k + 3;
+                        const float *r0 =
+                            Ab + ((int64_t)(j0 + k3 * per) * WS_RS + 8 * w) * XK;
+                        uint8_t *dst = sh + WS_LDS_F + ((k + 3) & 1) * WS_FSLOT + w * 8 * 1024;
+                        glds16_s(r0 + 32 * (2 * u), voff_f, lds_addr(dst + (2 * u) * 1024));
+                        glds16_s(r0 + 32 * (2 * u + 1), voff_f,
+                                 lds_addr(dst + (2 * u + 1) * 1024));
+                    }
+                }
+            }
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        read_frag(k + 1, 0, fb[0]);          // after the last step: unused
+        read_frag(k + 1, 1, fb[1]);
+    };
+    for (int k = 0; k < R; ++k) row_step(k);
+    if (R > 0) {
+        finish_tile(1);
+#pragma unroll
+        for (int i = 0; i < 16; ++i) store_one(R - 1, 1, i);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+// ---------------------------------------------------------------------------
 // Weight gradient of the same layer, dW[b] = G[b]^T H[b] (G = grad_z, H = the
 // layer input, both (m, 256) f32 row-major), split over C row chunks: block
 // (b, n-half, chunk) writes the 128 x 256 partial ws[b][chunk][n][k] of its
@@ -1044,7 +1284,8 @@ int dr_gemm_x6(int64_t batch, int64_t m, const float *a, const void *img, float 
     // plain stores: the next kernel reads C back from the Infinity Cache
     // (round 5: the streamed-l-plane form of gemm_x6_fl_kernel without its
     // epilogue, 112-113 vs 103-109 us for this kernel, bitwise the same C)
-    hipLaunchKernelGGL(gemm_x6_ws_kernel, dim3(grid), dim3(WS_THREADS), 0,
+    hipLaunchKernelGGL(X6_MFMA16 ? gemm_x6_ws16_kernel : gemm_x6_ws_kernel, dim3(grid),
+                       dim3(WS_THREADS), 0,
                        static_cast<hipStream_t>(stream), a, static_cast<const uint8_t *>(img), c,
                        m, (int)batch);
     const hipError_t e = hipGetLastError();

@@ -2608,8 +2608,15 @@ int dr_gemm_x6_bwd_first(int64_t batch, int64_t m, int64_t k, const float *grad_
     float *part = static_cast<float *>(workspace);
     float *part2 = reinterpret_cast<float *>(static_cast<char *>(workspace) +
                                              align_up(sizeof(float) * (size_t)(nb_fl * P)));
+    // the kernel writes one partial row per block and net: the workspace
+    // holds first_blocks(m) of them, checked before the launch (a device
+    // with more CUs than DR_FL_MAXB x 2 is refused, not overrun)
+    const int want = gemm_x6_fl_rows(2, m);
+    if (want < 1 || want > nb_fl)
+        return fail0(DR_ERR_UNSUPPORTED, "dr_gemm_x6_bwd_first: the kernel's grid exceeds the "
+                                         "workspace's partial rows on this device");
     const int per = gemm_x6_fl_launch(2, m, grad_z, img, h, ximg, part, st);
-    if (per < 1 || per > nb_fl)
+    if (per != want)
         return fail0(DR_ERR_HIP, std::string("dr_gemm_x6_bwd_first: ") +
                                      hipGetErrorString(hipGetLastError()));
     // direct: the per-block rows stay at the workspace start for a finish

@@ -55,9 +55,22 @@ constexpr int64_t W_FRAG = 64 * 16;     // one plane fragment: 1 KB
 // net) for wave w's column tile j and k16 step s: lane = fr + 32 fh holds
 // Bt[n = 64 w + 32 j + fr][k = 16 s + 8 fh .. + 7], so each fragment is one
 // coalesced 1-KB load.
+//
+// X6_MFMA16 (round 6): the fragments of v_mfma_f32_16x16x32_bf16 instead:
+// img[b][w][ct][s][p][lane][16 B], lane = c + 16 q holds
+// Bt[n = 64 w + 16 ct + c][k = 32 s + 8 q .. + 7] (4 column tiles of 16 x 8
+// k32 steps per wave; the same 1-KB fragments, the same image size).
+#ifndef X6_MFMA16
+#define X6_MFMA16 0
+#endif
 __host__ __device__ inline int64_t wimg_off(int n, int k0) {
+#if X6_MFMA16
+    const int w = n >> 6, ct = (n >> 4) & 3, c = n & 15, s = k0 >> 5, q = (k0 >> 3) & 3;
+    return ((int64_t)((w * 4 + ct) * 8 + s) * 3 * 64 + c + 16 * q) * 16;
+#else
     const int w = n >> 6, j = (n >> 5) & 1, fr = n & 31, s = k0 >> 4, fh = (k0 >> 3) & 1;
     return ((int64_t)((w * 2 + j) * 16 + s) * 3 * 64 + fr + 32 * fh) * 16;
+#endif
 }
 
 // Item t (b, n, 8-k chunk) of the weight image; transpose 2 builds both forms

@@ -408,10 +408,17 @@ class FusedTrainStep:
         # first layer's forward launch
         fl = (defer_finish and rows is None and pol.gemm_x6_fl and pol.obs_dim == 15 and
               pol.net_arch == (256, 256) and x6_weights(pol, M) is not None)
-        if fl and getattr(self, "_ximg", None) is None:
+        if fl:
+            # the observation image is written for the minibatch's M rows
+            # (by the first layer's launch or dr_gemm_x6_split_x) and read
+            # for M rows by dr_gemm_x6_bwd_first: sized for M, which the
+            # step's preallocated buffers fix at self.m (advisor r05)
             from . import _lib
-            self._ximg = torch.empty(_lib.lib().dr_gemm_x6_x_bytes(M), dtype=torch.uint8,
-                                     device=pol.device)
+            if M != self.m:
+                raise ValueError(f"minibatch of {M} rows on a FusedTrainStep built for {self.m}")
+            need = _lib.lib().dr_gemm_x6_x_bytes(M)
+            if getattr(self, "_ximg", None) is None or self._ximg.numel() < need:
+                self._ximg = torch.empty(need, dtype=torch.uint8, device=pol.device)
         fused_img = fl and pol.x6_fused_images
         hs = hidden_forward(pol, obs, self._acts, self._acts2, rows, top_preact=preact,
                             mark=self.mark, ximg=self._ximg if fused_img else None)
@@ -441,7 +448,8 @@ class FusedTrainStep:
             xw = x6_weights(pol, M)
             st = torch.cuda.current_stream(pol.device).cuda_stream
             if not fused_img:
-                _lib.check(_lib.lib().dr_gemm_x6_split_x(M, 15, obs.data_ptr(),
+                xo = obs.to(torch.float32).contiguous()
+                _lib.check(_lib.lib().dr_gemm_x6_split_x(M, 15, xo.data_ptr(),
                                                          self._ximg.data_ptr(), st))
                 mark("split_x")
             direct = int(pol.gemm_x6_fl_direct)

@@ -108,3 +108,18 @@ def test_no_collective_inside_the_timed_region_gloo_world2():
         # t0 up: the skew is scheduling jitter, far below the barrier's
         assert any(n == "all_reduce" and b <= t0 for n, a, b in calls)
         assert 0 <= tm["start_skew_us"] < 5_000, tm
+
+
+def test_multi_node_spans_use_the_slowest_rank(monkeypatch):
+    """Advisor r05: ranks on several nodes have unrelated CLOCK_MONOTONIC
+    readings, so the node wall falls back to the slowest rank's own span and
+    the start alignment is skipped."""
+    monkeypatch.setenv("LOCAL_WORLD_SIZE", "1")
+    assert not bench.single_node(2)
+    spans = [(1_000, 5_000, 1_000_000), (9_000_000_000, 9_000_007_000, 2_000_000)]
+    t = bench.node_timing(spans)
+    assert t["wall_s"] == t["max_rank_s"] == 7_000 / 1e9 and t["start_skew_us"] is None
+    monkeypatch.setenv("LOCAL_WORLD_SIZE", "2")
+    assert bench.single_node(2)
+    monkeypatch.delenv("LOCAL_WORLD_SIZE")
+    assert bench.single_node(2) and bench.single_node(1)

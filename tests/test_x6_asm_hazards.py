@@ -23,7 +23,7 @@ import pytest
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 SRC = os.path.join(ROOT, "drone_rl_amd", "csrc", "gemm_x6.hip")
 # the weight-stationary GEMM and (round 5) its first-layer-backward form
-KERNELS = ("gemm_x6_ws_kernel", "gemm_x6_fl_kernel")
+KERNELS = ("gemm_x6_ws_kernel", "gemm_x6_fl_kernel", "gemm_x6_ws16_kernel")
 # XDL (v_mfma_f32_32x32x16_bf16, 8 passes on gfx950) write VGPR -> VALU, VMEM
 # or LDS access of it: 11 wait states on gfx940-class parts; checked with margin
 WAIT = 18
