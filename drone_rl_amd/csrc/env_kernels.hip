@@ -42,14 +42,6 @@ constexpr double kFactor = kArm / 1.4142135623730951;  // L / np.sqrt(2)
 constexpr float kKyaw32 = 0.01f;  // python float * np.float32 -> f32 (NEP 50)
 constexpr double kDt = 0.02;
 
-// DR_ABLATE (diagnostic builds only, scripts/micro/ablate.sh; never set in
-// the product build): 1 = f32 trig, 2 = no auto-reset, 3 = no LDS obs
-// staging, 4 = divides by reciprocal multiplies, 5 = constant reset draws,
-// 6 = no physics, 7 = rollout kernel without its obs stores, 8 = rollout
-// kernel without the auto-reset.
-#ifndef DR_ABLATE
-#define DR_ABLATE 0
-#endif
 #ifndef DR_STRIDE_PAD
 #define DR_STRIDE_PAD 0
 #endif
@@ -80,11 +72,6 @@ __device__ unsigned long long g_stamps[16384 * 8];
 // 1: obs staged per wave (no block barrier); 0: per block
 #ifndef DR_WAVE_STAGE
 #define DR_WAVE_STAGE 1
-#endif
-// 1: load eps with the state, so the Philox reset path holds no global load
-// (6-8 % faster at 65,536-131,072 envs than loading it inside the reset)
-#ifndef DR_PREFETCH_EPS
-#define DR_PREFETCH_EPS 1
 #endif
 // 1 (A/B builds only; measured no gain): the Philox block of the reset draws
 // is computed for every lane right after the loads are issued (keyed by
@@ -269,7 +256,7 @@ __device__ inline void reset_uniforms(const EnvView<S> &v, int64_t i,
         for (int k = 0; k < NU; ++k) u[k] = v.host_u[i * NU + k];
         return;
     }
-    if (mode == 2 || DR_ABLATE == 5) {
+    if (mode == 2) {
 #pragma unroll
         for (int k = 0; k < NU; ++k) u[k] = 0.5;
         return;
@@ -296,13 +283,12 @@ __device__ inline void gym_reset_regs(const EnvView<S> &v, int64_t i, int mode,
                                       S st[F_N], int32_t ep_old, double eps,
                                       const u32x4 *pre0 = nullptr) {
     const int32_t ep_new = ep_old + 1;        // ep_num += 1          (61)
-    if (!DR_PREFETCH_EPS) eps = v.eps[i];
     if (ep_new % 2000 == 0) {                 // curriculum bump      (68-70)
         eps += 0.1;
         v.eps[i] = eps;
     }
     double u[5];
-    if (mode == 0 && DR_ABLATE != 5) {
+    if (mode == 0) {
         // Philox block 0 = (pos x, pos y, target x, target y); block 1 word
         // 0 = target z.  The target draws are multiplied by eps, and 0 * u
         // is exactly +0 for the uniforms in [0,1): while the curriculum is
@@ -415,7 +401,6 @@ __device__ inline void moving_reset_regs(const EnvView<S> &v, int64_t i, int mod
     const int32_t ep_new = ep_old + 1;
     double u[14];
     reset_uniforms<14>(v, i, ep_new, mode, u, pre4);
-    if (!DR_PREFETCH_EPS) eps = v.eps[i];
     if (ep_new % 2000 == 0) {
         eps += 0.1;
         v.eps[i] = eps;
@@ -469,13 +454,6 @@ __device__ inline MotorMix motor_mix(float4 act) {
 
 template <typename S, int VAR>
 __device__ inline S physics_step_mixed(S st[F_N], MotorMix mx, S dt, bool &crash) {
-#if DR_ABLATE == 6
-    // diagnostic: no physics (loads / stores / reset / obs as built)
-#pragma unroll
-    for (int k = 0; k < 12; ++k) st[k] += (S)mx.thr * (S)1e-300;
-    crash = st[F_POS + 2] < (S)0;
-    return (S)mx.phi;
-#endif
     // thrust / torques (drone.py:106, 113-117): f32 sums, f64 factor product,
     // the yaw torque stays f32.
     const float thr = mx.thr;
@@ -523,15 +501,9 @@ __device__ inline S physics_step_mixed(S st[F_N], MotorMix mx, S dt, bool &crash
     st[F_EUL + 2] += ed2 * dt;
 
     // Angular dynamics, diagonal inertia, old omega (135-139).
-#if DR_ABLATE == 4
-    const S wd0 = (tau_phi - (S)(kIyy - kIzz) * w1 * w2) * (S)(1.0 / kIxx);
-    const S wd1 = (tau_theta - (S)(kIzz - kIxx) * w0 * w2) * (S)(1.0 / kIyy);
-    const S wd2 = ((S)tau_psi - (S)(kIxx - kIyy) * w0 * w1) * (S)(1.0 / kIzz);
-#else
     const S wd0 = div_rcp(tau_phi - (S)(kIyy - kIzz) * w1 * w2, (S)kIxx, (S)(1.0 / kIxx));
     const S wd1 = div_rcp(tau_theta - (S)(kIzz - kIxx) * w0 * w2, (S)kIyy, (S)(1.0 / kIyy));
     const S wd2 = div_rcp((S)tau_psi - (S)(kIxx - kIyy) * w0 * w1, (S)kIzz, (S)(1.0 / kIzz));
-#endif
     st[F_OMG + 0] += wd0 * dt;
     st[F_OMG + 1] += wd1 * dt;
     st[F_OMG + 2] += wd2 * dt;
@@ -705,7 +677,9 @@ __global__ __launch_bounds__(kEnvBlock) void env_step_kernel(EnvView<S> v,
     double eps_old = 0.0;
     if constexpr (GYMLIKE) {
         if (!DR_HOIST_RESET) ep_old = *at(p_epn, i);
-        if (DR_PREFETCH_EPS) eps_old = *at(p_eps, i);
+        // eps loaded with the state: the Philox reset path holds no global
+        // load (6-8 % faster at 65,536-131,072 envs than loading it in the reset)
+        eps_old = *at(p_eps, i);
     }
     // VecMonitor counters: also loaded up front (a load after the physics
     // would put one more full memory latency on every wave)
@@ -768,7 +742,7 @@ __global__ __launch_bounds__(kEnvBlock) void env_step_kernel(EnvView<S> v,
         len = len0 + 1;
     }
     if constexpr (GYMLIKE) {
-        if (done && io.auto_reset && DR_ABLATE != 2) {
+        if (done && io.auto_reset) {
             // DummyVecEnv: keep the terminal obs, reset in the same step.
             if (io.term_obs) {
 #if DR_OBS_ONCE
@@ -825,13 +799,7 @@ __global__ __launch_bounds__(kEnvBlock) void env_step_kernel(EnvView<S> v,
 #pragma unroll
         for (int k = 0; k < OD; ++k) ob[k] = 0.f;
     }
-#if DR_ABLATE == 3
-    if (live) {
-#pragma unroll
-        for (int k = 0; k < OD; ++k) io.obs[i * OD + k] = ob[k];
-    }
-    (void)sh4;
-#elif DR_WAVE_STAGE
+#if DR_WAVE_STAGE
     store_obs_wave<OD, RPW>(reinterpret_cast<float *>(sh4), ob, io.obs, v.n);
 #else
     store_obs_block<OD>(reinterpret_cast<float *>(sh4), ob, io.obs, base, v.n);
@@ -962,7 +930,7 @@ __global__ __launch_bounds__(kEnvBlock) void env_rollout_kernel(EnvView<S> v, Ro
             st_out(at(io.done + row, i), (uint8_t)done);
         }
         if constexpr (GYMLIKE) {
-            if (done && io.auto_reset && DR_ABLATE != 8) {
+            if (done && io.auto_reset) {
                 step = 0;
                 reset_any = true;
                 if constexpr (VAR == DR_VARIANT_GYM) {
@@ -986,11 +954,7 @@ __global__ __launch_bounds__(kEnvBlock) void env_rollout_kernel(EnvView<S> v, Ro
         }
         // (plain stores for these outputs measured the same: 60.2 / 62.2 us
         // per 32-step launch at 65,536 envs)
-        if (DR_ABLATE == 7) {
-            asm volatile("" ::"v"(ob[0]), "v"(ob[5]), "v"(ob[14 % OD]));
-        } else {
-            store_obs_wave<OD, RPW>(reinterpret_cast<float *>(sh4), ob, io.obs + row * OD, n_);
-        }
+        store_obs_wave<OD, RPW>(reinterpret_cast<float *>(sh4), ob, io.obs + row * OD, n_);
     };
 
     if constexpr (GEN) {
@@ -1120,16 +1084,6 @@ __global__ __launch_bounds__(kEnvBlock) void env_rollout_kernel(EnvView<S> v, Ro
 //            hand: vmcnt counts loads and stores in issue order), B_t.
 //   After the last barrier the memory waves store step K - 1's outputs.
 // ----------------------------------------------------------------------------
-// DR_WS_ABL (diagnostic builds, wrong by construction; timing only):
-// 1 = the memory waves store no outputs; 2 = the physics waves skip the
-// physics (the state only advances by the action's thrust); 3 = no
-// auto-reset; 4 = no observation formed (zeros staged); 5 = no reset
-// Philox draws (the reset takes zero words: the same branch, fewer VALU);
-// 6 = no per-step barrier: the memory waves end after the prologue, the
-// physics waves step on the first action slot with no synchronisation
-#ifndef DR_WS_ABL
-#define DR_WS_ABL 0
-#endif
 constexpr int kWsEnvs = 256;                 // envs per block: 4 physics waves
 constexpr int kWsThreads = 2 * kWsEnvs;
 // D: how many steps ahead of the physics the memory waves issue an action
@@ -1217,7 +1171,7 @@ __global__ __launch_bounds__(kWsThreads) void env_rollout_ws_kernel(EnvView<S> v
             }
         };
         auto store_out = [&](int t) {
-            if (nvalid <= 0 || DR_WS_ABL == 1) return;
+            if (nvalid <= 0) return;
             const int so = t & 1;
             const int64_t row = (int64_t)t * n_;
             const float *src = &sh.obs[so][p * 64 * OD];
@@ -1245,7 +1199,6 @@ __global__ __launch_bounds__(kWsThreads) void env_rollout_ws_kernel(EnvView<S> v
         for (int t = 0; t <= kWsAhead && t < K; ++t) load_act(t);
         if (!GEN) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // actions 0 .. D
         asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");   // B_(-1)
-        if (DR_WS_ABL == 6) return;
         for (int t = 0; t < K; ++t) {
             if (t + kWsAhead + 1 < K) load_act(t + kWsAhead + 1);
             if (t >= 1) store_out(t - 1);
@@ -1317,10 +1270,10 @@ __global__ __launch_bounds__(kWsThreads) void env_rollout_ws_kernel(EnvView<S> v
     asm volatile("s_barrier" ::: "memory");                          // B_(-1)
     for (int t = 0; t < K; ++t) {
         asm volatile("" : "+s"(vk.seed_lo), "+s"(vk.seed_hi));
-        const float4 a_cur = sh.act[DR_WS_ABL == 6 ? 0 : t % kWsNA][p * 64 + lane];
+        const float4 a_cur = sh.act[t % kWsNA][p * 64 + lane];
         const MotorMix mx = motor_mix(a_cur);
         if constexpr (GYMLIKE) {
-            if (t % kResetAhead == 0 && !nd_ok && DR_WS_ABL != 5) {
+            if (t % kResetAhead == 0 && !nd_ok) {
 #pragma unroll
                 for (int b = 0; b < NB; ++b)
                     nd[b] = philox4x32_10(u32x4{(uint32_t)(ep_num + 1), (uint32_t)gid,
@@ -1333,18 +1286,11 @@ __global__ __launch_bounds__(kWsThreads) void env_rollout_ws_kernel(EnvView<S> v
             moving_target(cen, mp, step + 1, (float)v.dt, &st[F_TGT], tvel);
         bool crash;
         S r;
-        if (DR_WS_ABL == 2) {
-            st[F_VEL + 2] += (S)mx.thr * v.dt;
-            st[F_POS + 2] += st[F_VEL + 2] * v.dt;
-            crash = st[F_POS + 2] < (S)0;
-            r = st[F_POS + 2];
-        } else {
-            r = physics_step_mixed<S, VAR>(st, mx, v.dt, crash);
-        }
+        r = physics_step_mixed<S, VAR>(st, mx, v.dt, crash);
         step += 1;
         const bool done = live && (crash || (step >= max_steps));
         if constexpr (GYMLIKE) {
-            const bool rs = done && io.auto_reset && DR_WS_ABL != 3;
+            const bool rs = done && io.auto_reset;
             if (rs) {
                 step = 0;
                 reset_any = true;
@@ -1352,7 +1298,7 @@ __global__ __launch_bounds__(kWsThreads) void env_rollout_ws_kernel(EnvView<S> v
                 // same words the reset would draw; always passing the array
                 // keeps it in registers -- a pointer-or-null argument put it
                 // on the scratch stack)
-                if (!nd_ok && DR_WS_ABL != 5) {
+                if (!nd_ok) {
 #pragma unroll
                     for (int b = 0; b < NB; ++b)
                         nd[b] = philox4x32_10(u32x4{(uint32_t)(ep_num + 1), (uint32_t)gid,
@@ -1371,12 +1317,7 @@ __global__ __launch_bounds__(kWsThreads) void env_rollout_ws_kernel(EnvView<S> v
                 if (ep_num % 2000 == 0) eps += 0.1;
             }
         }
-        if (DR_WS_ABL == 4) {
-#pragma unroll
-            for (int k = 0; k < OD; ++k) ob[k] = 0.f;
-        } else {
-            make_obs<S, OD>(st, ob, tvel);
-        }
+        make_obs<S, OD>(st, ob, tvel);
         if (!live) {
 #pragma unroll
             for (int k = 0; k < OD; ++k) ob[k] = 0.f;
@@ -1388,10 +1329,7 @@ __global__ __launch_bounds__(kWsThreads) void env_rollout_ws_kernel(EnvView<S> v
         sh.rew[so][p * 64 + lane] = (float)r;
         sh.done[so][p * 64 + lane] = (uint8_t)done;
         __builtin_amdgcn_sched_barrier(0);
-        if (DR_WS_ABL == 6)
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        else
-            asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");   // B_t
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");   // B_t
     }
     if (live) {
 #pragma unroll

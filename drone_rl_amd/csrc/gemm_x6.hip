@@ -116,7 +116,7 @@ __device__ inline uint32_t lds_addr(const uint8_t *p) {
 // Measured (scripts/micro/gemm_x6_bench.py, both nets, 65,536 rows): 112-117
 // us against 118-120 for round 3's kernel on the same boxes.  In-kernel stamps
 // (DR_WS_STAMPS, scripts/micro/ws_stamps.py): a row step takes ~9,800-10,500
-// shader cycles against 6,144 of MFMA; by ablation (DR_WS_ABL) the split
+// shader cycles against 6,144 of MFMA; by ablation (scripts/micro/patches/x6_diag.patch) the split
 // costs ~2,300 of them, the fragment reads ~900, the stores ~570.  Moving the
 // split VALU into the MFMA asm (so it issues in the MFMAs' shadow) needs ~10
 // more VGPRs than the 512-register budget leaves (weights 384 + accumulators
@@ -128,12 +128,6 @@ constexpr int WS_FSLOT = WS_RS * XK * 4;             // 32 KB: f32 rows of a row
 constexpr int WS_LDS_F = 2 * WS_PSTAGE;              // staging after the two plane stages
 constexpr int WS_LDS = 2 * WS_PSTAGE + 2 * WS_FSLOT; // 160 KB
 constexpr int WS_THREADS = 256;
-// DR_WS_ABL (diagnostic builds only, wrong results): 1 no split in the loop,
-// 2 no row DMA in the loop, 3 no output stores, 4 no fragment reads in the
-// loop, 5 no barrier in the loop
-#ifndef DR_WS_ABL
-#define DR_WS_ABL 0
-#endif
 // fragment sets in flight (read two k16 steps ahead)
 constexpr int WS_NF = 3;
 // DR_WS_STAMPS (diagnostic builds only): s_memtime at six points of every row
@@ -311,7 +305,6 @@ __global__ __launch_bounds__(WS_THREADS, 1) void gemm_x6_ws_kernel(
         const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
             Cb + (int64_t)(j0 + k * per) * WS_RS * XN, 0, k < 0 ? 0 : WS_RS * XN * 4,
             0x00020000);
-        if (DR_WS_ABL == 3 && acc_h[t][r] != 12345.f) return;
         __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(acc_h[t][r]), rs, st_off,
                                               ((8 * (r >> 2) + (r & 3)) * XN + 64 * w + 32 * t) * 4,
                                               0);
@@ -380,19 +373,18 @@ __global__ __launch_bounds__(WS_THREADS, 1) void gemm_x6_ws_kernel(
                 // fragments of g + D (tile 1 re-reads steps 0 .. D - 1)
                 const int g = 16 * t + s;
                 constexpr int D = WS_NF - 1;           // prefetch distance
-                if (g + D < 32 && (DR_WS_ABL != 4 || g < D))
+                if (g + D < 32)
                     read_frag(k, (g + D) & 15, fb[(g + D) % WS_NF]);
                 const int q = 4 * t + (s >> 2);        // split half-unit
                 // half-unit q: read before k16 step 4 (q - 4 t) + 1; its two
                 // pairs split inside the MFMA groups of steps + 2 and + 3;
                 // written (3 x 8 B) after the second
-                const bool sp = DR_WS_ABL != 1;
-                if (sp && (s & 3) == 0) split_read(k + 1, q >> 1, q & 1, v);
+                if ((s & 3) == 0) split_read(k + 1, q >> 1, q & 1, v);
                 const AFrag &x = fb[g % WS_NF];
                 mfma_x6_group(s == 0, acc_h[t], acc_l[t], x[0], x[1], x[2], Wa[t][s][0],
                               Wa[t][s][1], Wv[t][s]);
-                if (DR_WS_ABL != 3) store_one(ko, 1 - t, s);
-                if (sp && (s & 3) == 1) {
+                store_one(ko, 1 - t, s);
+                if ((s & 3) == 1) {
                     // the half-unit's split (its read, one k16 step ago, has
                     // landed behind the MFMAs)
                     sh0 = pk_bf16(v.x, v.y);
@@ -404,9 +396,9 @@ __global__ __launch_bounds__(WS_THREADS, 1) void gemm_x6_ws_kernel(
                     sm1 = pk_bf16(ra, rb);
                     sl1 = pk_bf16(ra - lo_f(sm1), rb - hi_f(sm1));
                 }
-                if (sp && (s & 3) == 1) {
+                if ((s & 3) == 1) {
                     split_store(k + 1, q >> 1, q & 1, sh0, sh1, sm0, sm1, sl0, sl1);
-                    if ((q & 1) && DR_WS_ABL != 2) {
+                    if (q & 1) {
                         // unit q >> 1's two staging pieces were read (the
                         // split above consumed the data, and asm volatile
                         // keeps the DMA behind it): refill them with step k + 3
@@ -428,10 +420,7 @@ __global__ __launch_bounds__(WS_THREADS, 1) void gemm_x6_ws_kernel(
         // this wave's plane writes (step k + 1) and fragment reads (step k)
         // done; after the barrier the planes of k + 1 are complete
         __builtin_amdgcn_sched_barrier(0);
-        if (DR_WS_ABL == 5)
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        else
-            asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
         WS_STAMP(k, 5);
         read_frag(k + 1, 0, fb[0]);          // after the last step: unused
         if (WS_NF == 3) read_frag(k + 1, 1, fb[1]);
@@ -1058,13 +1047,8 @@ __global__ __launch_bounds__(WS_THREADS, 1) void gemm_x6_fl_kernel(
         float *hv = hb[FL_H_EARLY ? tt : 0];
         const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
             (void *)(Hb + (int64_t)(j0 + kk * per) * WS_RS * XN), 0, WS_RS * XN * 4, kBufFlags);
-#ifdef FL_NO_H
-        (void)rs;
-        hv[r] = 0.5f;
-#else
         hv[r] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(
             rs, hoff[tt], (8 * (r >> 2) + (r & 3)) * XN * 4, 0));
-#endif
     };
     // lane (m = fr, fh) of X^T's fragment: feature fr & 15 of column tile
     // fr >> 4; the other tile's lanes load from past the record's end, which
@@ -1083,9 +1067,6 @@ __global__ __launch_bounds__(WS_THREADS, 1) void gemm_x6_fl_kernel(
     // registers 8 j .. 8 j + 7 of tile tt, split into the B fragment planes,
     // and the six x6 products into D2
     auto d2_kstep = [&](int tt, int j, const bf16x8_t (&xf)[3]) {
-#ifdef FL_NO_D2
-        return;
-#endif
         float gz[8];
 #pragma unroll
         for (int e = 0; e < 8; ++e) {

@@ -940,13 +940,7 @@ __device__ inline void x6_aux_block(int bx, int64_t m, int k, const float *__res
 // (round 3 A/B, removed in round 4: two rows per wave and iteration measured
 // 38.1 vs 37.6-37.8 us per call; the input row through per-lane loads and
 // readlanes instead of scalar loads, slower)
-// diagnostic builds of linear_tanh_kernel (wrong by construction; timing
-// only, scripts/micro/ab_ppo_kern.sh, scripts/micro/lt_ab.py): 1 = no tanh,
-// 2 = no per-row store, 3 = no input loads, 4 = no input loads and no
-// arithmetic (the row stores alone), 5 = no weight loads
-#ifndef DR_LT_ABL
-#define DR_LT_ABL 0
-#endif
+// (diagnostic ablations of linear_tanh_kernel and the head kernel: scripts/micro/patches/ppo_diag.patch)
 // minimum rows per block (4 waves) of linear_tanh_kernel (A/B knob)
 #ifndef DR_LT_RPB
 #define DR_LT_RPB 64
@@ -981,8 +975,7 @@ __global__ __launch_bounds__(kBlock) void linear_tanh_kernel(int64_t m, int n,
         float flat[4 * K];
 #pragma unroll
         for (int t = 0; t < K; ++t) {
-            const float4 v4 = DR_LT_ABL == 5 ? make_float4(0.01f * t, 0.02f, 0.03f, 0.04f * c0)
-                                             : w4[t];
+            const float4 v4 = w4[t];
             flat[4 * t + 0] = v4.x;
             flat[4 * t + 1] = v4.y;
             flat[4 * t + 2] = v4.z;
@@ -1005,11 +998,8 @@ __global__ __launch_bounds__(kBlock) void linear_tanh_kernel(int64_t m, int n,
     if (r < m) {
         const float *xr = x + xrow(r) * K;
 #pragma unroll
-        for (int k = 0; k < K; ++k) xn[k] = DR_LT_ABL >= 3 ? 0.1f * (float)k : xr[k];
+        for (int k = 0; k < K; ++k) xn[k] = xr[k];
     }
-#if DR_LT_ABL == 2
-    float4 keep = make_float4(0.f, 0.f, 0.f, 0.f);
-#endif
     for (; r < m; r += stride) {
         float xv[K];
 #pragma unroll
@@ -1018,13 +1008,8 @@ __global__ __launch_bounds__(kBlock) void linear_tanh_kernel(int64_t m, int n,
         if (rn < m) {
             const float *xr = x + xrow(rn) * K;
 #pragma unroll
-            for (int k = 0; k < K; ++k)
-                xn[k] = DR_LT_ABL >= 3 ? xv[k] + 1e-3f * (float)(rn & 7) : xr[k];
+            for (int k = 0; k < K; ++k) xn[k] = xr[k];
         }
-#if DR_LT_ABL == 4      // diagnostic: the row stores alone
-        if (act) st4(h + r * n + c0, make_float4(xv[0], xv[1], xv[2], xv[3]));
-        continue;
-#endif
 #if DR_TANH_RAT
         // the same fmaf chain per column, written as packed pairs (columns
         // 0-1, 2-3), and the pairs' rational tanh
@@ -1036,17 +1021,9 @@ __global__ __launch_bounds__(kBlock) void linear_tanh_kernel(int64_t m, int n,
             a23 = pk_fma(xk, f32x2{wr[2][k], wr[3][k]}, a23);
         }
         if (act) {
-#if DR_LT_ABL == 1      // diagnostic: no tanh
-            const f32x2 t01 = a01 + f32x2{bb[0], bb[1]}, t23 = a23 + f32x2{bb[2], bb[3]};
-#else
             const f32x2 t01 = tanh_rat2(a01 + f32x2{bb[0], bb[1]});
             const f32x2 t23 = tanh_rat2(a23 + f32x2{bb[2], bb[3]});
-#endif
-#if DR_LT_ABL == 2      // diagnostic: no per-row store
-            keep = add4(keep, make_float4(t01.x, t01.y, t23.x, t23.y));
-#else
             st4(h + r * n + c0, make_float4(t01.x, t01.y, t23.x, t23.y));
-#endif
         }
         continue;
 #endif
@@ -1056,24 +1033,11 @@ __global__ __launch_bounds__(kBlock) void linear_tanh_kernel(int64_t m, int n,
 #pragma unroll
             for (int q = 0; q < 4; ++q) acc[q] = fmaf(xv[k], wr[q][k], acc[q]);
         }
-#if DR_LT_ABL == 1      // diagnostic: no tanh
-        if (act)
-            st4(h + r * n + c0, make_float4(acc[0] + bb[0], acc[1] + bb[1], acc[2] + bb[2],
-                                            acc[3] + bb[3]));
-#elif DR_LT_ABL == 2    // diagnostic: no per-row store (one store per wave at the end)
-        const float4 t4 = make_float4(tanh_fast(acc[0] + bb[0]), tanh_fast(acc[1] + bb[1]),
-                                      tanh_fast(acc[2] + bb[2]), tanh_fast(acc[3] + bb[3]));
-        keep = add4(keep, t4);
-#else
         if (act)
             st4(h + r * n + c0,
                 make_float4(tanh_fast(acc[0] + bb[0]), tanh_fast(acc[1] + bb[1]),
                             tanh_fast(acc[2] + bb[2]), tanh_fast(acc[3] + bb[3])));
-#endif
     }
-#if DR_LT_ABL == 2
-    if (act && keep.x == 12345.f) st4(h + c0, keep);
-#endif
 }
 
 // Policy heads for inference (rollouts): mean = h_pi Wa^T + ba (m,4),
@@ -1160,9 +1124,6 @@ struct HeadArgs {
 #define DR_HEAD_TILE 4
 #endif
 constexpr int kHeadTile = DR_HEAD_TILE;
-#ifndef DR_HEAD_DIAG
-#define DR_HEAD_DIAG 0
-#endif
 // (round 3 A/B, removed in round 4: the next tile's activation rows loaded
 // while this tile computes, +16 VGPRs per wave, slower)
 
@@ -1195,11 +1156,7 @@ __device__ inline void head_policy_wave(const HeadArgs &a, const RowLossConst &c
         if (a.preact) {
 #pragma unroll
             for (int i = 0; i < kHeadTile; ++i)
-#if DR_HEAD_DIAG == 1  // timing diagnostic only (wrong results): no top tanh
-                h[i] = add4(h[i], zb);
-#else
                 h[i] = tanh4(add4(h[i], zb));
-#endif
         }
         float mu[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
@@ -1273,11 +1230,7 @@ __device__ inline void head_value_wave(const HeadArgs &a, const RowLossConst &c,
         if (a.preact) {
 #pragma unroll
             for (int i = 0; i < kHeadTile; ++i)
-#if DR_HEAD_DIAG == 1
-                h[i] = add4(h[i], zb);
-#else
                 h[i] = tanh4(add4(h[i], zb));
-#endif
         }
         float v = 0.f;
 #pragma unroll
