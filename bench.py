@@ -665,11 +665,8 @@ def ppo_kernel_times(tr, reps=20):
     the timed region (it applies more optimizer steps)."""
     import torch
 
-    from drone_rl_amd import ppo_kernels as K
     cfg = tr.cfg
-    T, N, M = cfg.n_steps, cfg.num_envs, cfg.batch_size
-    obs_flat = tr.obs[:T].reshape(T * N, -1)
-    act_flat = tr.actions.reshape(T * N, 4)
+    M = cfg.batch_size
     idx = tr.perm(seed=99, counter=0)[:M]
     stream = torch.cuda.current_stream(tr.device)
     sched = tr.opt.schedule(tr.opt.t + 1, 1).to(tr.device)
@@ -686,8 +683,7 @@ def ppo_kernel_times(tr, reps=20):
                 raise _StopStep
         tr.fused.mark = mark
         try:
-            K.gather_minibatch(idx, obs_flat, act_flat, tr.aux, tr.mb_obs, tr.mb_act,
-                               tr.mb_aux, adv_part=tr.head.adv_part)
+            tr.gather(idx, tr.mb_obs, tr.mb_act, tr.mb_aux, tr.head.adv_part)
             mark("gather_minibatch")
             grad, _ = tr.fused.step(tr.mb_obs, tr.mb_act, tr.mb_aux, tr.head, adv_ready=True,
                                     defer_finish=True)
@@ -755,7 +751,7 @@ def ppo_kernel_times(tr, reps=20):
 
 
 # bench.py's PPO step names -> the kernel each launches (rocprofv3 names)
-PPO_KERNEL_NAMES = {"gather_minibatch": "gather_minibatch_kernel",
+PPO_KERNEL_NAMES = {"gather_minibatch": "gather_records_kernel",
                     "linear_tanh": "linear_tanh_kernel", "ppo_head": "ppo_head_kernel",
                     "first_layer_bwd": "first_layer_bwd_kernel",
                     "gemm_x6_fwd": "gemm_x6_ws_kernel", "gemm_x6_bwd": "gemm_x6_ws_kernel",
@@ -828,7 +824,9 @@ def ppo_roofline(cfg, s_per_update, ktimes, rocprof=None, isolated=None, rocprof
     M, NT, E = cfg.batch_size, cfg.num_envs * cfg.n_steps, cfg.n_epochs
     flop_update = NT * PPO_FWD_FLOP * (1 + 3 * E)
     gemm_flop = 2 * 2 * M * 256 * 256            # both nets, one fp32 GEMM
-    rows = {"gather_minibatch": 2 * (15 + 4 + 3) * 4,
+    # the gather: 88 B of each row's record read (one 128-B line) + its 4-B
+    # index, 88 B written
+    rows = {"gather_minibatch": 2 * (15 + 4 + 3) * 4 + 4,
             "linear_tanh": 15 * 4 + 2 * 256 * 4,
             "ppo_head": 2 * 1024 + 2 * 1024 + 44,
             "first_layer_bwd": 2 * 2 * 1024 + 60,

@@ -23,7 +23,7 @@ DR_ERR_HIP = -2
 DR_ERR_NOMEM = -3
 DR_ERR_UNSUPPORTED = -4
 
-ABI_VERSION = 15                # DR_ABI_VERSION in include/dronerl.h
+ABI_VERSION = 16                # DR_ABI_VERSION in include/dronerl.h
 DR_VARIANT_GYM = 0
 DR_VARIANT_VECTORIZED = 1
 DR_VARIANT_MOVING = 2
@@ -104,6 +104,8 @@ SIGNATURES = {
     "dr_permutation_dev": (c_int, [c_int64, c_uint64, _P, c_uint64, _P, _P, c_size_t, _P]),
     "dr_gather_rows": (c_int, [c_int64, c_int64, _P, _P, _P, _P]),
     "dr_gather_minibatch": (c_int, [c_int64, _P, c_int64] + [_P] * 8),
+    "dr_pack_rollout_records": (c_int, [c_int64, c_int64] + [_P] * 7),
+    "dr_gather_records": (c_int, [c_int64, _P, c_int64] + [_P] * 6),
     "dr_linear_tanh2": (c_int, [c_int64, c_int64, c_int64] + [_P] * 9),
     "dr_first_layer_backward2_workspace_bytes": (c_size_t, [c_int64, c_int64, c_int64]),
     "dr_first_layer_backward2": (c_int, [c_int64, c_int64, c_int64] + [_P] * 10 +

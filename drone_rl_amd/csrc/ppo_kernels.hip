@@ -569,6 +569,98 @@ __global__ __launch_bounds__(kBlock) void gather_minibatch_kernel(
     }
 }
 
+// ---------------------------------------------------------------------------
+// One-line rollout records (round 6, verdict r05 item 5).  gather_minibatch_
+// kernel reads each random rollout row from three arrays (60-B obs, 16-B
+// action, 12-B aux), each in its own 128-B lines: 3.7 TCP -> TCC requests per
+// row and 5.1x the algorithmic read bytes (profiles/r05_gather_pmc.json).
+// pack_records_kernel writes every rollout row once per PPO iteration as one
+// aligned 128-B record -- floats 0 .. obs_dim - 1 the obs, 16 .. 19 the
+// action, 20 .. 22 (old log-prob, advantage, return), the rest zero -- and
+// gather_records_kernel reads ONE line per gathered row.
+constexpr int kRecF = DR_RECORD_FLOATS;          // 32 floats = 128 B
+
+// thread (row, float4 slot s of 8): s 0..3 obs floats 4 s .. 4 s + 3, s 4
+// the action, s 5 the aux triple, s 6..7 zeros; the stores are contiguous
+__global__ __launch_bounds__(kBlock) void pack_records_kernel(
+    int64_t n, int obs_dim, const float *__restrict__ obs, const float4 *__restrict__ act,
+    const float *__restrict__ logp, const float *__restrict__ adv, const float *__restrict__ ret,
+    float4 *__restrict__ rec) {
+    const int64_t t = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    const int64_t row = t >> 3;
+    const int s = (int)(t & 7);
+    if (row >= n) return;
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (s < 4) {
+        const float *o = obs + row * obs_dim;
+        const int c = 4 * s;
+        if (c + 0 < obs_dim) v.x = o[c + 0];
+        if (c + 1 < obs_dim) v.y = o[c + 1];
+        if (c + 2 < obs_dim) v.z = o[c + 2];
+        if (c + 3 < obs_dim) v.w = o[c + 3];
+    } else if (s == 4) {
+        v = act[row];
+    } else if (s == 5) {
+        v = make_float4(logp[row], adv[row], ret[row], 0.f);
+    }
+    rec[row * (kRecF / 4) + s] = v;
+}
+
+// One thread per gathered row (blocks of 256 rows, as the aux blocks of
+// gather_minibatch_kernel): six 16-B loads of the row's record (one line),
+// the obs rows staged in LDS and written as contiguous float4, the action
+// and aux rows stored directly, and the block's advantage (count, mean, M2)
+// partial -- the same rows, values and reduction order as
+// gather_minibatch_kernel, so every output byte is the same.
+__global__ __launch_bounds__(kBlock) void gather_records_kernel(
+    int64_t m, int obs_dim, const int32_t *__restrict__ idx, const float4 *__restrict__ rec,
+    float *__restrict__ obs_out, float4 *__restrict__ act_out, float *__restrict__ aux_out,
+    float *__restrict__ adv_part) {
+    __shared__ float so[kBlock * 15];
+    __shared__ float sh[8];
+    const int b = blockIdx.x;
+    const int64_t i0 = (int64_t)b * kBlock, i = i0 + threadIdx.x;
+    const int cnt = (int)min((int64_t)kBlock, m - i0);
+    float ai = 0.f;
+    if (i < m) {
+        const float4 *r = rec + (int64_t)idx[i] * (kRecF / 4);
+        float4 q[6];
+#pragma unroll
+        for (int s = 0; s < 6; ++s) q[s] = r[s];
+        const float o[16] = {q[0].x, q[0].y, q[0].z, q[0].w, q[1].x, q[1].y, q[1].z, q[1].w,
+                             q[2].x, q[2].y, q[2].z, q[2].w, q[3].x, q[3].y, q[3].z, q[3].w};
+#pragma unroll
+        for (int k = 0; k < 15; ++k)
+            if (k < obs_dim) so[threadIdx.x * obs_dim + k] = o[k];
+        act_out[i] = q[4];
+        aux_out[3 * i] = q[5].x;
+        aux_out[3 * i + 1] = q[5].y;
+        aux_out[3 * i + 2] = q[5].z;
+        ai = q[5].y;
+    }
+    __syncthreads();
+    // the block's cnt obs rows are cnt * obs_dim contiguous floats starting
+    // at a multiple of 256 * obs_dim (16-byte aligned: obs_out is)
+    const int nf = cnt * obs_dim;
+    float *dst = obs_out + i0 * obs_dim;
+    for (int q = threadIdx.x; q < nf / 4; q += kBlock)
+        reinterpret_cast<float4 *>(dst)[q] =
+            make_float4(so[4 * q], so[4 * q + 1], so[4 * q + 2], so[4 * q + 3]);
+    for (int q = (nf / 4) * 4 + threadIdx.x; q < nf; q += kBlock) dst[q] = so[q];
+    if (!adv_part) return;
+    float x[1] = {ai};
+    block_sum<1>(x, sh);
+    const float mean = x[0] / (float)cnt;
+    float d = i < m ? ai - mean : 0.f;
+    float y[1] = {d * d};
+    block_sum<1>(y, sh);
+    if (threadIdx.x == 0) {
+        adv_part[3 * b + 0] = (float)cnt;
+        adv_part[3 * b + 1] = mean;
+        adv_part[3 * b + 2] = y[0];
+    }
+}
+
 // Chan et al. merge of (n, mean, M2) b into a.
 __device__ inline void chan_merge(double &n, double &mu, double &M2, double nb_, double mb,
                                   double m2b) {
@@ -1981,6 +2073,43 @@ int dr_gather_minibatch(int64_t m, const int32_t *idx, int64_t obs_dim, const fl
                        (int)nb_rows, idx, obs, reinterpret_cast<const float4 *>(actions), aux,
                        obs_out, reinterpret_cast<float4 *>(actions_out), aux_out, adv_part);
     return check_launch("dr_gather_minibatch");
+}
+
+int dr_pack_rollout_records(int64_t n, int64_t obs_dim, const float *obs, const float *actions,
+                            const float *logp, const float *adv, const float *ret,
+                            float *records, void *stream) {
+    if (n < 0 || obs_dim < 1 || obs_dim > 15 || !obs || !actions || !logp || !adv || !ret ||
+        !records)
+        return fail0(DR_ERR_INVALID, "dr_pack_rollout_records: bad arguments (1 <= obs_dim <= 15)");
+    if ((((uintptr_t)actions) | ((uintptr_t)records)) & 15)
+        return fail0(DR_ERR_INVALID,
+                     "dr_pack_rollout_records: actions and records must be 16-byte aligned");
+    if (n == 0) return DR_OK;
+    if (n > (int64_t(1) << 31))
+        return fail0(DR_ERR_INVALID, "dr_pack_rollout_records: n too large");
+    hipLaunchKernelGGL(pack_records_kernel, dim3((unsigned)grid_for(8 * n)), dim3(kBlock), 0,
+                       as_stream(stream), n, (int)obs_dim, obs,
+                       reinterpret_cast<const float4 *>(actions), logp, adv, ret,
+                       reinterpret_cast<float4 *>(records));
+    return check_launch("dr_pack_rollout_records");
+}
+
+int dr_gather_records(int64_t m, const int32_t *idx, int64_t obs_dim, const float *records,
+                      float *obs_out, float *actions_out, float *aux_out, float *adv_part,
+                      void *stream) {
+    if (m < 0 || obs_dim < 1 || obs_dim > 15 || !idx || !records || !obs_out || !actions_out ||
+        !aux_out)
+        return fail0(DR_ERR_INVALID, "dr_gather_records: bad arguments (1 <= obs_dim <= 15)");
+    if ((((uintptr_t)records) | ((uintptr_t)actions_out) | ((uintptr_t)obs_out)) & 15)
+        return fail0(DR_ERR_INVALID,
+                     "dr_gather_records: records, obs_out and actions_out must be 16-byte aligned");
+    if (m == 0) return DR_OK;
+    if (grid_for(m) > INT32_MAX) return fail0(DR_ERR_INVALID, "dr_gather_records: m too large");
+    hipLaunchKernelGGL(gather_records_kernel, dim3((unsigned)grid_for(m)), dim3(kBlock), 0,
+                       as_stream(stream), m, (int)obs_dim, idx,
+                       reinterpret_cast<const float4 *>(records), obs_out,
+                       reinterpret_cast<float4 *>(actions_out), aux_out, adv_part);
+    return check_launch("dr_gather_records");
 }
 
 size_t dr_tanh_backward_workspace_bytes(int64_t m, int64_t n) {

@@ -146,6 +146,10 @@ class PPOTrainer:
         self.adv = torch.zeros(T, N, **f32)
         self.ret = torch.zeros(T, N, **f32)
         self.aux = torch.zeros(T * N, 3, **f32)                 # (old logp, adv, return)
+        # the fused path's minibatch source: every rollout row as one 128-B
+        # record (obs, action, aux), packed once per iteration, so the
+        # gather reads one cache line per row (dr_gather_records, round 6)
+        self.rec = None
         # bootstrap_timeouts: per-step truncation flags (dr_step_monitored_trunc)
         self.trunc = torch.zeros(T, N, dtype=torch.uint8, device=dev) \
             if cfg.bootstrap_timeouts else None
@@ -256,8 +260,17 @@ class PPOTrainer:
         _, last_values = fwd(self.obs[T])
         K.gae(self.rewards, self.values, self.dones[:T], last_values, self.dones[T],
               cfg.gamma, cfg.gae_lambda, advantages=self.adv, returns=self.ret)
+        # (old log-prob, advantage, return) rows: the unfused path's minibatch
+        # source, and what callers inspect after a rollout
         torch.stack([self.logp.reshape(-1), self.adv.reshape(-1), self.ret.reshape(-1)],
                     dim=1, out=self.aux)
+        if self.use_fused:
+            if self.rec is None:
+                self.rec = torch.zeros(T * cfg.num_envs, K.RECORD_FLOATS, dtype=torch.float32,
+                                       device=self.device)
+            K.pack_rollout_records(self.obs[:T].reshape(T * cfg.num_envs, -1),
+                                   self.actions.reshape(-1, 4), self.logp.reshape(-1),
+                                   self.adv.reshape(-1), self.ret.reshape(-1), self.rec)
         self.num_timesteps += T * cfg.num_envs * self.world
 
     def _rollout_steps(self, fwd):
@@ -327,10 +340,16 @@ class PPOTrainer:
                                  counter_offset=epoch)
             for k in range(nmb):
                 idx = perm[k * M:(k + 1) * M]
-                K.gather_minibatch(idx, obs_flat, act_flat, self.aux, self.mb_obs, self.mb_act,
-                                   self.mb_aux, adv_part=self.head.adv_part)
+                self.gather(idx, self.mb_obs, self.mb_act, self.mb_aux, self.head.adv_part)
                 self._train_minibatch(j, self.mb_obs, self.mb_act, self.mb_aux)
                 j += 1
+
+    def gather(self, idx, obs_out, act_out, aux_out, adv_part):
+        """The fused path's minibatch gather (RolloutBuffer.get's indexing)
+        from this iteration's packed rollout records: one launch, one cache
+        line per row, the same bytes as dr_gather_minibatch."""
+        K.gather_records(idx, self.rec, self.env.obs_dim, obs_out, act_out, aux_out,
+                         adv_part=adv_part)
 
     def _train_minibatch(self, j, mb_obs, mb_act, mb_aux):
         """Optimizer step j on one gathered minibatch (its advantage partials
@@ -375,8 +394,7 @@ class PPOTrainer:
         def gather(j):
             k = j % nmb
             o, a, x, ws = slots[j & 1]
-            K.gather_minibatch(perm[0][k * M:(k + 1) * M], obs_flat, act_flat, self.aux, o, a,
-                               x, adv_part=ws)
+            self.gather(perm[0][k * M:(k + 1) * M], o, a, x, ws)
 
         ws0 = self.head.ws
         try:
@@ -459,8 +477,8 @@ class PPOTrainer:
                 if self.use_fused:
                     # one launch gathers obs, actions and aux rows and the
                     # advantage partials the head's normalisation needs
-                    K.gather_minibatch(idx, obs_flat, act_flat, self.aux, self.mb_obs,
-                                       self.mb_act, self.mb_aux, adv_part=self.head.adv_part)
+                    self.gather(idx, self.mb_obs, self.mb_act, self.mb_aux,
+                                self.head.adv_part)
                     kw = dict(adv_ready=True, stats_out=stats[j])
                     if self.world > 1:
                         # DP: one all-reduce of the flat gradient, or (2

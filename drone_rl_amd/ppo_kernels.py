@@ -306,6 +306,34 @@ def gather_minibatch(idx, obs, actions, aux, obs_out, actions_out, aux_out, adv_
                                          _s(obs)))
 
 
+RECORD_FLOATS = 32      # DR_RECORD_FLOATS: one 128-B rollout record
+
+
+def pack_rollout_records(obs, actions, logp, adv, ret, records):
+    """records (n, 32) f32: rollout row r as one 128-B record (obs, action,
+    old log-prob, advantage, return; dr_pack_rollout_records), for
+    gather_records."""
+    n, d = obs.shape
+    assert actions.shape == (n, 4) and records.shape == (n, RECORD_FLOATS)
+    assert logp.numel() == adv.numel() == ret.numel() == n and records.is_contiguous()
+    check(_lib.lib().dr_pack_rollout_records(n, d, ptr(_f32(obs)), ptr(_f32(actions)),
+                                             ptr(_f32(logp)), ptr(_f32(adv)), ptr(_f32(ret)),
+                                             ptr(records), _s(obs)))
+
+
+def gather_records(idx, records, obs_dim, obs_out, actions_out, aux_out, adv_part=None):
+    """gather_minibatch's outputs (the same bytes) from the packed records:
+    one cache line per gathered row."""
+    m = idx.numel()
+    assert idx.dtype == torch.int32 and idx.is_contiguous()
+    assert records.shape[1] == RECORD_FLOATS and records.is_contiguous()
+    assert obs_out.shape == (m, obs_dim) and actions_out.shape == (m, 4)
+    assert aux_out.shape == (m, 3)
+    check(_lib.lib().dr_gather_records(m, ptr(idx), obs_dim, ptr(records), ptr(obs_out),
+                                       ptr(actions_out), ptr(aux_out), ptr(adv_part),
+                                       _s(records)))
+
+
 def policy_heads(h_pi, h_vf, w_act, b_act, w_val, b_val, mean, value, preact=False,
                  zb_pi=None, zb_vf=None):
     """mean (m,4) = h_pi w_act^T + b_act, value (m) = h_vf w_val^T + b_val;

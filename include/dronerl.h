@@ -39,7 +39,7 @@
 extern "C" {
 #endif
 
-#define DR_ABI_VERSION 15
+#define DR_ABI_VERSION 16
 
 enum dr_status {
     DR_OK = 0,
@@ -307,6 +307,25 @@ int dr_gather_minibatch(int64_t m, const int32_t *idx, int64_t obs_dim,
                         const float *obs, const float *actions,
                         const float *aux, float *obs_out, float *actions_out,
                         float *aux_out, float *adv_part, void *stream);
+
+/* One-line rollout records (ABI v16, round 6): the PPO.train minibatch
+   gather of RolloutBuffer.get (`self.observations[batch_inds]`,
+   `self.actions[...]`, old log-probs / advantages / returns) reads one
+   aligned 128-B line per row instead of three arrays' lines.
+   dr_pack_rollout_records writes record r (DR_RECORD_FLOATS floats) from
+   rollout row r once per iteration: floats 0 .. obs_dim-1 = obs[r,:],
+   16 .. 19 = actions[r,:], 20 .. 22 = (logp[r], adv[r], ret[r]), the rest 0
+   (obs_dim <= 15; actions and records 16-byte aligned; n rows).
+   dr_gather_records then writes exactly dr_gather_minibatch's outputs
+   (obs_out (m, obs_dim), actions_out (m, 4), aux_out (m, 3), the advantage
+   partials when adv_part is non-null) from the records of rows idx[0..m). */
+#define DR_RECORD_FLOATS 32
+int dr_pack_rollout_records(int64_t n, int64_t obs_dim, const float *obs,
+                            const float *actions, const float *logp, const float *adv,
+                            const float *ret, float *records, void *stream);
+int dr_gather_records(int64_t m, const int32_t *idx, int64_t obs_dim, const float *records,
+                      float *obs_out, float *actions_out, float *aux_out, float *adv_part,
+                      void *stream);
 
 /* Tanh-layer backward fused with the bias gradient (the MLP backward of
    PPO.train): grad_z = grad_h * (1 - h^2) for an (m, n) activation h =

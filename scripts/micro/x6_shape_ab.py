@@ -9,6 +9,7 @@ both weight images (transpose 0 / 1).
   DRONERL_LIB=... python scripts/micro/x6_shape_ab.py [--m 65536] [--warm-s 2]
 """
 import argparse
+import hashlib
 import json
 import os
 import sys
@@ -46,6 +47,7 @@ for tr in (1, 0):
     out[f"rel_err_t{tr}"] = ((C[:, :n].double() - ref).abs() / den).max().item()
     # the full-size output against the f32 bmm (a layout slip shows as O(1))
     out[f"max_abs_vs_f32_t{tr}"] = (C - torch.bmm(A, Wt)).abs().max().item()
+    out[f"sha_t{tr}"] = hashlib.sha256(C.cpu().numpy().tobytes()).hexdigest()[:16]
 t_end = time.perf_counter() + a.warm_s
 while time.perf_counter() < t_end:
     for _ in range(100):

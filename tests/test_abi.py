@@ -41,7 +41,7 @@ def test_library_exports_every_declared_symbol():
 def test_library_loads_and_validates_without_gpu():
     from drone_rl_amd import _lib
     L = _lib.lib()
-    assert L.dr_abi_version() == _lib.ABI_VERSION == 15
+    assert L.dr_abi_version() == _lib.ABI_VERSION == 16
     # argument validation happens before any HIP call
     cfg = _lib.dr_config(num_envs=0)
     h = ctypes.c_void_p()

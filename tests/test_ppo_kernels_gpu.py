@@ -434,6 +434,42 @@ def test_gather_minibatch_ragged_and_runtime_widths(m, d):
     assert torch.equal(o, obs[r]) and torch.equal(a, act[r]) and torch.equal(x, aux[r])
 
 
+@pytest.mark.parametrize("m,d", [(65536, 15), (1, 15), (1025, 12), (4099, 5), (70001, 15)])
+def test_gather_records_is_gather_minibatch(m, d):
+    """The one-line record path (round 6): dr_pack_rollout_records once, then
+    dr_gather_records writes exactly dr_gather_minibatch's bytes -- obs,
+    action and aux rows and the advantage (count, mean, M2) partials -- at
+    full size, ragged row counts and other obs widths; the records hold
+    each row's values at their documented offsets."""
+    from drone_rl_amd import ppo_kernels as K
+    g = torch.Generator(device="cuda").manual_seed(m * 7 + d)
+    total = 2 * m + 3
+    obs = torch.randn(total, d, device="cuda", generator=g)
+    act = torch.rand(total, 4, device="cuda", generator=g) * 7.3575
+    lp, adv, ret = (torch.randn(total, device="cuda", generator=g) for _ in range(3))
+    aux = torch.stack([lp, adv, ret], dim=1)
+    rec = torch.full((total, K.RECORD_FLOATS), float("nan"), device="cuda")
+    K.pack_rollout_records(obs, act, lp, adv, ret, rec)
+    assert torch.equal(rec[:, :d], obs) and torch.equal(rec[:, 16:20], act)
+    assert torch.equal(rec[:, 20:23], aux)
+    assert (rec[:, d:16] == 0).all() and (rec[:, 23:] == 0).all()
+    idx = torch.randperm(total, device="cuda", generator=g)[:m].to(torch.int32)
+    nb = (m + 255) // 256
+    outs = []
+    for use_rec in (False, True):
+        o, a, x = (torch.full((m, w), float("nan"), device="cuda") for w in (d, 4, 3))
+        part = torch.full((3 * nb,), float("nan"), device="cuda")
+        if use_rec:
+            K.gather_records(idx, rec, d, o, a, x, adv_part=part)
+        else:
+            K.gather_minibatch(idx, obs, act, aux, o, a, x, adv_part=part)
+        outs.append((o, a, x, part))
+    for u, v in zip(*outs):
+        assert torch.equal(u, v)
+    r = idx.long()
+    assert torch.equal(outs[1][0], obs[r]) and torch.equal(outs[1][2], aux[r])
+
+
 @pytest.mark.parametrize("arch,m", [((256, 256), 65536), ((64, 64), 1000), ((64, 128), 4096)])
 def test_deferred_finish_equals_separate_finishes(arch, m):
     """FusedTrainStep.step(defer_finish=True) + ClipAdam.step_finish (the
