@@ -575,13 +575,16 @@ __global__ __launch_bounds__(kBlock) void gather_minibatch_kernel(
 // action, 12-B aux), each in its own 128-B lines: 3.7 TCP -> TCC requests per
 // row and 5.1x the algorithmic read bytes (profiles/r05_gather_pmc.json).
 // pack_records_kernel writes every rollout row once per PPO iteration as one
-// aligned 128-B record -- floats 0 .. obs_dim - 1 the obs, 16 .. 19 the
-// action, 20 .. 22 (old log-prob, advantage, return), the rest zero -- and
-// gather_records_kernel reads ONE line per gathered row.
+// aligned 128-B record -- floats 0 .. d - 1 the obs (d = obs_dim <= 24), the
+// action at rec_act_off(d) = 4 ceil(d / 4) (16 for the 15-d drone obs), the
+// (old log-prob, advantage, return) triple right after it, the rest zero --
+// and gather_records_kernel reads ONE line per gathered row.
 constexpr int kRecF = DR_RECORD_FLOATS;          // 32 floats = 128 B
+constexpr int kRecMaxObs = 24;
+__host__ __device__ inline int rec_act_off(int d) { return 4 * ((d + 3) / 4); }
 
-// thread (row, float4 slot s of 8): s 0..3 obs floats 4 s .. 4 s + 3, s 4
-// the action, s 5 the aux triple, s 6..7 zeros; the stores are contiguous
+// thread (row, float4 slot s of 8): slot s holds floats 4 s .. 4 s + 3 of
+// the record; the stores are contiguous
 __global__ __launch_bounds__(kBlock) void pack_records_kernel(
     int64_t n, int obs_dim, const float *__restrict__ obs, const float4 *__restrict__ act,
     const float *__restrict__ logp, const float *__restrict__ adv, const float *__restrict__ ret,
@@ -590,57 +593,69 @@ __global__ __launch_bounds__(kBlock) void pack_records_kernel(
     const int64_t row = t >> 3;
     const int s = (int)(t & 7);
     if (row >= n) return;
+    const int ao = rec_act_off(obs_dim);
     float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (s < 4) {
+    if (4 * s < ao) {
         const float *o = obs + row * obs_dim;
         const int c = 4 * s;
         if (c + 0 < obs_dim) v.x = o[c + 0];
         if (c + 1 < obs_dim) v.y = o[c + 1];
         if (c + 2 < obs_dim) v.z = o[c + 2];
         if (c + 3 < obs_dim) v.w = o[c + 3];
-    } else if (s == 4) {
+    } else if (4 * s == ao) {
         v = act[row];
-    } else if (s == 5) {
+    } else if (4 * s == ao + 4) {
         v = make_float4(logp[row], adv[row], ret[row], 0.f);
     }
     rec[row * (kRecF / 4) + s] = v;
 }
 
 // One thread per gathered row (blocks of 256 rows, as the aux blocks of
-// gather_minibatch_kernel): six 16-B loads of the row's record (one line),
-// the obs rows staged in LDS and written as contiguous float4, the action
-// and aux rows stored directly, and the block's advantage (count, mean, M2)
-// partial -- the same rows, values and reduction order as
+// gather_minibatch_kernel): the record's first ao / 4 + 2 float4 (one
+// line), the obs rows staged in LDS and written as contiguous float4, the
+// action and aux rows stored directly, and the block's advantage (count,
+// mean, M2) partial -- the same rows, values and reduction order as
 // gather_minibatch_kernel, so every output byte is the same.
 __global__ __launch_bounds__(kBlock) void gather_records_kernel(
     int64_t m, int obs_dim, const int32_t *__restrict__ idx, const float4 *__restrict__ rec,
     float *__restrict__ obs_out, float4 *__restrict__ act_out, float *__restrict__ aux_out,
     float *__restrict__ adv_part) {
-    __shared__ float so[kBlock * 15];
+    __shared__ float so[kBlock * kRecMaxObs];
     __shared__ float sh[8];
     const int b = blockIdx.x;
     const int64_t i0 = (int64_t)b * kBlock, i = i0 + threadIdx.x;
     const int cnt = (int)min((int64_t)kBlock, m - i0);
+    const int aq = rec_act_off(obs_dim) / 4;       // the action's float4 slot
     float ai = 0.f;
     if (i < m) {
         const float4 *r = rec + (int64_t)idx[i] * (kRecF / 4);
-        float4 q[6];
+        float4 q[8];
 #pragma unroll
-        for (int s = 0; s < 6; ++s) q[s] = r[s];
-        const float o[16] = {q[0].x, q[0].y, q[0].z, q[0].w, q[1].x, q[1].y, q[1].z, q[1].w,
-                             q[2].x, q[2].y, q[2].z, q[2].w, q[3].x, q[3].y, q[3].z, q[3].w};
+        for (int s = 0; s < 8; ++s)
+            if (s <= aq + 1) q[s] = r[s];
 #pragma unroll
-        for (int k = 0; k < 15; ++k)
-            if (k < obs_dim) so[threadIdx.x * obs_dim + k] = o[k];
-        act_out[i] = q[4];
-        aux_out[3 * i] = q[5].x;
-        aux_out[3 * i + 1] = q[5].y;
-        aux_out[3 * i + 2] = q[5].z;
-        ai = q[5].y;
+        for (int s = 0; s < kRecMaxObs / 4; ++s) {
+            const float o4[4] = {q[s].x, q[s].y, q[s].z, q[s].w};
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+                if (4 * s + e < obs_dim) so[threadIdx.x * obs_dim + 4 * s + e] = o4[e];
+        }
+        float4 a4 = q[0], x4 = q[1];
+#pragma unroll
+        for (int s = 1; s < 7; ++s)
+            if (s == aq) {
+                a4 = q[s];
+                x4 = q[s + 1];
+            }
+        act_out[i] = a4;
+        aux_out[3 * i] = x4.x;
+        aux_out[3 * i + 1] = x4.y;
+        aux_out[3 * i + 2] = x4.z;
+        ai = x4.y;
     }
     __syncthreads();
     // the block's cnt obs rows are cnt * obs_dim contiguous floats starting
-    // at a multiple of 256 * obs_dim (16-byte aligned: obs_out is)
+    // at 256 * obs_dim * b floats (16-byte aligned: obs_out is)
     const int nf = cnt * obs_dim;
     float *dst = obs_out + i0 * obs_dim;
     for (int q = threadIdx.x; q < nf / 4; q += kBlock)
@@ -2078,9 +2093,9 @@ int dr_gather_minibatch(int64_t m, const int32_t *idx, int64_t obs_dim, const fl
 int dr_pack_rollout_records(int64_t n, int64_t obs_dim, const float *obs, const float *actions,
                             const float *logp, const float *adv, const float *ret,
                             float *records, void *stream) {
-    if (n < 0 || obs_dim < 1 || obs_dim > 15 || !obs || !actions || !logp || !adv || !ret ||
-        !records)
-        return fail0(DR_ERR_INVALID, "dr_pack_rollout_records: bad arguments (1 <= obs_dim <= 15)");
+    if (n < 0 || obs_dim < 1 || obs_dim > kRecMaxObs || !obs || !actions || !logp || !adv ||
+        !ret || !records)
+        return fail0(DR_ERR_INVALID, "dr_pack_rollout_records: bad arguments (1 <= obs_dim <= 24)");
     if ((((uintptr_t)actions) | ((uintptr_t)records)) & 15)
         return fail0(DR_ERR_INVALID,
                      "dr_pack_rollout_records: actions and records must be 16-byte aligned");
@@ -2097,9 +2112,9 @@ int dr_pack_rollout_records(int64_t n, int64_t obs_dim, const float *obs, const 
 int dr_gather_records(int64_t m, const int32_t *idx, int64_t obs_dim, const float *records,
                       float *obs_out, float *actions_out, float *aux_out, float *adv_part,
                       void *stream) {
-    if (m < 0 || obs_dim < 1 || obs_dim > 15 || !idx || !records || !obs_out || !actions_out ||
-        !aux_out)
-        return fail0(DR_ERR_INVALID, "dr_gather_records: bad arguments (1 <= obs_dim <= 15)");
+    if (m < 0 || obs_dim < 1 || obs_dim > kRecMaxObs || !idx || !records || !obs_out ||
+        !actions_out || !aux_out)
+        return fail0(DR_ERR_INVALID, "dr_gather_records: bad arguments (1 <= obs_dim <= 24)");
     if ((((uintptr_t)records) | ((uintptr_t)actions_out) | ((uintptr_t)obs_out)) & 15)
         return fail0(DR_ERR_INVALID,
                      "dr_gather_records: records, obs_out and actions_out must be 16-byte aligned");

@@ -313,9 +313,10 @@ int dr_gather_minibatch(int64_t m, const int32_t *idx, int64_t obs_dim,
    `self.actions[...]`, old log-probs / advantages / returns) reads one
    aligned 128-B line per row instead of three arrays' lines.
    dr_pack_rollout_records writes record r (DR_RECORD_FLOATS floats) from
-   rollout row r once per iteration: floats 0 .. obs_dim-1 = obs[r,:],
-   16 .. 19 = actions[r,:], 20 .. 22 = (logp[r], adv[r], ret[r]), the rest 0
-   (obs_dim <= 15; actions and records 16-byte aligned; n rows).
+   rollout row r once per iteration: floats 0 .. obs_dim-1 = obs[r,:], from
+   a = 4 ceil(obs_dim / 4): a .. a+3 = actions[r,:], a+4 .. a+6 = (logp[r],
+   adv[r], ret[r]), the rest 0 (obs_dim <= 24: 16 / 20 for the 15-d gym and
+   18-d moving obs; actions and records 16-byte aligned; n rows).
    dr_gather_records then writes exactly dr_gather_minibatch's outputs
    (obs_out (m, obs_dim), actions_out (m, 4), aux_out (m, 3), the advantage
    partials when adv_part is non-null) from the records of rows idx[0..m). */

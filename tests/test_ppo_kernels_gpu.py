@@ -434,7 +434,8 @@ def test_gather_minibatch_ragged_and_runtime_widths(m, d):
     assert torch.equal(o, obs[r]) and torch.equal(a, act[r]) and torch.equal(x, aux[r])
 
 
-@pytest.mark.parametrize("m,d", [(65536, 15), (1, 15), (1025, 12), (4099, 5), (70001, 15)])
+@pytest.mark.parametrize("m,d", [(65536, 15), (1, 15), (1025, 12), (4099, 5), (70001, 18),
+                                 (300, 24)])
 def test_gather_records_is_gather_minibatch(m, d):
     """The one-line record path (round 6): dr_pack_rollout_records once, then
     dr_gather_records writes exactly dr_gather_minibatch's bytes -- obs,
@@ -450,9 +451,10 @@ def test_gather_records_is_gather_minibatch(m, d):
     aux = torch.stack([lp, adv, ret], dim=1)
     rec = torch.full((total, K.RECORD_FLOATS), float("nan"), device="cuda")
     K.pack_rollout_records(obs, act, lp, adv, ret, rec)
-    assert torch.equal(rec[:, :d], obs) and torch.equal(rec[:, 16:20], act)
-    assert torch.equal(rec[:, 20:23], aux)
-    assert (rec[:, d:16] == 0).all() and (rec[:, 23:] == 0).all()
+    ao = 4 * ((d + 3) // 4)
+    assert torch.equal(rec[:, :d], obs) and torch.equal(rec[:, ao:ao + 4], act)
+    assert torch.equal(rec[:, ao + 4:ao + 7], aux)
+    assert (rec[:, d:ao] == 0).all() and (rec[:, ao + 7:] == 0).all()
     idx = torch.randperm(total, device="cuda", generator=g)[:m].to(torch.int32)
     nb = (m + 255) // 256
     outs = []
