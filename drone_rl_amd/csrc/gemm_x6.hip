@@ -889,6 +889,161 @@ __global__ __launch_bounds__(XTHREADS) void gemm_x6_wgrad_kernel(
         }
 }
 
+#if X6_MFMA16
+// ---------------------------------------------------------------------------
+// gemm_x6_wgrad16_kernel (round 6, X6_MFMA16): gemm_x6_wgrad_kernel on
+// v_mfma_f32_16x16x32_bf16.  A stage's 32 rows are ONE k32 step: each wave's
+// 64 x 64 outputs are 4 x 4 tiles of 16 x 16 (the same 128 accumulator
+// registers), 96 MFMAs of 16 cycles per stage (the same 1,536 pipe cycles).
+// Fragments come from the same row-major plane image through two
+// transposed reads each; K (the rows) is permuted so the two reads of a
+// 32-lane half cover 8 distinct rows: A/B lane L = i + 16 g holds column i
+// of rows 4 g + e (e < 4) and 16 + 4 g + e - 4 (e >= 4) -- the same
+// permutation in both operands, so the products are the same.  The row
+// stride is 2,336 B (== 32 mod 256): rows 0..7 of a half fall in distinct
+// 8-bank groups, conflict-free.
+constexpr int TW16_ROW = 3 * TW_PLANE_ROW + 32;    // 2,336 B
+constexpr int TW16_STAGE = TW_BM * TW16_ROW;       // 74,752 B
+constexpr int TW16_LDS = 2 * TW16_STAGE;           // 149,504 B
+
+__device__ inline bf16x8_t tr16_frag(const uint8_t *p) {
+    typedef __attribute__((address_space(3))) i16x4_t lds_i16x4;
+    const i16x4_t a = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+        (lds_i16x4 *)(uintptr_t)lds_addr(p));
+    const i16x4_t c = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+        (lds_i16x4 *)(uintptr_t)lds_addr(p + 16 * TW16_ROW));
+    return __builtin_bit_cast(bf16x8_t, __builtin_shufflevector(a, c, 0, 1, 2, 3, 4, 5, 6, 7));
+}
+
+__global__ __launch_bounds__(XTHREADS) void gemm_x6_wgrad16_kernel(
+    const float *__restrict__ Gm, const float *__restrict__ Hm, float *__restrict__ ws,
+    int64_t m, int chunks) {
+    __shared__ __attribute__((aligned(16))) uint8_t sh[TW16_LDS];
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wn = wid >> 2, wk = wid & 3;
+    const int chunk = (int)(blockIdx.x % chunks);
+    const int nh = (int)((blockIdx.x / chunks) & 1);
+    const int b = (int)(blockIdx.x / chunks / 2);
+    const int64_t rows = m / chunks;
+    const int G_ = (int)(rows / TW_BM);
+    const float *Gb = Gm + ((int64_t)b * m + (int64_t)chunk * rows) * 256 + nh * 128;
+    const float *Hb = Hm + ((int64_t)b * m + (int64_t)chunk * rows) * 256;
+
+    int ld_src[6], ld_dst[6];
+#pragma unroll
+    for (int i = 0; i < 6; ++i) {
+        const int q = tid + 512 * (i < 2 ? i : i - 2);
+        const int r = i < 2 ? q >> 5 : q >> 6;
+        const int c = i < 2 ? (q & 31) * 4 : (q & 63) * 4;
+        ld_src[i] = r * 256 + c;
+        ld_dst[i] = r * TW16_ROW + (i < 2 ? c : 128 + c) * 2;
+    }
+    f32x4_t ld[6];
+    auto load = [&](int g) {
+        const int64_t r0 = (int64_t)g * TW_BM * 256;
+#pragma unroll
+        for (int i = 0; i < 6; ++i)
+            ld[i] = *reinterpret_cast<const f32x4_t *>((i < 2 ? Gb : Hb) + r0 + ld_src[i]);
+    };
+    auto split_store = [&](int buf) {
+        uint8_t *S = sh + buf * TW16_STAGE;
+#pragma unroll
+        for (int i = 0; i < 6; ++i) {
+            const f32x4_t x = ld[i];
+            uint32_t h[2], mm[2], l[2];
+#pragma unroll
+            for (int q = 0; q < 2; ++q) {
+                const float a = x[2 * q], c = x[2 * q + 1];
+                const uint32_t ph = pk_bf16(a, c);
+                const float ra = a - lo_f(ph), rc = c - hi_f(ph);
+                const uint32_t pm = pk_bf16(ra, rc);
+                h[q] = ph;
+                mm[q] = pm;
+                l[q] = pk_bf16(ra - lo_f(pm), rc - hi_f(pm));
+            }
+            uint8_t *d = S + ld_dst[i];
+            *reinterpret_cast<uint2 *>(d) = make_uint2(h[0], h[1]);
+            *reinterpret_cast<uint2 *>(d + TW_PLANE_ROW) = make_uint2(mm[0], mm[1]);
+            *reinterpret_cast<uint2 *>(d + 2 * TW_PLANE_ROW) = make_uint2(l[0], l[1]);
+        }
+    };
+    // transposed-read lane address (T10): lane 4 q + p of 16-lane group g
+    // supplies row 4 g + q, columns 4 p .. 4 p + 3 of the tile's 16 columns
+    const int li = lane & 15, gq = lane >> 4;
+    const int fbase = (4 * gq + (li >> 2)) * TW16_ROW + 8 * (li & 3);
+    const int gcol = (wn * 64) * 2, hcol = (128 + wk * 64) * 2;
+
+    f32x4_t acc_h[4][4], acc_l[4][4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc_h[i][j] = acc_l[i][j] = (f32x4_t){};
+
+    // the stage's fragments: G tile i (columns wn 64 + 16 i ..), H tile j
+    auto read_g = [&](int g, int i, bf16x8_t (&f)[3]) {
+        const uint8_t *S = sh + (g & 1) * TW16_STAGE + fbase + gcol + 32 * i;
+#pragma unroll
+        for (int p = 0; p < 3; ++p) f[p] = tr16_frag(S + p * TW_PLANE_ROW);
+    };
+    auto read_h = [&](int g, int j, bf16x8_t (&f)[3]) {
+        const uint8_t *S = sh + (g & 1) * TW16_STAGE + fbase + hcol + 32 * j;
+#pragma unroll
+        for (int p = 0; p < 3; ++p) f[p] = tr16_frag(S + p * TW_PLANE_ROW);
+    };
+    auto mfma6 = [&](int i, int j, const bf16x8_t (&a)[3], const bf16x8_t (&c)[3]) {
+        acc_h[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], c[0], acc_h[i][j], 0, 0, 0);
+        f32x4_t t = acc_l[i][j];
+        t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], c[1], t, 0, 0, 0);
+        t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[1], c[0], t, 0, 0, 0);
+        t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], c[2], t, 0, 0, 0);
+        t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[2], c[0], t, 0, 0, 0);
+        t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[1], c[1], t, 0, 0, 0);
+        acc_l[i][j] = t;
+    };
+
+    load(0);
+    split_store(0);
+    load(G_ > 1 ? 1 : 0);
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    // Stage g, per wave: the G fragments of its 4 tiles, then per H tile
+    // j its fragments and the 4 x 6 MFMAs of column j (the next tile's
+    // reads behind them), the split of stage g + 1 after the second H tile,
+    // lgkmcnt(0) + barrier at the end, the loads of stage g + 2 behind the
+    // split.  The last iteration re-splits the last stage (no branch).
+    bf16x8_t fg[4][3], fh[2][3];
+    for (int g = 0; g < G_; ++g) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) read_g(g, i, fg[i]);
+        read_h(g, 0, fh[0]);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            if (j + 1 < 4) read_h(g, j + 1, fh[(j + 1) & 1]);
+#pragma unroll
+            for (int i = 0; i < 4; ++i) mfma6(i, j, fg[i], fh[j & 1]);
+            if (j == 1) {
+                split_store((g + 1) & 1);
+                load(g + 2 < G_ ? g + 2 : G_ - 1);
+            }
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    }
+    // D[n][k] of tile (i, j): column k = 16 j + (lane & 15), row n =
+    // 16 i + 4 (lane >> 4) + r
+    const int fc = lane & 15, fq = lane >> 4;
+    float *out = ws + ((int64_t)b * chunks + chunk) * 256 * 256 + (int64_t)(nh * 128) * 256;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const f32x4_t v = acc_h[i][j] + acc_l[i][j];
+            float *c = out + (int64_t)(wn * 64 + 16 * i + 4 * fq) * 256 + wk * 64 + 16 * j + fc;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) c[r * 256] = v[r];
+        }
+}
+#endif  // X6_MFMA16
+
 // ---------------------------------------------------------------------------
 // dr_gemm_x6_bwd_first (round 5): the 256 x 256 layer's input gradient with
 // the first layer's backward fused into its epilogue.  The unfused step wrote
@@ -925,6 +1080,292 @@ __global__ __launch_bounds__(256) void split_x_kernel(const float *__restrict__ 
     split_x_item(x, nullptr, m, k, img, (int64_t)blockIdx.x * 256 + threadIdx.x);
 }
 
+#if X6_MFMA16
+// ---------------------------------------------------------------------------
+// gemm_x6_fl16_kernel (round 6, X6_MFMA16): gemm_x6_fl_kernel on
+// v_mfma_f32_16x16x32_bf16.  Phase t of a row step runs the wave's column
+// tiles 2 t, 2 t + 1 (16 columns each) for both 16-row tiles -- per k32
+// step 2 row tiles x 2 column tiles x 6 products = 24 MFMAs, the same 192
+// per phase and 6,144 pipe cycles per row step as gemm_x6_fl_kernel -- and
+// the epilogue of the other phase's four tiles.  The l plane of the weights
+// is streamed from L2 as before (two 1-KB fragments per k32 step).
+//
+// D2 = X^T grad_z1 runs on the same shape with K = the row step's 32 rows:
+// the B fragment of column tile ct is registers 0..3 of row tile 0's
+// accumulator and 0..3 of row tile 1's (K index 8 q + e <-> row 4 q + e and
+// 16 + 4 q + e - 4, q = lane >> 4), the A fragment is the record of
+// x6_split.h (X6_MFMA16 split_x_item), so no lane ever holds a zero half:
+// 12 MFMAs of 16 cycles per phase against 12 of 32 in gemm_x6_fl_kernel.
+__global__ __launch_bounds__(WS_THREADS, 1) void gemm_x6_fl16_kernel(
+    const float *__restrict__ A, const uint8_t *__restrict__ img, const float *__restrict__ H,
+    const uint8_t *__restrict__ ximg, float *__restrict__ part, int64_t m, int batch) {
+    __shared__ __attribute__((aligned(16))) uint8_t sh[2 * WS_PSTAGE];
+    const int lane = threadIdx.x & 63;
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int b = (int)blockIdx.x % batch;
+    const int per = (int)gridDim.x / batch;
+    const int j0 = (int)blockIdx.x / batch;
+    const int steps_net = (int)(m / WS_RS);
+    const int R = (steps_net - j0 + per - 1) / per;
+    const float *Ab = A + (int64_t)b * m * XK;
+    const float *Hb = H + (int64_t)b * m * XN;
+    const int fc = lane & 15, fq = lane >> 4;
+
+    constexpr int kBufFlags = 0x00020000;
+    const __amdgpu_buffer_rsrc_t wrs =
+        __builtin_amdgcn_make_buffer_rsrc((void *)(img + (int64_t)b * W_IMG), 0, (int)W_IMG,
+                                          kBufFlags);
+    const int lane16 = lane * 16;
+    auto wfrag = [&](int ct, int s, int p) {
+        return __builtin_bit_cast(
+            bf16x8_t, __builtin_amdgcn_raw_buffer_load_b128(
+                          wrs, lane16, (((w * 4 + ct) * 8 + s) * 3 + p) * W_FRAG, 0));
+    };
+    // the weights' h and m planes in AGPRs (the X6_MFMA16 image order)
+    bf16x8_t Wa[4][8][2];
+#pragma unroll
+    for (int ct = 0; ct < 4; ++ct)
+#pragma unroll
+        for (int s = 0; s < 8; ++s) {
+            Wa[ct][s][0] = wfrag(ct, s, 0);
+            Wa[ct][s][1] = wfrag(ct, s, 1);
+        }
+    // the l plane: fragment u of a row step (k32 step g = u >> 1 of the row
+    // step's 16, g = 8 t + s, column tile 2 t + (u & 1)), loaded WLA ahead
+    auto wl_load = [&](int u) {
+        const int g = (u >> 1) & 15;
+        return wfrag(2 * (g >> 3) + (u & 1), g & 7, 2);
+    };
+    constexpr int WLA = 6, WLR = 8;
+    bf16x8_t wl[WLR];
+#pragma unroll
+    for (int u = 0; u < WLA; ++u) wl[u] = wl_load(u);
+
+    // activation staging and split: gemm_x6_fl_kernel's
+    const int sr = lane & 7, sch = lane >> 3, sodd = sch & 1;
+    const int soff[2] = {sr * 1024 + 32 * sch + 16 * sodd, sr * 1024 + 32 * sch + 16 * (sodd ^ 1)};
+    auto stage_load = [&](int k, int q) {
+        const int kk = k < R ? k : R - 1;
+        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+            (void *)(Ab + ((int64_t)(j0 + kk * per) * WS_RS + 8 * w) * XK), 0, 8 * XK * 4,
+            kBufFlags);
+        return __builtin_bit_cast(
+            float4, __builtin_amdgcn_raw_buffer_load_b128(rs, soff[q & 1], 256 * (q >> 1), 0));
+    };
+    const int wr_base = sch * 512 + (8 * w + sr) * 16;
+    const int wr_half[2] = {wr_base + 8 * sodd, wr_base + 8 * (sodd ^ 1)};
+    auto split_store = [&](int k, int q, const float4 &v) {
+        uint32_t h[2], mm[2], l[2];
+        const float x[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int p = 0; p < 2; ++p) {
+            const float a = x[2 * p], c = x[2 * p + 1];
+            const uint32_t ph = pk_bf16(a, c);
+            const float ra = a - lo_f(ph), rc = c - hi_f(ph);
+            const uint32_t pm = pk_bf16(ra, rc);
+            h[p] = ph;
+            mm[p] = pm;
+            l[p] = pk_bf16(ra - lo_f(pm), rc - hi_f(pm));
+        }
+        uint8_t *dst = sh + (k & 1) * WS_PSTAGE + wr_half[q & 1] + (q >> 1) * 8 * 512;
+        typedef uint32_t u32x2_t __attribute__((ext_vector_type(2)));
+        *reinterpret_cast<u32x2_t *>(dst) = (u32x2_t){h[0], h[1]};
+        *reinterpret_cast<u32x2_t *>(dst + WS_PLANE) = (u32x2_t){mm[0], mm[1]};
+        *reinterpret_cast<u32x2_t *>(dst + 2 * WS_PLANE) = (u32x2_t){l[0], l[1]};
+    };
+    // A fragments of k32 step s for both row tiles (gemm_x6_ws16_kernel's
+    // addressing): row 16 rt + fc, chunk 4 s + fq
+    typedef bf16x8_t AFrag[2][3];
+    const int fr_base = fq * 512 + fc * 16;
+    auto read_frag = [&](int k, int s, AFrag &f) {
+        const uint8_t *src = sh + (k & 1) * WS_PSTAGE + fr_base + s * 2048;
+#pragma unroll
+        for (int rt = 0; rt < 2; ++rt)
+#pragma unroll
+            for (int p = 0; p < 3; ++p)
+                f[rt][p] = *reinterpret_cast<const bf16x8_t *>(src + rt * 256 + p * WS_PLANE);
+    };
+    // accumulators [phase][row tile][column tile of the phase]
+    f32x4_t acc_h[2][2][2], acc_l[2][2][2];
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int rt = 0; rt < 2; ++rt)
+#pragma unroll
+            for (int j = 0; j < 2; ++j) acc_h[t][rt][j] = acc_l[t][rt][j] = (f32x4_t){};
+    auto finish_tiles = [&](int t) {
+        asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7"
+                     : "+v"(acc_h[t][0][0]), "+v"(acc_h[t][0][1]), "+v"(acc_h[t][1][0]),
+                       "+v"(acc_h[t][1][1]), "+v"(acc_l[t][0][0]), "+v"(acc_l[t][0][1]),
+                       "+v"(acc_l[t][1][0]), "+v"(acc_l[t][1][1])::"memory");
+#pragma unroll
+        for (int rt = 0; rt < 2; ++rt)
+#pragma unroll
+            for (int j = 0; j < 2; ++j) acc_h[t][rt][j] = acc_h[t][rt][j] + acc_l[t][rt][j];
+    };
+    // the six products of k32 step s for phase t's 2 x 2 tiles, interleaved
+    // over the tiles (per output gemm_x6_ws16_kernel's order)
+    auto mfma_group = [&](bool first, int t, int s, const AFrag &x, const bf16x8_t &wl0,
+                          const bf16x8_t &wl1) {
+#pragma unroll
+        for (int rt = 0; rt < 2; ++rt)
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                if (first) mfma16_first(acc_h[t][rt][j], x[rt][0], Wa[2 * t + j][s][0]);
+                else mfma16_a(acc_h[t][rt][j], x[rt][0], Wa[2 * t + j][s][0]);
+            }
+#pragma unroll
+        for (int rt = 0; rt < 2; ++rt)
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                if (first) mfma16_first(acc_l[t][rt][j], x[rt][0], Wa[2 * t + j][s][1]);
+                else mfma16_a(acc_l[t][rt][j], x[rt][0], Wa[2 * t + j][s][1]);
+            }
+#pragma unroll
+        for (int rt = 0; rt < 2; ++rt)
+#pragma unroll
+            for (int j = 0; j < 2; ++j) mfma16_a(acc_l[t][rt][j], x[rt][1], Wa[2 * t + j][s][0]);
+#pragma unroll
+        for (int rt = 0; rt < 2; ++rt)
+#pragma unroll
+            for (int j = 0; j < 2; ++j) mfma16_v(acc_l[t][rt][j], x[rt][0], j ? wl1 : wl0);
+#pragma unroll
+        for (int rt = 0; rt < 2; ++rt)
+#pragma unroll
+            for (int j = 0; j < 2; ++j) mfma16_a(acc_l[t][rt][j], x[rt][2], Wa[2 * t + j][s][0]);
+#pragma unroll
+        for (int rt = 0; rt < 2; ++rt)
+#pragma unroll
+            for (int j = 0; j < 2; ++j) mfma16_a(acc_l[t][rt][j], x[rt][1], Wa[2 * t + j][s][1]);
+    };
+
+    // ---- the epilogue: grad_z1 of phase tt's tiles of row step kk into D2
+    f32x4_t d2[4];
+#pragma unroll
+    for (int ct = 0; ct < 4; ++ct) d2[ct] = (f32x4_t){};
+    // h1 of (row tile rt, column tile j of phase tt, register r): row
+    // 16 rt + 4 fq + r, column 64 w + 16 (2 tt + j) + fc
+    float hb[2][2][4];
+    const int hoff = (4 * fq * XN + 64 * w + fc) * 4;
+    auto h_load = [&](int kk, int tt, int i) {
+        const int rt = i >> 3, j = (i >> 2) & 1, r = i & 3;
+        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+            (void *)(Hb + (int64_t)(j0 + kk * per) * WS_RS * XN), 0, WS_RS * XN * 4, kBufFlags);
+        hb[rt][j][r] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(
+            rs, hoff, ((16 * rt + r) * XN + 16 * (2 * tt + j)) * 4, 0));
+    };
+    const int xoff = xrec_off(0, lane);
+    auto x_frag = [&](int kk, bf16x8_t (&xf)[3]) {
+        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+            (void *)(ximg + (int64_t)(j0 + kk * per) * XREC), 0, XREC, kBufFlags);
+#pragma unroll
+        for (int p = 0; p < 3; ++p)
+            xf[p] = __builtin_bit_cast(bf16x8_t, __builtin_amdgcn_raw_buffer_load_b128(
+                                                     rs, xoff, p * 1024, 0));
+    };
+    // grad_z1 = grad_h1 (1 - h1^2) of phase tt's column tile j (both row
+    // tiles: the B fragment's 8 K values), split, and the six products
+    auto d2_tile = [&](int tt, int j, const bf16x8_t (&xf)[3]) {
+        float gz[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+            const float y = hb[e >> 2][j][e & 3];
+            gz[e] = acc_h[tt][e >> 2][j][e & 3] * (1.0f - y * y);
+        }
+        u32x4_t gh, gm, gl;
+        split8(gz, gh, gm, gl);
+        const bf16x8_t bh = __builtin_bit_cast(bf16x8_t, gh);
+        const bf16x8_t bm = __builtin_bit_cast(bf16x8_t, gm);
+        const bf16x8_t bl = __builtin_bit_cast(bf16x8_t, gl);
+        f32x4_t &d = d2[2 * tt + j];
+        // one asm statement (gemm_x6_fl_kernel's D2 order); s_nop 4 covers
+        // the VALU writes of bh, bm, bl -> SrcB reads
+        asm volatile("s_nop 4\n\t"
+                     "v_mfma_f32_16x16x32_bf16 %0, %1, %4, %0\n\t"
+                     "v_mfma_f32_16x16x32_bf16 %0, %1, %5, %0\n\t"
+                     "v_mfma_f32_16x16x32_bf16 %0, %2, %4, %0\n\t"
+                     "v_mfma_f32_16x16x32_bf16 %0, %1, %6, %0\n\t"
+                     "v_mfma_f32_16x16x32_bf16 %0, %3, %4, %0\n\t"
+                     "v_mfma_f32_16x16x32_bf16 %0, %2, %5, %0"
+                     : "+v"(d)
+                     : "v"(xf[0]), "v"(xf[1]), "v"(xf[2]), "v"(bh), "v"(bm), "v"(bl));
+    };
+
+    // ---- prologue: step 0's planes, the staging ring for step 1 ----
+    {
+        float4 v0[8];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) v0[q] = stage_load(0, q);
+#pragma unroll
+        for (int q = 0; q < 8; ++q) split_store(0, q, v0[q]);
+    }
+    float4 stg[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) stg[q] = stage_load(1, q);
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    AFrag fb[2];
+    read_frag(0, 0, fb[0]);
+    bf16x8_t xf[3];
+
+    // Row step k, per wave: phase t = column tiles 2 t, 2 t + 1 over the 8
+    // k32 steps (24 MFMAs each) and the epilogue of phase tt = 1 - t's
+    // tiles (row step k - 1 in phase 0, k in phase 1): h1 loads at k32
+    // steps 0..3 (four each), the X fragment at 1, D2 of tile 0 at 5 and of
+    // tile 1 at 7; A fragments one k32 step ahead; split half-unit q = 4 t +
+    // (s >> 1) of step k + 1 at odd s, with the staging load of q + 4 behind
+    // it.  Step 0's phase-0 epilogue is of the zeroed phase-1 tiles: D2 += 0.
+    auto row_step = [&](int k) {
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+            const int tt = 1 - t;
+            const int kk = t == 0 ? (k > 0 ? k - 1 : 0) : k;
+            finish_tiles(tt);
+#pragma unroll
+            for (int s = 0; s < 8; ++s) {
+                const int g = 8 * t + s;
+                if (g + 1 < 16) read_frag(k, (g + 1) & 7, fb[(g + 1) & 1]);
+                wl[(2 * g + WLA) % WLR] = wl_load(2 * g + WLA);
+                wl[(2 * g + 1 + WLA) % WLR] = wl_load(2 * g + 1 + WLA);
+                mfma_group(s == 0, t, s, fb[g & 1], wl[(2 * g) % WLR], wl[(2 * g + 1) % WLR]);
+                if (s < 4) {
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) h_load(kk, tt, 4 * s + i);
+                }
+                if (s == 1) x_frag(kk, xf);
+                if (s == 5) d2_tile(tt, 0, xf);
+                if (s == 7) d2_tile(tt, 1, xf);
+                if (s & 1) {
+                    const int q = 4 * t + (s >> 1);
+                    split_store(k + 1, q, stg[q & 3]);
+                    stg[q & 3] = stage_load(q + 4 < 8 ? k + 1 : k + 2, (q + 4) & 7);
+                }
+            }
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        read_frag(k + 1, 0, fb[0]);
+    };
+    for (int k = 0; k < R; ++k) row_step(k);
+    // phase 1's tiles of the last row step
+    if (R > 0) {
+        finish_tiles(1);
+#pragma unroll
+        for (int i = 0; i < 16; ++i) h_load(R - 1, 1, i);
+        x_frag(R - 1, xf);
+        d2_tile(1, 0, xf);
+        d2_tile(1, 1, xf);
+    }
+    // D2 -> this block's partial row (first_layer_bwd_kernel's layout:
+    // [feature * 256 + column], row j0 * batch + b): tile ct, lane (fc, fq),
+    // register r = feature 4 fq + r, column 64 w + 16 ct + fc
+    float *out = part + ((int64_t)j0 * batch + b) * (FL_F * XN);
+    asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7"
+                 : "+v"(d2[0]), "+v"(d2[1]), "+v"(d2[2]), "+v"(d2[3])::"memory");
+#pragma unroll
+    for (int ct = 0; ct < 4; ++ct)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) out[(4 * fq + r) * XN + 64 * w + 16 * ct + fc] = d2[ct][r];
+}
+#else
 __global__ __launch_bounds__(WS_THREADS, 1) void gemm_x6_fl_kernel(
     const float *__restrict__ A, const uint8_t *__restrict__ img, const float *__restrict__ H,
     const uint8_t *__restrict__ ximg, float *__restrict__ part, int64_t m, int batch) {
@@ -1184,6 +1625,7 @@ __global__ __launch_bounds__(WS_THREADS, 1) void gemm_x6_fl_kernel(
         out[(mrow & 15) * XN + 64 * w + 32 * (mrow >> 4) + fr] = d2[r];
     }
 }
+#endif  // X6_MFMA16
 
 int fail_g(int code, const std::string &msg) {
     set_global_error(msg);
@@ -1217,7 +1659,12 @@ int gemm_x6_fl_rows(int batch, int64_t m) {
 int gemm_x6_fl_launch(int batch, int64_t m, const float *gz, const void *img, const float *h,
                       const void *ximg, float *part, hipStream_t st) {
     const int grid = gemm_x6_fl_rows(batch, m) * batch;
-    hipLaunchKernelGGL(gemm_x6_fl_kernel, dim3(grid), dim3(WS_THREADS), 0, st, gz,
+#if X6_MFMA16
+    constexpr auto fl_kernel = gemm_x6_fl16_kernel;
+#else
+    constexpr auto fl_kernel = gemm_x6_fl_kernel;
+#endif
+    hipLaunchKernelGGL(fl_kernel, dim3(grid), dim3(WS_THREADS), 0, st, gz,
                        static_cast<const uint8_t *>(img), h, static_cast<const uint8_t *>(ximg),
                        part, m, batch);
     return hipGetLastError() == hipSuccess ? grid / batch : -1;
@@ -1283,7 +1730,12 @@ int dr_gemm_x6_wgrad(int64_t batch, int64_t m, int64_t chunks, const float *g, c
         return fail_g(DR_ERR_INVALID,
                       "dr_gemm_x6_wgrad: bad arguments (m / chunks a positive multiple of 32; "
                       "pointers 16-byte aligned)");
-    hipLaunchKernelGGL(gemm_x6_wgrad_kernel, dim3((unsigned)(batch * 2 * chunks)),
+#if X6_MFMA16
+    constexpr auto wgrad_kernel = gemm_x6_wgrad16_kernel;
+#else
+    constexpr auto wgrad_kernel = gemm_x6_wgrad_kernel;
+#endif
+    hipLaunchKernelGGL(wgrad_kernel, dim3((unsigned)(batch * 2 * chunks)),
                        dim3(XTHREADS), 0, static_cast<hipStream_t>(stream), g, h, ws, m,
                        (int)chunks);
     const hipError_t e = hipGetLastError();

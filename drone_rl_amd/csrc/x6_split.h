@@ -98,8 +98,37 @@ __device__ inline void split_weights_item(const float *__restrict__ w, int trans
 }
 
 // The first-layer observation image of the fused input-gradient GEMM
-// (gemm_x6_fl_kernel): per row step a 3,136-B record of X^T's A fragments.
+// (gemm_x6_fl_kernel): per row step a record of X^T's A fragments.
 constexpr int FL_F = 16;                                // 15 features + the bias column
+#if X6_MFMA16
+// X6_MFMA16 (gemm_x6_fl16_kernel): one v_mfma_f32_16x16x32_bf16 A fragment
+// per plane and row step, K = the step's 32 rows: lane L = f + 16 q holds
+// feature f of rows 4 q + e (e < 4, row tile 0) and 16 + 4 q + e - 4 (e >= 4,
+// row tile 1) -- the rows the main GEMM's 16 x 16 accumulators of the two
+// row tiles hold in lane (column, q), registers e & 3.
+constexpr int XREC = 3 * 64 * 16;                       // 3,072 B per row step
+__host__ __device__ inline int xrec_off(int p, int lane) { return (p * 64 + lane) * 16; }
+
+__device__ inline void split_x_item(const float *__restrict__ x, const int32_t *__restrict__ rows,
+                                    int64_t m, int k, uint8_t *__restrict__ img, int64_t t) {
+    const int64_t g = t >> 6;
+    if (g >= m / X6_RS) return;
+    const int L = (int)(t & 63), f = L & 15, q = L >> 4;
+    uint8_t *rec = img + g * XREC;
+    float v[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+        const int64_t row = g * X6_RS + (e < 4 ? 4 * q + e : 16 + 4 * q + (e - 4));
+        const int64_t src = rows ? (int64_t)rows[row] : row;
+        v[e] = f < k ? x[src * k + f] : (f == FL_F - 1 ? 1.0f : 0.0f);
+    }
+    u32x4_t h, mm, l;
+    split8(v, h, mm, l);
+    *reinterpret_cast<u32x4_t *>(rec + xrec_off(0, L)) = h;
+    *reinterpret_cast<u32x4_t *>(rec + xrec_off(1, L)) = mm;
+    *reinterpret_cast<u32x4_t *>(rec + xrec_off(2, L)) = l;
+}
+#else
 constexpr int XREC = 64 + 3 * 2 * 2 * FL_F * 16;         // 3,136 B of X planes per row step
 
 // byte offset in a row step's X record of plane p, K step j, half fh,
@@ -133,5 +162,6 @@ __device__ inline void split_x_item(const float *__restrict__ x, const int32_t *
     *reinterpret_cast<u32x4_t *>(rec + xrec_off(1, j, fh, f)) = mm;
     *reinterpret_cast<u32x4_t *>(rec + xrec_off(2, j, fh, f)) = l;
 }
+#endif
 
 }  // namespace dr
