@@ -754,9 +754,10 @@ def ppo_kernel_times(tr, reps=20):
 PPO_KERNEL_NAMES = {"gather_minibatch": "gather_records_kernel",
                     "linear_tanh": "linear_tanh_kernel", "ppo_head": "ppo_head_kernel",
                     "first_layer_bwd": "first_layer_bwd_kernel",
-                    "gemm_x6_fwd": "gemm_x6_ws_kernel", "gemm_x6_bwd": "gemm_x6_ws_kernel",
-                    "gemm_x6_wgrad": "gemm_x6_wgrad_kernel", "split_weights": "split_weights_kernel",
-                    "split_x": "split_x_kernel", "gemm_x6_bwd_first": "gemm_x6_fl_kernel"}
+                    "gemm_x6_fwd": "gemm_x6_ws16_kernel", "gemm_x6_bwd": "gemm_x6_ws16_kernel",
+                    "gemm_x6_wgrad": "gemm_x6_wgrad16_kernel",
+                    "split_weights": "split_weights_kernel", "split_x": "split_x_kernel",
+                    "gemm_x6_bwd_first": "gemm_x6_fl16_kernel"}
 
 
 def rollout_rocprof_k32(path, n, state_dtype):

@@ -3,7 +3,7 @@
 //
 // gfx950 has no xf32 MFMA and its f32-input MFMA runs at 1/16 of the bf16
 // rate, so the hipBLASLt fp32 GEMMs of the 256 x 256 layer cap at 157 TF/s.
-// This kernel keeps fp32 accuracy on the bf16 MFMA instead:
+// These kernels keep fp32 accuracy on the bf16 MFMA instead:
 //
 //   * every fp32 operand x is split EXACTLY into three bf16 planes,
 //     x = h + m + l (8 + 8 + 8 significant bits, RNE at each level: x - h
@@ -20,12 +20,21 @@
 // accurate than the f32 MFMA chain (tests/test_gemm_x6_gpu.py), at 6 bf16
 // MFMAs per product: 2.67x the f32 MFMA rate in peak terms.
 //
+// Every kernel runs on v_mfma_f32_16x16x32_bf16 (round 6).  The chip holds
+// its clock down under these MFMA-dense loops (DVFS give-back), and at equal
+// cycles per FLOP the 16x16x32 shape holds a higher clock than 32x32x16
+// (MI355X_MICROARCH.md, DVFS give-back item 7); same-box A/B against the
+// round-5 32x32x16 kernels (profiles/r06_x6_shape_ab*.json): forward 82-84
+// vs 85-86 us, the fused input gradient 113 vs 120 us, PPO 7.64-7.65 vs
+// 7.41-7.43 updates/s.
+//
 // Shape: C[b] = A[b] . B[b]^T, b < batch (the pi and vf MLPs), A (m, 256) f32
 // row-major, B given as a pre-split image (dr_gemm_x6_split_weights: the
 // layer weight W for the forward z = h W^T, or W^T for grad_h = grad_z W),
-// C (m, 256) f32: gemm_x6_ws_kernel, weight-stationary (the weights in
+// C (m, 256) f32: gemm_x6_ws16_kernel, weight-stationary (the weights in
 // registers, A streamed once); the weight gradient dW = G^T H by
-// gemm_x6_wgrad_kernel (split-K over row chunks).
+// gemm_x6_wgrad16_kernel (split-K over row chunks); the input gradient with
+// the first layer's backward in its epilogue by gemm_x6_fl16_kernel.
 //
 // Reference: the MLP layers of SB3's ActorCriticPolicy (MlpExtractor,
 // net_arch [256, 256], /root/reference/train.py:36-43) -- torch fp32 Linear.
@@ -37,7 +46,7 @@
 #include "x6_split.h"
 
 #pragma clang fp contract(off)
-// glds16 clobbers m0 (reserved: the compiler sets it before each own use)
+// glds16_s clobbers m0 (reserved: the compiler sets it before each own use)
 #pragma clang diagnostic ignored "-Winline-asm"
 
 namespace dr {
@@ -71,56 +80,27 @@ __device__ inline uint32_t lds_addr(const uint8_t *p) {
 }
 
 // ---------------------------------------------------------------------------
-// dr_gemm_x6: weight-stationary (round 4).
-//
-// Round 3's cooperative-split kernel re-streamed the whole 384-KB weight
-// image of its net through LDS for every 128-row tile: 48 of its 64 LDS-DMA
-// pieces per stage were weights, and the SIMD's vector issue (MFMA issue, DMA
-// pieces, fragment reads, split VALU) -- not the matrix pipe -- set its time
-// (MFMA busy 0.44, waves waiting on issue 0.54 of their cycles, r03 PMC).
-// Here the weights never move after the prologue: a 256-thread block (one
-// wave per SIMD, 512 registers) holds its net's three weight planes in
-// registers, wave w the 64 output columns 64 w .. + 63 (2 column tiles x 16
-// k16 steps x 3 planes of MFMA B fragments = 384 registers: the h and m
-// planes in AGPRs, read there by asm MFMAs, the l plane in VGPRs), and
-// streams only the activations: per 32-row step each wave moves its 8 rows of
-// f32 by LDS-DMA into a private staging slot (8 pieces: no other wave reads
-// them, so no barrier orders them), splits them into the block's plane
-// buffer (4 split units per lane) and runs 192 MFMAs (2 column tiles x 16
-// k16 steps x 6 products) on the block's 32 rows.  One barrier per row step
-// publishes the planes.  The same splits, products and per-output order as
-// round 3's kernel (bitwise the same C, checked while both existed).
-//
-// Per SIMD and row step: 192 MFMAs (6,144 pipe cycles, 1,536 of issue)
-// against 8 DMA pieces, 96 fragment reads, 32 stores and ~180 split VALU --
-// round 3: 16 DMA pieces per 96 MFMAs.
+// dr_gemm_x6: weight-stationary.  A 256-thread block (one wave per SIMD, 512
+// registers) holds its net's three weight planes in registers for the whole
+// launch -- wave w the 64 output columns 64 w .. + 63 as 4 column tiles of
+// 16 x 8 k32 steps x 3 planes of MFMA B fragments = 384 registers, the h and
+// m planes in AGPRs (read there by inline-asm MFMAs: hipcc's MFMA builtin
+// copies AGPR operands back to VGPRs before every use), the l plane in VGPRs
+// -- and streams only the activations: per 32-row step each wave moves its 8
+// rows of f32 by LDS-DMA into a private staging slot (no other wave reads
+// them, so no barrier orders them), splits them into the block's
+// double-buffered plane image and runs 384 MFMAs on the block's 32 rows; one
+// barrier per row step publishes the planes.
 //
 // LDS: planes 2 x 48 KB (32 rows x 256 k x 3 planes, stored chunk-major:
-// the 16-B chunk c (8 k) of row r at c * 512 + 16 r, so the fragment reads'
-// lane groups (16 distinct rows of one chunk) are conflict-free, and every
-// address is a per-lane base plus an immediate; the split writes' 16-lane
-// groups (8 rows of two adjacent chunks) are conflict-free because the odd
-// chunk's lanes write the other 8-B half of their slots, round 5) + f32 staging 2 x 32 KB (wave w's 8 KB:
-// piece i holds split chunks 4 i .. + 3 of its 8 rows, slot 32 h + 8 c' + r
-// = row r, chunk 4 i + c', float4 h) = 160 KB.
-//
-// Row step k of a block (its k-th 32-row step), per wave: wait for the
-// staging of step k + 1 (issued in step k - 2); phase 0 = the 16 k16 steps
-// of column tile 0 with tile 1's 16 output stores of row step k - 1 beside
-// them, phase 1 = tile 1 with tile 0's stores of row step k (each store two
-// full 128-B row segments, through a buffer descriptor); fragments read two
-// k16 steps ahead; split half-units of row step k + 1 every 4 k16 steps and,
-// behind each unit's two half-units, the DMA of its two staging pieces for
-// step k + 3; then lgkmcnt(0) + barrier.
-//
-// Measured (scripts/micro/gemm_x6_bench.py, both nets, 65,536 rows): 112-117
-// us against 118-120 for round 3's kernel on the same boxes.  In-kernel stamps
-// (DR_WS_STAMPS, scripts/micro/ws_stamps.py): a row step takes ~9,800-10,500
-// shader cycles against 6,144 of MFMA; by ablation (scripts/micro/patches/x6_diag.patch) the split
-// costs ~2,300 of them, the fragment reads ~900, the stores ~570.  Moving the
-// split VALU into the MFMA asm (so it issues in the MFMAs' shadow) needs ~10
-// more VGPRs than the 512-register budget leaves (weights 384 + accumulators
-// 64 + fragments 36 + split): the allocator spilled the weights.
+// the 16-B chunk c (8 k) of row r at c * 512 + 16 r, so a fragment read's
+// 16-lane group (16 consecutive rows of one chunk) is 256 contiguous bytes,
+// and every address is a per-lane base plus an immediate; the split writes'
+// 16-lane groups (8 rows of two adjacent chunks) are conflict-free because
+// the odd chunk's lanes write the other 8-B half of their slots) + f32
+// staging 2 x 32 KB (wave w's 8 KB: piece i holds split chunks 4 i .. + 3 of
+// its 8 rows, slot 32 h + 8 c' + r = row r, chunk 4 i + c', float4 h) =
+// 160 KB.
 constexpr int WS_RS = X6_RS;                         // rows per row step
 constexpr int WS_PLANE = WS_RS * XK * 2;             // 16 KB: one plane of a row step
 constexpr int WS_PSTAGE = 3 * WS_PLANE;              // 48 KB
@@ -128,329 +108,17 @@ constexpr int WS_FSLOT = WS_RS * XK * 4;             // 32 KB: f32 rows of a row
 constexpr int WS_LDS_F = 2 * WS_PSTAGE;              // staging after the two plane stages
 constexpr int WS_LDS = 2 * WS_PSTAGE + 2 * WS_FSLOT; // 160 KB
 constexpr int WS_THREADS = 256;
-// fragment sets in flight (read two k16 steps ahead)
+// fragment sets in flight (read two k32 steps ahead)
 constexpr int WS_NF = 3;
-// DR_WS_STAMPS (diagnostic builds only): s_memtime at six points of every row
-// step for the waves of blocks 0-7 (read back by dr_x6_diag_stamps,
-// scripts/micro/ws_stamps.py); no output depends on a stamp
-#ifndef DR_WS_STAMPS
-#define DR_WS_STAMPS 0
-#endif
-#if DR_WS_STAMPS
-__device__ unsigned long long g_ws_st[8 * 4 * 24 * 8];
-#define WS_STAMP(k, i)                                                                     \
-    do {                                                                                   \
-        __builtin_amdgcn_sched_barrier(0);                                                 \
-        const unsigned long long t__ = __builtin_amdgcn_s_memtime();                       \
-        if (blockIdx.x < 8 && (k) < 24 && lane == 0)                                       \
-            g_ws_st[((blockIdx.x * 4 + w) * 24 + (k)) * 8 + (i)] = t__;                     \
-        __builtin_amdgcn_sched_barrier(0);                                                 \
-    } while (0)
-#else
-#define WS_STAMP(k, i) \
-    do {               \
-    } while (0)
-#endif
-
-// The MFMAs of the weight-stationary kernel by inline asm, so that the
-// weights' h and m planes are read straight from AGPRs (hipcc's MFMA builtin
-// takes VGPR operands and copies AGPR-held values back before every use).
-// D[m][n] += X[m][k] W[n][k]: the activation fragment is the A operand, the
-// weight fragment the B operand, D in VGPRs.  Consecutive MFMAs on one
-// accumulator need no wait states; a VALU or VMEM reader of D does: the
-// epilogue pads them, and tests/test_x6_asm_hazards.py checks that no
-// compiler-generated instruction reads an accumulator between these
-// statements.
-__device__ inline void mfma_x6_a(f32x16_t &d, const bf16x8_t &x, const bf16x8_t &w) {
-    asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+v"(d) : "v"(x), "a"(w));
-}
-__device__ inline void mfma_x6_v(f32x16_t &d, const bf16x8_t &x, const bf16x8_t &w) {
-    asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+v"(d) : "v"(x), "v"(w));
-}
-__device__ inline void mfma_x6_first(f32x16_t &d, const bf16x8_t &x, const bf16x8_t &w) {
-    asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, 0" : "=v"(d) : "v"(x), "a"(w));
-}
-// The six products of one (column tile, k16 step): h += xh.wh; l += xh.wm,
-// xm.wh, xh.wl, xl.wh, xm.wm (round 3's order, so bitwise its C)
-__device__ inline void mfma_x6_group(bool first, f32x16_t &h, f32x16_t &l, const bf16x8_t &xh,
-                                     const bf16x8_t &xm, const bf16x8_t &xl, const bf16x8_t &wh,
-                                     const bf16x8_t &wm, const bf16x8_t &wl) {
-    if (first) {
-        mfma_x6_first(h, xh, wh);
-        mfma_x6_first(l, xh, wm);
-    } else {
-        mfma_x6_a(h, xh, wh);
-        mfma_x6_a(l, xh, wm);
-    }
-    mfma_x6_a(l, xm, wh);
-    mfma_x6_v(l, xh, wl);
-    mfma_x6_a(l, xl, wh);
-    mfma_x6_a(l, xm, wm);
-}
-
-__global__ __launch_bounds__(WS_THREADS, 1) void gemm_x6_ws_kernel(
-    const float *__restrict__ A, const uint8_t *__restrict__ img, float *__restrict__ C,
-    int64_t m, int batch) {
-    __shared__ __attribute__((aligned(16))) uint8_t sh[WS_LDS];
-    const int lane = threadIdx.x & 63;
-    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int b = (int)blockIdx.x % batch;
-    const int per = (int)gridDim.x / batch;          // blocks per net
-    const int j0 = (int)blockIdx.x / batch;
-    const int steps_net = (int)(m / WS_RS);
-    const int R = (steps_net - j0 + per - 1) / per;  // row steps j0, j0 + per, ...
-    const float *Ab = A + (int64_t)b * m * XK;
-    float *Cb = C + (int64_t)b * m * XN;
-    const int fr = lane & 31, fh = lane >> 5;
-
-    // the weights: wave w's 64 columns, every k16 step, three planes, as MFMA
-    // B fragments (lane: column 64 w + 32 j + fr, k 16 s + 8 fh .. + 7).  The
-    // h and m planes live in AGPRs (256) and are read there by the MFMAs, the
-    // l plane in VGPRs (128)
-    bf16x8_t Wa[2][16][2], Wv[2][16];
-    {
-        const uint8_t *ib = img + (int64_t)b * W_IMG + lane * 16;
-#pragma unroll
-        for (int j = 0; j < 2; ++j)
-#pragma unroll
-            for (int s = 0; s < 16; ++s) {
-                const uint8_t *src = ib + ((w * 2 + j) * 16 + s) * 3 * W_FRAG;
-                Wa[j][s][0] = *reinterpret_cast<const bf16x8_t *>(src);
-                Wa[j][s][1] = *reinterpret_cast<const bf16x8_t *>(src + W_FRAG);
-                Wv[j][s] = *reinterpret_cast<const bf16x8_t *>(src + 2 * W_FRAG);
-            }
-    }
-
-    // staging: wave w's 8 rows of row step k in its 8 KB of slot k & 1.  Piece
-    // i: lane L = 32 h + 8 c' + r loads float4 h of split chunk 4 i + c' of
-    // row r (each row contributes 128 contiguous bytes per piece)
-    // Odd chunks are staged with their two float4 halves swapped (half shf ^ 1
-    // in slot half shf), so that the lanes splitting an odd chunk process its
-    // halves in the opposite order to their even-chunk neighbours (see
-    // wr_base below).
-    const int sr = lane & 7, sc = (lane >> 3) & 3, shf = lane >> 5;
-    const uint32_t voff_f = (uint32_t)(sr * 1024 + 32 * sc + 16 * (shf ^ (sc & 1)));
-    auto issue_rows = [&](int k) {
-        const float *r0 = Ab + ((int64_t)(j0 + k * per) * WS_RS + 8 * w) * XK;
-        uint8_t *dst = sh + WS_LDS_F + (k & 1) * WS_FSLOT + w * 8 * 1024;
-#pragma unroll
-        for (int i = 0; i < 8; ++i) glds16_s(r0 + 32 * i, voff_f, lds_addr(dst + i * 1024));
-    };
-    // split unit u of row step k: lane L splits row L & 7 of the wave's 8,
-    // chunk 8 u + (L >> 3) (pieces 2 u + (L >> 5), slots L & 31 and 32 + (L & 31)),
-    // in halves of 4 k (one float4 read, 3 ds_write_b64); half-unit hf of a
-    // lane whose chunk is odd is the chunk's half hf ^ 1 (the staging swap)
-    const int rd_base = WS_LDS_F + w * 8 * 1024 + fh * 1024 + fr * 16;
-    auto split_read = [&](int k, int u, int hf, float4 &v) {
-        v = *reinterpret_cast<const float4 *>(sh + rd_base + (k & 1) * WS_FSLOT + u * 2048 +
-                                              hf * 512);
-    };
-    // ds_write_b64 banks are (a / 4) mod 32 over 16-lane groups: a group is 8
-    // rows of two adjacent chunks (512 B apart, the same banks), so with one
-    // half (8 B) of each 16-B slot written per instruction the two chunks hit
-    // the same 16 banks (2-way: the 1.67 M SQ_LDS_BANK_CONFLICT cycles per
-    // dispatch of profiles/r04_pmc_x6.json, = 1,024 waves x 17 row steps x 24
-    // writes x 4 groups).  Odd chunks write the other half in each
-    // instruction: 16 distinct 8-B positions of a 128-B bank row.
-    const int wr_base = (lane >> 3) * 512 + (8 * w + sr) * 16;
-    const int wr_odd = (lane >> 3) & 1;
-    const int wr_half[2] = {wr_base + 8 * wr_odd, wr_base + 8 * (wr_odd ^ 1)};
-    auto split_write = [&](int k, int u, int hf, const float4 &v) {
-        const float x[4] = {v.x, v.y, v.z, v.w};
-        uint32_t h[2], mm[2], l[2];
-#pragma unroll
-        for (int q = 0; q < 2; ++q) {
-            const float a = x[2 * q], bb = x[2 * q + 1];
-            const uint32_t ph = pk_bf16(a, bb);
-            const float ra = a - lo_f(ph), rb = bb - hi_f(ph);
-            const uint32_t pm = pk_bf16(ra, rb);
-            h[q] = ph;
-            mm[q] = pm;
-            l[q] = pk_bf16(ra - lo_f(pm), rb - hi_f(pm));
-        }
-        uint8_t *dst = sh + (k & 1) * WS_PSTAGE + wr_half[hf] + u * 8 * 512;
-        typedef uint32_t u32x2_t __attribute__((ext_vector_type(2)));
-        *reinterpret_cast<u32x2_t *>(dst) = (u32x2_t){h[0], h[1]};
-        *reinterpret_cast<u32x2_t *>(dst + WS_PLANE) = (u32x2_t){mm[0], mm[1]};
-        *reinterpret_cast<u32x2_t *>(dst + 2 * WS_PLANE) = (u32x2_t){l[0], l[1]};
-    };
-    auto split_store = [&](int k, int u, int hf, uint32_t h0, uint32_t h1, uint32_t m0,
-                           uint32_t m1, uint32_t l0, uint32_t l1) {
-        uint8_t *dst = sh + (k & 1) * WS_PSTAGE + wr_half[hf] + u * 8 * 512;
-        typedef uint32_t u32x2_t __attribute__((ext_vector_type(2)));
-        *reinterpret_cast<u32x2_t *>(dst) = (u32x2_t){h0, h1};
-        *reinterpret_cast<u32x2_t *>(dst + WS_PLANE) = (u32x2_t){m0, m1};
-        *reinterpret_cast<u32x2_t *>(dst + 2 * WS_PLANE) = (u32x2_t){l0, l1};
-    };
-    // activation fragments of k16 step s (MFMA A operand): row fr, k 16 s +
-    // 8 fh .. + 7 (chunk 2 s + fh)
-    typedef bf16x8_t AFrag[3];
-    const int fr_base = fh * 512 + fr * 16;
-    auto read_frag = [&](int k, int s, AFrag &f) {
-        const uint8_t *src = sh + (k & 1) * WS_PSTAGE + fr_base + s * 1024;
-#pragma unroll
-        for (int p = 0; p < 3; ++p) f[p] = *reinterpret_cast<const bf16x8_t *>(src + p * WS_PLANE);
-    };
-    // accumulators D[m][n] (m the tile row, n the column): hi (h.h) and lo
-    // (the five small products), per column tile
-    f32x16_t acc_h[2], acc_l[2];
-    // the output stores of tile t: D[m][n] map: column n = 32 t + fr, row
-    // m = 8 (r >> 2) + 4 fh + (r & 3); each store writes two full 128-B row
-    // segments, through a buffer descriptor of the row step's 32 KB of C (a
-    // per-lane offset plus an SGPR offset per register: no VALU per store)
-    const int st_off = (4 * fh * XN + fr) * 4;
-    auto store_one = [&](int k, int t, int r) {
-        // k = -1 (tile 1 of no row step, in row step 0): a 0-byte range, the
-        // stores are dropped
-        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-            Cb + (int64_t)(j0 + k * per) * WS_RS * XN, 0, k < 0 ? 0 : WS_RS * XN * 4,
-            0x00020000);
-        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(acc_h[t][r]), rs, st_off,
-                                              ((8 * (r >> 2) + (r & 3)) * XN + 64 * w + 32 * t) * 4,
-                                              0);
-    };
-    // hi + lo of tile t, in place, after the MFMA -> VALU wait states
-    auto finish_tile = [&](int t) {
-        asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
-        acc_h[t] = acc_h[t] + acc_l[t];
-    };
-
-    if (R > 0) issue_rows(0);
-    if (R > 1) issue_rows(1);
-    __builtin_amdgcn_sched_barrier(0);
-    if (R > 1)
-        asm volatile("s_waitcnt vmcnt(8)" ::: "memory");     // weights + rows of step 0
-    else
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#pragma unroll
-    for (int q = 0; q < 8; ++q) {
-        float4 v;
-        split_read(0, q >> 1, q & 1, v);
-        split_write(0, q >> 1, q & 1, v);
-    }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");       // staging slot 0 read
-    issue_rows(R > 2 ? 2 : R - 1);                           // clamped: never split
-    asm volatile("s_waitcnt vmcnt(8)" ::: "memory");         // step 1's staging
-    asm volatile("s_barrier" ::: "memory");                  // planes of step 0
-    WS_STAMP(23, 1);
-    AFrag fb[WS_NF];
-    read_frag(0, 0, fb[0]);
-    if (WS_NF == 3) read_frag(0, 1, fb[1]);
-    // Row step k, per wave: phase 0 = the 16 k16 steps of column tile 0
-    // (96 MFMAs) with tile 1's stores of row step k - 1 beside them, phase 1 =
-    // tile 1 with tile 0's stores of row step k; fragments read two k16 steps
-    // ahead (3 sets); split half-units q = 0..7 of row step k + 1 at k16
-    // steps 1, 5, 9, 13 of each phase (read one step before), the DMA of step
-    // k + 3 two pieces at a time behind the split reads of its slot; then
-    // lgkmcnt(0) + barrier.
-    // The body has no data-dependent branch (measured 99-100 vs 105-106 us
-    // with branches around the first and last steps' work, bitwise the same
-    // C): row step 0's phase-0 stores go through a 0-byte buffer range (no
-    // row step -1), the last steps split their successor's staging into the
-    // unused plane buffer, and the staging DMA past the last step re-loads it
-    // (clamped rows).  Branches also risk the compiler copying an accumulator
-    // between asm MFMA groups, a VALU read of an MFMA result inside its wait
-    // states (tests/test_x6_asm_hazards.py).
-    auto row_step = [&](int k) {
-        WS_STAMP(k, 0);
-        // the staging of step k + 1 (issued in step k - 2): every vector
-        // memory op of step k - 1 (32 stores + 8 DMA pieces) is younger; for
-        // k = 0 the prologue waited
-        __builtin_amdgcn_sched_barrier(0);
-        asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
-        WS_STAMP(k, 1);
-#pragma unroll
-        for (int t = 0; t < 2; ++t) {
-            if (t == 1) WS_STAMP(k, 2);
-            // the other tile's finished outputs (t = 0: tile 1 of step k - 1)
-            const int ko = t == 1 ? k : k - 1;
-            finish_tile(1 - t);
-            float4 v;
-            uint32_t sh0, sm0, sl0, sh1, sm1, sl1;
-#pragma unroll
-            for (int s = 0; s < 16; ++s) {
-                // global k16 step index of this row step: g = 16 t + s; the
-                // fragments of g + D (tile 1 re-reads steps 0 .. D - 1)
-                const int g = 16 * t + s;
-                constexpr int D = WS_NF - 1;           // prefetch distance
-                if (g + D < 32)
-                    read_frag(k, (g + D) & 15, fb[(g + D) % WS_NF]);
-                const int q = 4 * t + (s >> 2);        // split half-unit
-                // half-unit q: read before k16 step 4 (q - 4 t) + 1; its two
-                // pairs split inside the MFMA groups of steps + 2 and + 3;
-                // written (3 x 8 B) after the second
-                if ((s & 3) == 0) split_read(k + 1, q >> 1, q & 1, v);
-                const AFrag &x = fb[g % WS_NF];
-                mfma_x6_group(s == 0, acc_h[t], acc_l[t], x[0], x[1], x[2], Wa[t][s][0],
-                              Wa[t][s][1], Wv[t][s]);
-                store_one(ko, 1 - t, s);
-                if ((s & 3) == 1) {
-                    // the half-unit's split (its read, one k16 step ago, has
-                    // landed behind the MFMAs)
-                    sh0 = pk_bf16(v.x, v.y);
-                    float ra = v.x - lo_f(sh0), rb = v.y - hi_f(sh0);
-                    sm0 = pk_bf16(ra, rb);
-                    sl0 = pk_bf16(ra - lo_f(sm0), rb - hi_f(sm0));
-                    sh1 = pk_bf16(v.z, v.w);
-                    ra = v.z - lo_f(sh1), rb = v.w - hi_f(sh1);
-                    sm1 = pk_bf16(ra, rb);
-                    sl1 = pk_bf16(ra - lo_f(sm1), rb - hi_f(sm1));
-                }
-                if ((s & 3) == 1) {
-                    split_store(k + 1, q >> 1, q & 1, sh0, sh1, sm0, sm1, sl0, sl1);
-                    if (q & 1) {
-                        // unit q >> 1's two staging pieces were read (the
-                        // split above consumed the data, and asm volatile
-                        // keeps the DMA behind it): refill them with step k + 3
-                        // (clamped to the last step: such rows are never split)
-                        const int u = q >> 1;
-                        const int k3 = k + 3 >= R ? R - 1 : k + 3;
-                        const float *r0 =
-                            Ab + ((int64_t)(j0 + k3 * per) * WS_RS + 8 * w) * XK;
-                        uint8_t *dst = sh + WS_LDS_F + ((k + 3) & 1) * WS_FSLOT + w * 8 * 1024;
-                        glds16_s(r0 + 32 * (2 * u), voff_f, lds_addr(dst + (2 * u) * 1024));
-                        glds16_s(r0 + 32 * (2 * u + 1), voff_f,
-                                 lds_addr(dst + (2 * u + 1) * 1024));
-                    }
-                }
-            }
-        }
-        WS_STAMP(k, 3);
-        WS_STAMP(k, 4);
-        // this wave's plane writes (step k + 1) and fragment reads (step k)
-        // done; after the barrier the planes of k + 1 are complete
-        __builtin_amdgcn_sched_barrier(0);
-        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-        WS_STAMP(k, 5);
-        read_frag(k + 1, 0, fb[0]);          // after the last step: unused
-        if (WS_NF == 3) read_frag(k + 1, 1, fb[1]);
-    };
-    for (int k = 0; k < R; ++k) row_step(k);
-    // tile 1 of the last row step
-    if (R > 0) {
-        finish_tile(1);
-#pragma unroll
-        for (int r = 0; r < 16; ++r) store_one(R - 1, 1, r);
-    }
-    // the clamped staging DMA of the last steps lands before the block's LDS
-    // is released
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-}
-
-// ---------------------------------------------------------------------------
-// gemm_x6_ws16_kernel (round 6, X6_MFMA16): gemm_x6_ws_kernel on
-// v_mfma_f32_16x16x32_bf16.  Under DVFS give-back the 16x16x32 form held a
-// higher clock than 32x32x16 at equal cycles per FLOP (MI355X_MICROARCH.md,
-// DVFS give-back item 7), and its 16-row A fragments let a phase be a ROW
+// The 16-row A fragments of v_mfma_f32_16x16x32_bf16 let a phase be a ROW
 // tile: phase t runs rows 16 t .. + 15 of the row step against all four of
 // the wave's 16-column tiles, so each activation fragment is read from LDS
-// once per row step (48 ds_read_b128 instead of 96).  Same block shape,
-// staging, split and LDS planes as gemm_x6_ws_kernel; the weights in the
-// X6_MFMA16 image order (wimg_off): wave w's column tile ct, k32 step s.
-// Per SIMD and row step: 384 MFMAs of 16 cycles (the same 6,144 pipe cycles,
-// 3,072 of issue), 48 fragment reads, 32 stores, 8 DMA pieces.
-// Accumulators D[m][n] of a 16 x 16 tile: column n = lane & 15, row
-// m = 4 (lane >> 4) + r, r = 0..3.
+// once per row step (48 ds_read_b128; the round-5 32x32x16 kernel re-read
+// them per column tile, 96).  The weights come in the image order of
+// wimg_off: wave w's column tile ct, k32 step s.  Per SIMD and row step:
+// 384 MFMAs of 16 cycles (6,144 pipe cycles, 3,072 of issue), 48 fragment
+// reads, 32 stores, 8 DMA pieces.  Accumulators D[m][n] of a 16 x 16 tile:
+// column n = lane & 15, row m = 4 (lane >> 4) + r, r = 0..3.
 typedef float f32x4_t __attribute__((ext_vector_type(4)));
 
 __device__ inline void mfma16_a(f32x4_t &d, const bf16x8_t &x, const bf16x8_t &w) {
@@ -495,7 +163,12 @@ __global__ __launch_bounds__(WS_THREADS, 1) void gemm_x6_ws16_kernel(
             }
     }
 
-    // staging and split: gemm_x6_ws_kernel's, unchanged
+    // staging: wave w's 8 rows of row step k in its 8 KB of slot k & 1.  Piece
+    // i: lane L = 32 h + 8 c' + r loads float4 h of split chunk 4 i + c' of
+    // row r (each row contributes 128 contiguous bytes per piece).  Odd
+    // chunks are staged with their two float4 halves swapped, so that the
+    // lanes splitting an odd chunk process its halves in the opposite order
+    // to their even-chunk neighbours (the conflict-free split writes)
     const int sr = lane & 7, sc = (lane >> 3) & 3, shf = lane >> 5;
     const uint32_t voff_f = (uint32_t)(sr * 1024 + 32 * sc + 16 * (shf ^ (sc & 1)));
     auto issue_rows = [&](int k) {
@@ -574,7 +247,7 @@ __global__ __launch_bounds__(WS_THREADS, 1) void gemm_x6_ws16_kernel(
     };
     // the six products of row tile t, k32 step s, for the four column tiles
     // (h += xh.wh; l += xh.wm, xm.wh, xh.wl, xl.wh, xm.wm: per output the
-    // order of gemm_x6_ws_kernel), interleaved over the column tiles
+    // order of every x6 kernel), interleaved over the column tiles
     auto mfma_group = [&](bool first, int t, int s, const AFrag &x) {
 #pragma unroll
         for (int ct = 0; ct < 4; ++ct) {
@@ -618,9 +291,17 @@ __global__ __launch_bounds__(WS_THREADS, 1) void gemm_x6_ws16_kernel(
     // two k32 steps ahead; split half-unit q = 4 t + (s >> 1) of row step
     // k + 1 read at even s, split and written at odd s, and behind each
     // unit's second half the DMA of its two staging pieces for step k + 3;
-    // then lgkmcnt(0) + barrier.  No data-dependent branch (the same edge
-    // handling as gemm_x6_ws_kernel).
+    // then lgkmcnt(0) + barrier.  No data-dependent branch (round 4: 99-100
+    // vs 105-106 us with branches around the first and last steps' work):
+    // row step 0's phase-0 stores go through a 0-byte buffer range, the last
+    // steps split their successor's clamped staging into the unused plane
+    // buffer.  Branches would also risk the compiler copying an accumulator
+    // between asm MFMA groups, a VALU read inside an MFMA's wait states
+    // (tests/test_x6_asm_hazards.py).
     auto row_step = [&](int k) {
+        // the staging of step k + 1 (issued in step k - 2): every vector
+        // memory op of step k - 1 (32 stores + 8 DMA pieces) is younger;
+        // for k = 0 the prologue waited
         __builtin_amdgcn_sched_barrier(0);
         asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
 #pragma unroll
@@ -678,6 +359,7 @@ __global__ __launch_bounds__(WS_THREADS, 1) void gemm_x6_ws16_kernel(
 }
 
 // ---------------------------------------------------------------------------
+// ---------------------------------------------------------------------------
 // Weight gradient of the same layer, dW[b] = G[b]^T H[b] (G = grad_z, H = the
 // layer input, both (m, 256) f32 row-major), split over C row chunks: block
 // (b, n-half, chunk) writes the 128 x 256 partial ws[b][chunk][n][k] of its
@@ -685,214 +367,19 @@ __global__ __launch_bounds__(WS_THREADS, 1) void gemm_x6_ws16_kernel(
 // deferred finish sums C = 64 chunks in a fixed order).  8 waves as 2 (n) x
 // 4 (k) of 64 x 64 outputs, the same split hi/lo accumulation as the forward.
 //
-// Both operands are reduced over rows, so an MFMA fragment is 8 consecutive
-// ROWS of one column.  Round 3's kernel had each lane gather its fragments
-// with ds_read_b32 from f32 stage images and split them itself: a G column
-// was split by each of the 4 k waves that read it and an H column by both n
-// waves, 64 elements per lane and stage (~350 VALU + 64 ds_read_b32 per wave
-// against 48 MFMAs), and the SIMD's issue, not the matrix pipe, bounded it.
-// Here each 32-row stage is split ONCE (round 4): every thread loads 6 float4
-// of the stage (2 of G's 32 x 128 half, 4 of H's 32 x 256) into registers
-// one stage ahead, splits them and writes the three bf16 planes ROW-major
-// into LDS; the fragments come back column-major through gfx950's
-// transposing read ds_read_b64_tr_b16 (two per fragment).  Per wave and
-// stage: 24 split elements (~130 VALU), 18 ds_write_b64, 48 transposed
-// reads, 48 MFMAs, one barrier (mid-stage, see the loop).  Bitwise round 3's
-// partials (same splits, products and per-output order); 110-111 vs 119-124
-// us for both nets at 65,536 rows, 64 chunks (scripts/micro/wgrad_ab.py, same
-// box), 101.5-103.5 vs 105.5-109.0 with the barrier moved mid-stage.
-//
-// DR_WG_STAMPS (diagnostic builds only): s_memtime at five points of every
-// stage for the waves of blocks 0-7 (read back by dr_x6_diag_wg_stamps,
-// scripts/micro/wg_stamps.py); the stamps' scheduling barriers separate the
-// phases the compiler otherwise interleaves
-#ifndef DR_WG_STAMPS
-#define DR_WG_STAMPS 0
-#endif
-#if DR_WG_STAMPS
-__device__ unsigned long long g_wg_st[8 * 8 * 24 * 8];
-#define WG_STAMP(k, i)                                                                     \
-    do {                                                                                   \
-        __builtin_amdgcn_sched_barrier(0);                                                 \
-        const unsigned long long t__ = __builtin_amdgcn_s_memtime();                       \
-        if (blockIdx.x < 8 && (k) < 24 && lane == 0)                                       \
-            g_wg_st[((blockIdx.x * 8 + wid) * 24 + (k)) * 8 + (i)] = t__;                   \
-        __builtin_amdgcn_sched_barrier(0);                                                 \
-    } while (0)
-#else
-#define WG_STAMP(k, i) \
-    do {               \
-    } while (0)
-#endif
+// Both operands are reduced over rows, so an MFMA fragment holds ROWS of one
+// column.  Each 32-row stage is split ONCE: every thread loads 6 float4 of
+// the stage (2 of G's 32 x 128 half, 4 of H's 32 x 256) into registers one
+// stage ahead, splits them and writes the three bf16 planes ROW-major into
+// LDS; the fragments come back column-major through gfx950's transposing
+// read ds_read_b64_tr_b16 (two per fragment).
 constexpr int TW_BM = 32;                          // rows per stage
 constexpr int TW_PLANE_ROW = (128 + 256) * 2;      // 768 B: one plane of one row
-constexpr int TW_ROW = 3 * TW_PLANE_ROW + 64;      // 2,368 B
-constexpr int TW_STAGE = TW_BM * TW_ROW;           // 75,776 B
-constexpr int TW_LDS = 2 * TW_STAGE;               // 151,552 B
 
 typedef short i16x4_t __attribute__((ext_vector_type(4)));
-typedef float f32x4_t __attribute__((ext_vector_type(4)));
 
-__device__ inline bf16x8_t tr_frag(const uint8_t *p) {
-    typedef __attribute__((address_space(3))) i16x4_t lds_i16x4;
-    const i16x4_t a = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-        (lds_i16x4 *)(uintptr_t)lds_addr(p));
-    const i16x4_t c = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-        (lds_i16x4 *)(uintptr_t)lds_addr(p + 4 * TW_ROW));
-    return __builtin_bit_cast(bf16x8_t, __builtin_shufflevector(a, c, 0, 1, 2, 3, 4, 5, 6, 7));
-}
-
-__global__ __launch_bounds__(XTHREADS) void gemm_x6_wgrad_kernel(
-    const float *__restrict__ Gm, const float *__restrict__ Hm, float *__restrict__ ws,
-    int64_t m, int chunks) {
-    __shared__ __attribute__((aligned(16))) uint8_t sh[TW_LDS];
-    const int tid = threadIdx.x, lane = tid & 63;
-    const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int wn = wid >> 2, wk = wid & 3;
-    const int chunk = (int)(blockIdx.x % chunks);
-    const int nh = (int)((blockIdx.x / chunks) & 1);
-    const int b = (int)(blockIdx.x / chunks / 2);
-    const int64_t rows = m / chunks;
-    const int G_ = (int)(rows / TW_BM);
-    const float *Gb = Gm + ((int64_t)b * m + (int64_t)chunk * rows) * 256 + nh * 128;
-    const float *Hb = Hm + ((int64_t)b * m + (int64_t)chunk * rows) * 256;
-
-    // thread tid's six float4 of a stage: G item i (row (tid + 512 i) / 32,
-    // columns 4 ((tid + 512 i) % 32) ..), H item i (row (tid + 512 i) / 64)
-    int ld_src[6], ld_dst[6];
-#pragma unroll
-    for (int i = 0; i < 6; ++i) {
-        const int q = tid + 512 * (i < 2 ? i : i - 2);
-        const int r = i < 2 ? q >> 5 : q >> 6;
-        const int c = i < 2 ? (q & 31) * 4 : (q & 63) * 4;
-        ld_src[i] = (i < 2 ? r * 256 + c : r * 256 + c);
-        ld_dst[i] = r * TW_ROW + (i < 2 ? c : 128 + c) * 2;
-    }
-    f32x4_t ld[6];
-    auto load = [&](int g) {
-        const int64_t r0 = (int64_t)g * TW_BM * 256;
-#pragma unroll
-        for (int i = 0; i < 6; ++i)
-            ld[i] = *reinterpret_cast<const f32x4_t *>((i < 2 ? Gb : Hb) + r0 + ld_src[i]);
-    };
-    auto split_store = [&](int buf) {
-        uint8_t *S = sh + buf * TW_STAGE;
-#pragma unroll
-        for (int i = 0; i < 6; ++i) {
-            const f32x4_t x = ld[i];
-            uint32_t h[2], mm[2], l[2];
-#pragma unroll
-            for (int q = 0; q < 2; ++q) {
-                const float a = x[2 * q], c = x[2 * q + 1];
-                const uint32_t ph = pk_bf16(a, c);
-                const float ra = a - lo_f(ph), rc = c - hi_f(ph);
-                const uint32_t pm = pk_bf16(ra, rc);
-                h[q] = ph;
-                mm[q] = pm;
-                l[q] = pk_bf16(ra - lo_f(pm), rc - hi_f(pm));
-            }
-            uint8_t *d = S + ld_dst[i];
-            *reinterpret_cast<uint2 *>(d) = make_uint2(h[0], h[1]);
-            *reinterpret_cast<uint2 *>(d + TW_PLANE_ROW) = make_uint2(mm[0], mm[1]);
-            *reinterpret_cast<uint2 *>(d + 2 * TW_PLANE_ROW) = make_uint2(l[0], l[1]);
-        }
-    };
-
-    // transposed-read lane address: the 16-lane group gq reads rows
-    // 8 (gq >> 1) + (0..3) (+ 4 for the second read), columns 16 (gq & 1) + 4 p
-    const int li = lane & 15, gq = lane >> 4;
-    const int fbase = (8 * (gq >> 1) + (li >> 2)) * TW_ROW + (16 * (gq & 1) + 4 * (li & 3)) * 2;
-    const int gcol = (wn * 64) * 2, hcol = (128 + wk * 64) * 2;
-
-    f32x16_t acc_h[2][2], acc_l[2][2];                    // [n tile i][k tile j]
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j) {
-            acc_h[i][j] = (f32x16_t){};
-            acc_l[i][j] = (f32x16_t){};
-        }
-
-    auto frag_addr = [&](int g, int s) { return sh + (g & 1) * TW_STAGE + fbase + 16 * s * TW_ROW; };
-    auto read_step = [&](int g, int s, bf16x8_t (&fg)[2][3], bf16x8_t (&fhp)[2][3]) {
-        const uint8_t *S = frag_addr(g, s);
-#pragma unroll
-        for (int i = 0; i < 2; ++i)
-#pragma unroll
-            for (int p = 0; p < 3; ++p) {
-                const uint8_t *q = S + p * TW_PLANE_ROW;
-                fg[i][p] = tr_frag(q + gcol + 64 * i);
-                fhp[i][p] = tr_frag(q + hcol + 64 * i);
-            }
-    };
-    auto mfma_step = [&](const bf16x8_t (&fg)[2][3], const bf16x8_t (&fhp)[2][3]) {
-#pragma unroll
-        for (int i = 0; i < 2; ++i)
-#pragma unroll
-            for (int j = 0; j < 2; ++j) {
-                const bf16x8_t *a = fg[i], *c = fhp[j];
-                acc_h[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], c[0], acc_h[i][j],
-                                                                      0, 0, 0);
-                f32x16_t t = acc_l[i][j];
-                t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], c[1], t, 0, 0, 0);
-                t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], c[0], t, 0, 0, 0);
-                t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], c[2], t, 0, 0, 0);
-                t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[2], c[0], t, 0, 0, 0);
-                t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], c[1], t, 0, 0, 0);
-                acc_l[i][j] = t;
-            }
-    };
-
-    load(0);
-    split_store(0);
-    load(G_ > 1 ? 1 : 0);
-    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-    // Stage g, per wave: (its first k16 step's fragments were read in stage
-    // g - 1) read the second k16 step's; the first k16 step's 24 MFMAs; the
-    // split of stage g + 1 into the other buffer; lgkmcnt(0) + barrier
-    // (publishes stage g + 1); read stage g + 1's
-    // first-step fragments; the second k16 step's 24 MFMAs; the loads of stage
-    // g + 2 (consumed by the next stage's split).  The barrier sits
-    // mid-stage, so the next stage's first reads hide behind MFMAs instead of
-    // all 48 reads of every wave queueing on the LDS right after it.  Stage
-    // g's buffer is rewritten only in stage g + 1, after this stage's
-    // barrier, by when every read of it has completed (lgkmcnt(0)).  The last
-    // iteration re-splits and re-reads the last stage (no branch).
-    bf16x8_t f0g[2][3], f0h[2][3], f1g[2][3], f1h[2][3];
-    read_step(0, 0, f0g, f0h);
-    for (int g = 0; g < G_; ++g) {
-        WG_STAMP(g, 0);
-        read_step(g, 1, f1g, f1h);
-        WG_STAMP(g, 1);
-        mfma_step(f0g, f0h);
-        WG_STAMP(g, 2);
-        split_store((g + 1) & 1);
-        WG_STAMP(g, 3);
-        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-        read_step(g + 1 < G_ ? g + 1 : g, 0, f0g, f0h);
-        WG_STAMP(g, 4);
-        mfma_step(f1g, f1h);
-        load(g + 2 < G_ ? g + 2 : G_ - 1);
-        WG_STAMP(g, 5);
-    }
-    // D[n][k]: column k = fr, row n = (r & 3) + 8 (r >> 2) + 4 fh
-    const int fr = lane & 31, fh = lane >> 5;
-    float *out = ws + ((int64_t)b * chunks + chunk) * 256 * 256 + (int64_t)(nh * 128) * 256;
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j) {
-            const f32x16_t v = acc_h[i][j] + acc_l[i][j];
-            float *c = out + (int64_t)(wn * 64 + i * 32 + 4 * fh) * 256 + wk * 64 + j * 32 + fr;
-#pragma unroll
-            for (int r = 0; r < 16; ++r) c[((r & 3) + 8 * (r >> 2)) * 256] = v[r];
-        }
-}
-
-#if X6_MFMA16
 // ---------------------------------------------------------------------------
-// gemm_x6_wgrad16_kernel (round 6, X6_MFMA16): gemm_x6_wgrad_kernel on
-// v_mfma_f32_16x16x32_bf16.  A stage's 32 rows are ONE k32 step: each wave's
+// gemm_x6_wgrad16_kernel: a stage's 32 rows are ONE k32 step: each wave's
 // 64 x 64 outputs are 4 x 4 tiles of 16 x 16 (the same 128 accumulator
 // registers), 96 MFMAs of 16 cycles per stage (the same 1,536 pipe cycles).
 // Fragments come from the same row-major plane image through two
@@ -901,7 +388,10 @@ __global__ __launch_bounds__(XTHREADS) void gemm_x6_wgrad_kernel(
 // of rows 4 g + e (e < 4) and 16 + 4 g + e - 4 (e >= 4) -- the same
 // permutation in both operands, so the products are the same.  The row
 // stride is 2,336 B (== 32 mod 256): rows 0..7 of a half fall in distinct
-// 8-bank groups, conflict-free.
+// 8-bank groups, conflict-free.  Per wave and stage: 24 split elements (~130
+// VALU), 18 ds_write_b64, 48 transposed reads, 96 MFMAs, one barrier.  The
+// round-5 32x32x16 form ran 116.7 us vs 114.2 for this one at 65,536 rows,
+// 64 chunks (scripts/micro/gemm_x6_bench.py, one box).
 constexpr int TW16_ROW = 3 * TW_PLANE_ROW + 32;    // 2,336 B
 constexpr int TW16_STAGE = TW_BM * TW16_ROW;       // 74,752 B
 constexpr int TW16_LDS = 2 * TW16_STAGE;           // 149,504 B
@@ -1042,7 +532,6 @@ __global__ __launch_bounds__(XTHREADS) void gemm_x6_wgrad16_kernel(
             for (int r = 0; r < 4; ++r) c[r * 256] = v[r];
         }
 }
-#endif  // X6_MFMA16
 
 // ---------------------------------------------------------------------------
 // dr_gemm_x6_bwd_first (round 5): the 256 x 256 layer's input gradient with
@@ -1069,24 +558,25 @@ __global__ __launch_bounds__(XTHREADS) void gemm_x6_wgrad16_kernel(
 // the wave's 64 columns x 16 features.
 //
 // Registers: the weights' h and m planes stay in AGPRs as in
-// gemm_x6_ws_kernel, but the l plane is streamed from L2 (one 1-KB fragment
-// per k16 step, two steps ahead) to make room for the epilogue, and the
-// activation rows are register-staged by compiler-tracked loads four split
-// half-units ahead (no LDS-DMA staging: every vector memory op is visible to
-// the compiler's waitcnt pass).  LDS holds only the double-buffered planes.
+// gemm_x6_ws16_kernel, but the l plane is streamed from L2 (two 1-KB
+// fragments per k32 step, six fragments ahead: every vector-memory wait is
+// in issue order, so a fragment load queued behind the h1 / staging loads
+// from HBM waits for them too -- round 5: 2 ahead 127 us per call, 6 ahead
+// 118) to make room for the epilogue, and the activation rows are
+// register-staged by compiler-tracked loads four split half-units ahead
+// (no LDS-DMA staging: every vector memory op is visible to the compiler's
+// waitcnt pass).  LDS holds only the double-buffered planes.
 // the X planes image (xrec_off, x6_split.h)
 __global__ __launch_bounds__(256) void split_x_kernel(const float *__restrict__ x, int64_t m,
                                                       int k, uint8_t *__restrict__ img) {
     split_x_item(x, nullptr, m, k, img, (int64_t)blockIdx.x * 256 + threadIdx.x);
 }
 
-#if X6_MFMA16
 // ---------------------------------------------------------------------------
-// gemm_x6_fl16_kernel (round 6, X6_MFMA16): gemm_x6_fl_kernel on
-// v_mfma_f32_16x16x32_bf16.  Phase t of a row step runs the wave's column
+// gemm_x6_fl16_kernel: phase t of a row step runs the wave's column
 // tiles 2 t, 2 t + 1 (16 columns each) for both 16-row tiles -- per k32
 // step 2 row tiles x 2 column tiles x 6 products = 24 MFMAs, the same 192
-// per phase and 6,144 pipe cycles per row step as gemm_x6_fl_kernel -- and
+// per phase and 6,144 pipe cycles per row step as the forward -- and
 // the epilogue of the other phase's four tiles.  The l plane of the weights
 // is streamed from L2 as before (two 1-KB fragments per k32 step).
 //
@@ -1094,8 +584,9 @@ __global__ __launch_bounds__(256) void split_x_kernel(const float *__restrict__ 
 // the B fragment of column tile ct is registers 0..3 of row tile 0's
 // accumulator and 0..3 of row tile 1's (K index 8 q + e <-> row 4 q + e and
 // 16 + 4 q + e - 4, q = lane >> 4), the A fragment is the record of
-// x6_split.h (X6_MFMA16 split_x_item), so no lane ever holds a zero half:
-// 12 MFMAs of 16 cycles per phase against 12 of 32 in gemm_x6_fl_kernel.
+// x6_split.h (split_x_item), so no lane ever holds a zero half: 12 MFMAs of
+// 16 cycles per phase (the round-5 32x32x16 kernel: 12 of 32, half of each
+// A fragment zero).
 __global__ __launch_bounds__(WS_THREADS, 1) void gemm_x6_fl16_kernel(
     const float *__restrict__ A, const uint8_t *__restrict__ img, const float *__restrict__ H,
     const uint8_t *__restrict__ ximg, float *__restrict__ part, int64_t m, int batch) {
@@ -1121,7 +612,7 @@ __global__ __launch_bounds__(WS_THREADS, 1) void gemm_x6_fl16_kernel(
             bf16x8_t, __builtin_amdgcn_raw_buffer_load_b128(
                           wrs, lane16, (((w * 4 + ct) * 8 + s) * 3 + p) * W_FRAG, 0));
     };
-    // the weights' h and m planes in AGPRs (the X6_MFMA16 image order)
+    // the weights' h and m planes in AGPRs (wimg_off's order)
     bf16x8_t Wa[4][8][2];
 #pragma unroll
     for (int ct = 0; ct < 4; ++ct)
@@ -1141,7 +632,11 @@ __global__ __launch_bounds__(WS_THREADS, 1) void gemm_x6_fl16_kernel(
 #pragma unroll
     for (int u = 0; u < WLA; ++u) wl[u] = wl_load(u);
 
-    // activation staging and split: gemm_x6_fl_kernel's
+    // activation staging: lane L splits row L & 7 of the wave's 8 rows,
+    // chunk 8 u + (L >> 3), half hf ^ (chunk & 1) (the conflict-free split
+    // writes of gemm_x6_ws16_kernel), as a float4 register loaded four split
+    // half-units ahead; half-unit q = 2 u + hf of row step k (clamped to the
+    // last step: such rows are split into the unused plane buffer, never read)
     const int sr = lane & 7, sch = lane >> 3, sodd = sch & 1;
     const int soff[2] = {sr * 1024 + 32 * sch + 16 * sodd, sr * 1024 + 32 * sch + 16 * (sodd ^ 1)};
     auto stage_load = [&](int k, int q) {
@@ -1278,8 +773,10 @@ __global__ __launch_bounds__(WS_THREADS, 1) void gemm_x6_fl16_kernel(
         const bf16x8_t bm = __builtin_bit_cast(bf16x8_t, gm);
         const bf16x8_t bl = __builtin_bit_cast(bf16x8_t, gl);
         f32x4_t &d = d2[2 * tt + j];
-        // one asm statement (gemm_x6_fl_kernel's D2 order); s_nop 4 covers
-        // the VALU writes of bh, bm, bl -> SrcB reads
+        // one asm statement: D2 stays in VGPRs (the builtin's accumulator
+        // took AGPRs, evicting a weight fragment with a copy back before each
+        // use, round 5) and no compiler VALU lands between the MFMAs; s_nop 4
+        // covers the VALU writes of bh, bm, bl -> SrcB reads
         asm volatile("s_nop 4\n\t"
                      "v_mfma_f32_16x16x32_bf16 %0, %1, %4, %0\n\t"
                      "v_mfma_f32_16x16x32_bf16 %0, %1, %5, %0\n\t"
@@ -1365,267 +862,6 @@ __global__ __launch_bounds__(WS_THREADS, 1) void gemm_x6_fl16_kernel(
 #pragma unroll
         for (int r = 0; r < 4; ++r) out[(4 * fq + r) * XN + 64 * w + 16 * ct + fc] = d2[ct][r];
 }
-#else
-__global__ __launch_bounds__(WS_THREADS, 1) void gemm_x6_fl_kernel(
-    const float *__restrict__ A, const uint8_t *__restrict__ img, const float *__restrict__ H,
-    const uint8_t *__restrict__ ximg, float *__restrict__ part, int64_t m, int batch) {
-    __shared__ __attribute__((aligned(16))) uint8_t sh[2 * WS_PSTAGE];
-    const int lane = threadIdx.x & 63;
-    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int b = (int)blockIdx.x % batch;
-    const int per = (int)gridDim.x / batch;
-    const int j0 = (int)blockIdx.x / batch;
-    const int steps_net = (int)(m / WS_RS);
-    const int R = (steps_net - j0 + per - 1) / per;
-    const float *Ab = A + (int64_t)b * m * XK;
-    const float *Hb = H + (int64_t)b * m * XN;
-    const int fr = lane & 31, fh = lane >> 5;
-
-    // every load goes through a buffer resource (an SGPR base, one per-lane
-    // offset register, the rest in SGPR / immediate offsets): the address
-    // arithmetic of plain loads cost registers this kernel does not have
-    constexpr int kBufFlags = 0x00020000;
-    const __amdgpu_buffer_rsrc_t wrs =
-        __builtin_amdgcn_make_buffer_rsrc((void *)(img + (int64_t)b * W_IMG), 0, (int)W_IMG,
-                                          kBufFlags);
-    const int lane16 = lane * 16;
-    auto wfrag = [&](int t, int s, int p) {
-        return __builtin_bit_cast(
-            bf16x8_t, __builtin_amdgcn_raw_buffer_load_b128(
-                          wrs, lane16, (((w * 2 + t) * 16 + s) * 3 + p) * W_FRAG, 0));
-    };
-    // the weights' h and m planes in AGPRs (gemm_x6_ws_kernel's layout)
-    bf16x8_t Wa[2][16][2];
-#pragma unroll
-    for (int j = 0; j < 2; ++j)
-#pragma unroll
-        for (int s = 0; s < 16; ++s) {
-            Wa[j][s][0] = wfrag(j, s, 0);
-            Wa[j][s][1] = wfrag(j, s, 1);
-        }
-    // the l plane's fragment of global k16 step g (tile g >> 4, step g & 15):
-    // a ring of 4, loaded two steps ahead
-    auto wl_load = [&](int g) { return wfrag((g >> 4) & 1, g & 15, 2); };
-// the l plane's fragments are loaded FL_WL_AHEAD k16 steps ahead: every
-// vector-memory wait is in issue order, so a fragment load queued behind the
-// HBM loads of h1 / the staging rows waits for them too (2 ahead: 127 us per
-// call, 6 ahead: 118, scripts/micro/r5_flvar.sh, round 5)
-#ifndef FL_WL_AHEAD
-#define FL_WL_AHEAD 6
-#endif
-    constexpr int WLA = FL_WL_AHEAD, WLR = WLA < 4 ? 4 : 8;
-    bf16x8_t wl[WLR];
-#pragma unroll
-    for (int g = 0; g < WLA; ++g) wl[g] = wl_load(g);
-
-    // activation staging: lane L splits row L & 7 of the wave's 8 rows,
-    // chunk 8 u + (L >> 3), half hf ^ (chunk & 1) (the conflict-free split
-    // writes of gemm_x6_ws_kernel), as a float4 register loaded four split
-    // half-units ahead; half-unit q = 2 u + hf of row step k (clamped to the
-    // last step: such rows are split into the unused plane buffer, never read)
-    const int sr = lane & 7, sch = lane >> 3, sodd = sch & 1;
-    // byte offset of the lane's float4 of half-unit hf within the wave's 8 rows
-    const int soff[2] = {sr * 1024 + 32 * sch + 16 * sodd, sr * 1024 + 32 * sch + 16 * (sodd ^ 1)};
-    auto stage_load = [&](int k, int q) {
-        const int kk = k < R ? k : R - 1;
-        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-            (void *)(Ab + ((int64_t)(j0 + kk * per) * WS_RS + 8 * w) * XK), 0, 8 * XK * 4,
-            kBufFlags);
-        return __builtin_bit_cast(
-            float4, __builtin_amdgcn_raw_buffer_load_b128(rs, soff[q & 1], 256 * (q >> 1), 0));
-    };
-    const int wr_base = sch * 512 + (8 * w + sr) * 16;
-    const int wr_half[2] = {wr_base + 8 * sodd, wr_base + 8 * (sodd ^ 1)};
-    auto split_store = [&](int k, int q, const float4 &v) {
-        uint32_t h[2], mm[2], l[2];
-        const float x[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-        for (int p = 0; p < 2; ++p) {
-            const float a = x[2 * p], c = x[2 * p + 1];
-            const uint32_t ph = pk_bf16(a, c);
-            const float ra = a - lo_f(ph), rc = c - hi_f(ph);
-            const uint32_t pm = pk_bf16(ra, rc);
-            h[p] = ph;
-            mm[p] = pm;
-            l[p] = pk_bf16(ra - lo_f(pm), rc - hi_f(pm));
-        }
-        uint8_t *dst = sh + (k & 1) * WS_PSTAGE + wr_half[q & 1] + (q >> 1) * 8 * 512;
-        typedef uint32_t u32x2_t __attribute__((ext_vector_type(2)));
-        *reinterpret_cast<u32x2_t *>(dst) = (u32x2_t){h[0], h[1]};
-        *reinterpret_cast<u32x2_t *>(dst + WS_PLANE) = (u32x2_t){mm[0], mm[1]};
-        *reinterpret_cast<u32x2_t *>(dst + 2 * WS_PLANE) = (u32x2_t){l[0], l[1]};
-    };
-    typedef bf16x8_t AFrag[3];
-    const int fr_base = fh * 512 + fr * 16;
-    auto read_frag = [&](int k, int s, AFrag &f) {
-        const uint8_t *src = sh + (k & 1) * WS_PSTAGE + fr_base + s * 1024;
-#pragma unroll
-        for (int p = 0; p < 3; ++p) f[p] = *reinterpret_cast<const bf16x8_t *>(src + p * WS_PLANE);
-    };
-    f32x16_t acc_h[2], acc_l[2];
-#pragma unroll
-    for (int t = 0; t < 2; ++t) {
-        acc_h[t] = (f32x16_t){};
-        acc_l[t] = (f32x16_t){};
-    }
-    auto finish_tile = [&](int t) {
-        asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
-        acc_h[t] = acc_h[t] + acc_l[t];
-    };
-
-    // ---- the epilogue: grad_z1 of tile tt of row step kk into D2 ----
-    f32x16_t d2 = (f32x16_t){};
-    // FL_H_EARLY (A/B knob): the epilogue's h1 rows loaded one phase ahead,
-    // tile t's in hb[t] (loaded while tile t's MFMAs run, read by the next
-    // phase).  Round 5: 123-125 vs 125-127 us alone, 117-121 vs 115-118 us
-    // beside FL_WL_AHEAD 6 -- no gain, off
-#ifndef FL_H_EARLY
-#define FL_H_EARLY 0
-#endif
-    float hb[FL_H_EARLY ? 2 : 1][16];
-    const int hoff[2] = {(4 * fh * XN + 64 * w + fr) * 4, (4 * fh * XN + 64 * w + 32 + fr) * 4};
-    auto h_load = [&](int kk, int tt, int r) {
-        float *hv = hb[FL_H_EARLY ? tt : 0];
-        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-            (void *)(Hb + (int64_t)(j0 + kk * per) * WS_RS * XN), 0, WS_RS * XN * 4, kBufFlags);
-        hv[r] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(
-            rs, hoff[tt], (8 * (r >> 2) + (r & 3)) * XN * 4, 0));
-    };
-    // lane (m = fr, fh) of X^T's fragment: feature fr & 15 of column tile
-    // fr >> 4; the other tile's lanes load from past the record's end, which
-    // the buffer range check returns as zeros
-    const int xoff[2] = {(fr >> 4) == 0 ? xrec_off(0, 0, fh, fr & 15) : 0x7ff00000,
-                         (fr >> 4) == 1 ? xrec_off(0, 0, fh, fr & 15) : 0x7ff00000};
-    auto x_frag = [&](int kk, int tt, int j, bf16x8_t (&xf)[3]) {
-        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-            (void *)(ximg + (int64_t)(j0 + kk * per) * XREC), 0, XREC, kBufFlags);
-#pragma unroll
-        for (int p = 0; p < 3; ++p)
-            xf[p] = __builtin_bit_cast(bf16x8_t, __builtin_amdgcn_raw_buffer_load_b128(
-                                                     rs, xoff[tt], (p * 2 + j) * 512, 0));
-    };
-    // grad_z1 = grad_h1 (1 - h1^2) (first_layer_bwd_kernel's expression) of
-    // registers 8 j .. 8 j + 7 of tile tt, split into the B fragment planes,
-    // and the six x6 products into D2
-    auto d2_kstep = [&](int tt, int j, const bf16x8_t (&xf)[3]) {
-        float gz[8];
-#pragma unroll
-        for (int e = 0; e < 8; ++e) {
-            const float y = hb[FL_H_EARLY ? tt : 0][8 * j + e];
-            gz[e] = acc_h[tt][8 * j + e] * (1.0f - y * y);
-        }
-        u32x4_t gh, gm, gl;
-        split8(gz, gh, gm, gl);
-        const bf16x8_t bh = __builtin_bit_cast(bf16x8_t, gh);
-        const bf16x8_t bm = __builtin_bit_cast(bf16x8_t, gm);
-        const bf16x8_t bl = __builtin_bit_cast(bf16x8_t, gl);
-        // one asm statement: D2 stays in VGPRs (the builtin's accumulator
-        // took 16 AGPRs, evicting a weight fragment to VGPRs and a copy back
-        // before each use), and no compiler VALU lands between the MFMAs;
-        // s_nop 4 covers the VALU writes of bh, bm, bl -> SrcB reads
-        asm volatile("s_nop 4\n\t"
-                     "v_mfma_f32_32x32x16_bf16 %0, %1, %4, %0\n\t"
-                     "v_mfma_f32_32x32x16_bf16 %0, %1, %5, %0\n\t"
-                     "v_mfma_f32_32x32x16_bf16 %0, %2, %4, %0\n\t"
-                     "v_mfma_f32_32x32x16_bf16 %0, %1, %6, %0\n\t"
-                     "v_mfma_f32_32x32x16_bf16 %0, %3, %4, %0\n\t"
-                     "v_mfma_f32_32x32x16_bf16 %0, %2, %5, %0"
-                     : "+v"(d2)
-                     : "v"(xf[0]), "v"(xf[1]), "v"(xf[2]), "v"(bh), "v"(bm), "v"(bl));
-    };
-
-    // ---- prologue: step 0's planes, the staging ring for step 1 ----
-    {
-        float4 v0[8];
-#pragma unroll
-        for (int q = 0; q < 8; ++q) v0[q] = stage_load(0, q);
-#pragma unroll
-        for (int q = 0; q < 8; ++q) split_store(0, q, v0[q]);
-    }
-    float4 stg[4];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) stg[q] = stage_load(1, q);
-    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-    if (FL_H_EARLY) {
-        // row step 0's phase-0 epilogue is of the zeroed tile 1: finite rows
-#pragma unroll
-        for (int r = 0; r < 16; ++r) h_load(0, 1, r);
-    }
-    constexpr int NF = 3;                     // fragment sets (two steps ahead)
-    AFrag fb[NF];
-    read_frag(0, 0, fb[0]);
-    read_frag(0, 1, fb[1]);
-    bf16x8_t xf0[3], xf1[3];
-
-    // Row step k, per wave: phase t runs column tile t's 16 k16 steps (96 x6
-    // MFMAs) and the epilogue of the other tile (tile 1 of step k - 1 in
-    // phase 0, tile 0 of step k in phase 1): its h1 rows loaded at k16 steps
-    // 0..7, X fragments of K step 0 at 2 and of K step 1 at 8, grad_z1 and
-    // the D2 MFMAs of K step 0 at 9 and of K step 1 at 13.  Split half-unit
-    // q of step k + 1 at steps 4 q' + 1 (q' = q - 4 t), the staging load of
-    // half-unit q + 4 behind it.  Step 0's phase-0 epilogue is of the zeroed
-    // tile 1: D2 += 0.
-    auto row_step = [&](int k) {
-#pragma unroll
-        for (int t = 0; t < 2; ++t) {
-            const int tt = 1 - t;
-            const int kk = t == 0 ? (k > 0 ? k - 1 : 0) : k;
-            finish_tile(tt);
-#pragma unroll
-            for (int s = 0; s < 16; ++s) {
-                const int g = 16 * t + s;
-                if (g + 2 < 32) read_frag(k, (g + 2) & 15, fb[(g + 2) % NF]);
-                wl[(g + WLA) % WLR] = wl_load(g + WLA);
-                const AFrag &x = fb[g % NF];
-                mfma_x6_group(s == 0, acc_h[t], acc_l[t], x[0], x[1], x[2], Wa[t][s][0],
-                              Wa[t][s][1], wl[g % WLR]);
-                if (s < 8) {
-                    if (FL_H_EARLY) {
-                        h_load(k, t, 2 * s);          // the next phase's epilogue
-                        h_load(k, t, 2 * s + 1);
-                    } else {
-                        h_load(kk, tt, 2 * s);
-                        h_load(kk, tt, 2 * s + 1);
-                    }
-                }
-                if (s == 2) x_frag(kk, tt, 0, xf0);
-                if (s == 6) x_frag(kk, tt, 1, xf1);
-                if (s == 9) d2_kstep(tt, 0, xf0);
-                if (s == 13) d2_kstep(tt, 1, xf1);
-                if ((s & 3) == 1) {
-                    const int q = 4 * t + (s >> 2);
-                    split_store(k + 1, q, stg[q & 3]);
-                    stg[q & 3] = stage_load(q + 4 < 8 ? k + 1 : k + 2, (q + 4) & 7);
-                }
-            }
-        }
-        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-        read_frag(k + 1, 0, fb[0]);
-        read_frag(k + 1, 1, fb[1]);
-    };
-    for (int k = 0; k < R; ++k) row_step(k);
-    // tile 1 of the last row step
-    if (R > 0) {
-        finish_tile(1);
-#pragma unroll
-        for (int r = 0; r < 16; ++r)
-            if (!FL_H_EARLY) h_load(R - 1, 1, r);
-        x_frag(R - 1, 1, 0, xf0);
-        x_frag(R - 1, 1, 1, xf1);
-        d2_kstep(1, 0, xf0);
-        d2_kstep(1, 1, xf1);
-    }
-    // D2 -> this block's partial row (first_layer_bwd_kernel's layout:
-    // [feature * 256 + column], row j0 * batch + b)
-    float *out = part + ((int64_t)j0 * batch + b) * (FL_F * XN);
-    asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");   // D2's asm MFMA writes
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-        const int mrow = 8 * (r >> 2) + 4 * fh + (r & 3);
-        out[(mrow & 15) * XN + 64 * w + 32 * (mrow >> 4) + fr] = d2[r];
-    }
-}
-#endif  // X6_MFMA16
 
 int fail_g(int code, const std::string &msg) {
     set_global_error(msg);
@@ -1647,7 +883,7 @@ int gemm_x6_split_x_launch(int64_t m, int k, const float *x, void *ximg, hipStre
 }
 
 // returns the blocks per net (the partial rows written), or -1
-// blocks per net of gemm_x6_fl_kernel at m rows (its partial rows)
+// blocks per net of gemm_x6_fl16_kernel at m rows (its partial rows)
 int gemm_x6_fl_rows(int batch, int64_t m) {
     const int n_cu = device_cu_count();
     const int units = (int)(batch * (m / WS_RS));
@@ -1659,12 +895,7 @@ int gemm_x6_fl_rows(int batch, int64_t m) {
 int gemm_x6_fl_launch(int batch, int64_t m, const float *gz, const void *img, const float *h,
                       const void *ximg, float *part, hipStream_t st) {
     const int grid = gemm_x6_fl_rows(batch, m) * batch;
-#if X6_MFMA16
-    constexpr auto fl_kernel = gemm_x6_fl16_kernel;
-#else
-    constexpr auto fl_kernel = gemm_x6_fl_kernel;
-#endif
-    hipLaunchKernelGGL(fl_kernel, dim3(grid), dim3(WS_THREADS), 0, st, gz,
+    hipLaunchKernelGGL(gemm_x6_fl16_kernel, dim3(grid), dim3(WS_THREADS), 0, st, gz,
                        static_cast<const uint8_t *>(img), h, static_cast<const uint8_t *>(ximg),
                        part, m, batch);
     return hipGetLastError() == hipSuccess ? grid / batch : -1;
@@ -1710,9 +941,9 @@ int dr_gemm_x6(int64_t batch, int64_t m, const float *a, const void *img, float 
     int grid = units < n_cu ? units : n_cu;
     grid -= grid % (int)batch;
     // plain stores: the next kernel reads C back from the Infinity Cache
-    // (round 5: the streamed-l-plane form of gemm_x6_fl_kernel without its
+    // (round 5: the streamed-l-plane form of the fused kernel without its
     // epilogue, 112-113 vs 103-109 us for this kernel, bitwise the same C)
-    hipLaunchKernelGGL(X6_MFMA16 ? gemm_x6_ws16_kernel : gemm_x6_ws_kernel, dim3(grid),
+    hipLaunchKernelGGL(gemm_x6_ws16_kernel, dim3(grid),
                        dim3(WS_THREADS), 0,
                        static_cast<hipStream_t>(stream), a, static_cast<const uint8_t *>(img), c,
                        m, (int)batch);
@@ -1730,35 +961,13 @@ int dr_gemm_x6_wgrad(int64_t batch, int64_t m, int64_t chunks, const float *g, c
         return fail_g(DR_ERR_INVALID,
                       "dr_gemm_x6_wgrad: bad arguments (m / chunks a positive multiple of 32; "
                       "pointers 16-byte aligned)");
-#if X6_MFMA16
-    constexpr auto wgrad_kernel = gemm_x6_wgrad16_kernel;
-#else
-    constexpr auto wgrad_kernel = gemm_x6_wgrad_kernel;
-#endif
-    hipLaunchKernelGGL(wgrad_kernel, dim3((unsigned)(batch * 2 * chunks)),
+    hipLaunchKernelGGL(gemm_x6_wgrad16_kernel, dim3((unsigned)(batch * 2 * chunks)),
                        dim3(XTHREADS), 0, static_cast<hipStream_t>(stream), g, h, ws, m,
                        (int)chunks);
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? DR_OK
-                           : fail_g(DR_ERR_HIP, std::string("gemm_x6_wgrad_kernel: ") +
+                           : fail_g(DR_ERR_HIP, std::string("gemm_x6_wgrad16_kernel: ") +
                                                     hipGetErrorString(e));
 }
-
-#if DR_WG_STAMPS
-int dr_x6_diag_wg_stamps(void *host_out, size_t bytes) {
-    if (bytes < sizeof(g_wg_st)) return DR_ERR_INVALID;
-    return hipMemcpyFromSymbol(host_out, HIP_SYMBOL(g_wg_st), sizeof(g_wg_st)) == hipSuccess
-               ? DR_OK
-               : DR_ERR_HIP;
-}
-#endif
-#if DR_WS_STAMPS
-int dr_x6_diag_stamps(void *host_out, size_t bytes) {
-    if (bytes < sizeof(g_ws_st)) return DR_ERR_INVALID;
-    return hipMemcpyFromSymbol(host_out, HIP_SYMBOL(g_ws_st), sizeof(g_ws_st)) == hipSuccess
-               ? DR_OK
-               : DR_ERR_HIP;
-}
-#endif
 
 }  // extern "C"

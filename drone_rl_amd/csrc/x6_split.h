@@ -50,27 +50,14 @@ constexpr int64_t W_IMG = (int64_t)3 * XN * XK * 2;   // 384 KB per net: 3 bf16 
 constexpr int64_t W_FRAG = 64 * 16;     // one plane fragment: 1 KB
 
 // Weight image of `batch` nets in the weight-stationary kernel's register
-// order: img[b][w][j][s][p][lane][16 B] is the MFMA B fragment of plane p of
-// Bt (= W for transpose 0, W^T for transpose 1; W (256, 256) row-major per
-// net) for wave w's column tile j and k16 step s: lane = fr + 32 fh holds
-// Bt[n = 64 w + 32 j + fr][k = 16 s + 8 fh .. + 7], so each fragment is one
-// coalesced 1-KB load.
-//
-// X6_MFMA16 (round 6): the fragments of v_mfma_f32_16x16x32_bf16 instead:
-// img[b][w][ct][s][p][lane][16 B], lane = c + 16 q holds
-// Bt[n = 64 w + 16 ct + c][k = 32 s + 8 q .. + 7] (4 column tiles of 16 x 8
-// k32 steps per wave; the same 1-KB fragments, the same image size).
-#ifndef X6_MFMA16
-#define X6_MFMA16 0
-#endif
+// order: img[b][w][ct][s][p][lane][16 B] is the v_mfma_f32_16x16x32_bf16 B
+// fragment of plane p of Bt (= W for transpose 0, W^T for transpose 1; W
+// (256, 256) row-major per net) for wave w's column tile ct and k32 step s:
+// lane = c + 16 q holds Bt[n = 64 w + 16 ct + c][k = 32 s + 8 q .. + 7], so
+// each fragment is one coalesced 1-KB load.
 __host__ __device__ inline int64_t wimg_off(int n, int k0) {
-#if X6_MFMA16
     const int w = n >> 6, ct = (n >> 4) & 3, c = n & 15, s = k0 >> 5, q = (k0 >> 3) & 3;
     return ((int64_t)((w * 4 + ct) * 8 + s) * 3 * 64 + c + 16 * q) * 16;
-#else
-    const int w = n >> 6, j = (n >> 5) & 1, fr = n & 31, s = k0 >> 4, fh = (k0 >> 3) & 1;
-    return ((int64_t)((w * 2 + j) * 16 + s) * 3 * 64 + fr + 32 * fh) * 16;
-#endif
 }
 
 // Item t (b, n, 8-k chunk) of the weight image; transpose 2 builds both forms
@@ -100,8 +87,7 @@ __device__ inline void split_weights_item(const float *__restrict__ w, int trans
 // The first-layer observation image of the fused input-gradient GEMM
 // (gemm_x6_fl_kernel): per row step a record of X^T's A fragments.
 constexpr int FL_F = 16;                                // 15 features + the bias column
-#if X6_MFMA16
-// X6_MFMA16 (gemm_x6_fl16_kernel): one v_mfma_f32_16x16x32_bf16 A fragment
+// One v_mfma_f32_16x16x32_bf16 A fragment
 // per plane and row step, K = the step's 32 rows: lane L = f + 16 q holds
 // feature f of rows 4 q + e (e < 4, row tile 0) and 16 + 4 q + e - 4 (e >= 4,
 // row tile 1) -- the rows the main GEMM's 16 x 16 accumulators of the two
@@ -128,40 +114,5 @@ __device__ inline void split_x_item(const float *__restrict__ x, const int32_t *
     *reinterpret_cast<u32x4_t *>(rec + xrec_off(1, L)) = mm;
     *reinterpret_cast<u32x4_t *>(rec + xrec_off(2, L)) = l;
 }
-#else
-constexpr int XREC = 64 + 3 * 2 * 2 * FL_F * 16;         // 3,136 B of X planes per row step
-
-// byte offset in a row step's X record of plane p, K step j, half fh,
-// feature f: the 8 bf16 K values of A-fragment lane (f or 16 + f, fh)
-__host__ __device__ inline int xrec_off(int p, int j, int fh, int f) {
-    return 64 + (((p * 2 + j) * 2 + fh) * FL_F + f) * 16;
-}
-
-// Item t = (row step g, K step j, half fh, feature f): the rows 16 j + 4 fh +
-// (e & 3) + 8 (e >> 2), e = 0..7, of feature f of x (m x k f32 row-major,
-// row r read as x[rows[r]] when rows is given; feature 15 is the constant
-// 1), split exactly like the GEMM operands; the record's first 64 B are zero
-// (the A fragment of the other column tile's lanes).
-__device__ inline void split_x_item(const float *__restrict__ x, const int32_t *__restrict__ rows,
-                                    int64_t m, int k, uint8_t *__restrict__ img, int64_t t) {
-    const int64_t g = t >> 6;
-    if (g >= m / X6_RS) return;
-    const int f = (int)(t & 15), fh = (int)((t >> 4) & 1), j = (int)((t >> 5) & 1);
-    uint8_t *rec = img + g * XREC;
-    if ((t & 63) < 4) reinterpret_cast<u32x4_t *>(rec)[t & 3] = (u32x4_t){0u, 0u, 0u, 0u};
-    float v[8];
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {
-        const int64_t row = g * X6_RS + 16 * j + 4 * fh + (e & 3) + 8 * (e >> 2);
-        const int64_t src = rows ? (int64_t)rows[row] : row;
-        v[e] = f < k ? x[src * k + f] : (f == FL_F - 1 ? 1.0f : 0.0f);
-    }
-    u32x4_t h, mm, l;
-    split8(v, h, mm, l);
-    *reinterpret_cast<u32x4_t *>(rec + xrec_off(0, j, fh, f)) = h;
-    *reinterpret_cast<u32x4_t *>(rec + xrec_off(1, j, fh, f)) = mm;
-    *reinterpret_cast<u32x4_t *>(rec + xrec_off(2, j, fh, f)) = l;
-}
-#endif
 
 }  // namespace dr

@@ -26,9 +26,10 @@ def test_committed_kernel_stats_cover_every_ppo_kernel():
     # round 4's summary: the unfused step; round 5's: the default step (the
     # first layer's backward inside the input-gradient GEMM, the operand
     # images built by the first layer's forward launch)
-    # (round 6's record gather and 16x16x32 forward GEMM postdate both)
+    # (round 6's record gather and 16x16x32 GEMMs postdate both)
     fused_away = {"split_x_kernel", "split_weights_kernel", "first_layer_bwd_kernel"}
-    newer = {"gather_records_kernel", "gemm_x6_ws16_kernel"}
+    newer = {"gather_records_kernel", "gemm_x6_ws16_kernel", "gemm_x6_fl16_kernel",
+             "gemm_x6_wgrad16_kernel"}
     r4 = bench.rocprof_averages(os.path.join(ROOT, "profiles", "r04_kernel_stats.csv"))
     for k in set(bench.PPO_KERNEL_NAMES.values()) - {"split_x_kernel", "gemm_x6_fl_kernel"} - newer:
         assert k in r4 and r4[k] > 0, k
@@ -41,7 +42,7 @@ def test_committed_kernel_stats_cover_every_ppo_kernel():
 def test_ppo_roofline_carries_rocprof_durations_and_fractions():
     class Cfg:
         batch_size, num_envs, n_steps, n_epochs = 65536, 65536, 32, 10
-    rp = {"gemm_x6_ws_kernel": 80.0, "linear_tanh_kernel": 30.0}
+    rp = {"gemm_x6_ws16_kernel": 80.0, "linear_tanh_kernel": 30.0}
     out = bench.ppo_roofline(Cfg, 0.15, {"gemm_x6_fwd": 100.0, "linear_tanh": 35.0,
                                          "grad_finish_clip_adam": 10.0}, rp,
                              {"gemm_x6_fwd": 90.0}, "profiles/x.csv")
@@ -79,30 +80,33 @@ def test_ppo_roofline_without_rocprof_picks_the_largest_prefix_split():
 
 
 def test_dominant_kernel_follows_the_stats_csv(tmp_path):
-    """verdict r05 item 4: the selection follows the committed rocprofv3
-    summary -- round 5's names the fused input-gradient kernel (111 us),
-    and a summary where the forward GEMM is the slowest names that one."""
+    """verdict r05 item 4: the selection follows the rocprofv3 summary it is
+    given -- one where the fused input-gradient kernel is the slowest names
+    it, one where the forward GEMM is the slowest names that one."""
     class Cfg:
         batch_size, num_envs, n_steps, n_epochs = 65536, 65536, 32, 10
     steps = {"gather_minibatch": 7.0, "linear_tanh": 37.0, "gemm_x6_fwd": 110.0,
              "ppo_head": 51.0, "gemm_x6_bwd_first": 100.0, "gemm_x6_wgrad": 86.0,
              "grad_finish_clip_adam": 15.0}
-    rp = bench.rocprof_averages(os.path.join(ROOT, "profiles", "r05_kernel_stats.csv"))
-    d = bench.ppo_roofline(Cfg, 0.14, steps, rp, {}, "r05")["dominant_kernel"]
-    assert d["step"] == "gemm_x6_bwd_first" and d["kernel"] == "gemm_x6_fl_kernel"
+
+    def stats(path, fl_ns, fwd_ns):
+        with open(path, "w", newline="") as f:
+            w = csv.DictWriter(f, ["Name", "Calls", "TotalDurationNs", "AverageNs",
+                                   "Percentage"])
+            w.writeheader()
+            for name, ns in ((bench.PPO_KERNEL_NAMES["gemm_x6_bwd_first"], fl_ns),
+                             (bench.PPO_KERNEL_NAMES["gemm_x6_fwd"], fwd_ns),
+                             ("ppo_head_kernel", 50000)):
+                w.writerow({"Name": "dr::(anonymous namespace)::%s(float const*)" % name,
+                            "Calls": 10, "TotalDurationNs": 10 * ns, "AverageNs": ns,
+                            "Percentage": 1})
+        return bench.rocprof_averages(str(path))
+    rp = stats(tmp_path / "a.csv", 111140, 88000)
+    d = bench.ppo_roofline(Cfg, 0.14, steps, rp, {}, "a")["dominant_kernel"]
+    assert d["step"] == "gemm_x6_bwd_first" and d["kernel"] == "gemm_x6_fl16_kernel"
     assert abs(d["us"] - 111.14) < 0.01 and abs(d["frac"] - 0.394) < 0.002
-    p = tmp_path / "stats.csv"
-    with open(p, "w", newline="") as f:
-        w = csv.DictWriter(f, ["Name", "Calls", "TotalDurationNs", "AverageNs", "Percentage"])
-        w.writeheader()
-        for name, ns in (("dr::(anonymous namespace)::gemm_x6_fl_kernel(float const*)", 90000),
-                         ("dr::(anonymous namespace)::%s(float const*)"
-                          % bench.PPO_KERNEL_NAMES["gemm_x6_fwd"], 120000),
-                         ("dr::(anonymous namespace)::ppo_head_kernel(HeadArgs)", 50000)):
-            w.writerow({"Name": name, "Calls": 10, "TotalDurationNs": 10 * ns,
-                        "AverageNs": ns, "Percentage": 1})
-    rp = bench.rocprof_averages(str(p))
-    d = bench.ppo_roofline(Cfg, 0.14, steps, rp, {}, str(p))["dominant_kernel"]
+    rp = stats(tmp_path / "b.csv", 90000, 120000)
+    d = bench.ppo_roofline(Cfg, 0.14, steps, rp, {}, "b")["dominant_kernel"]
     assert d["step"] == "gemm_x6_fwd" and d["us"] == 120.0
 
 

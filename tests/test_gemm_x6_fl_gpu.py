@@ -1,6 +1,6 @@
 """dr_gemm_x6_bwd_first (round 5): the 256 x 256 layer's input gradient with
 the first layer's backward fused into its epilogue (csrc/gemm_x6.hip
-gemm_x6_fl_kernel).  Checked against an f64 reference of the same math --
+gemm_x6_fl16_kernel).  Checked against an f64 reference of the same math --
 grad_z1 = (grad_z2 W1) (1 - h1^2), dW0 = grad_z1^T x, db0 = sum grad_z1 --
 within the fp32 reduction-order bound the flagship PPO parity test uses
 (Higham gamma_n sum |terms|), next to the unfused path (dr_gemm_x6 +
@@ -42,6 +42,10 @@ def _bf16_to_f64(u16):
 
 @pytest.mark.parametrize("m", [128, 384, 65536])
 def test_split_x_is_an_exact_three_plane_split(m):
+    """The observation image of the fused kernel (x6_split.h split_x_item):
+    per 32-row step three planes of 64 lanes x 8 bf16, lane f + 16 q holding
+    feature f (15: the constant 1) of rows 4 q + e (e < 4) and 16 + 4 q + e - 4
+    (e >= 4); the planes sum exactly to x."""
     L = _lib.lib()
     g = torch.Generator().manual_seed(m)
     x = (torch.randn(m, 15, generator=g) * torch.exp(torch.randn(m, 15, generator=g) * 3)).cuda()
@@ -49,16 +53,16 @@ def test_split_x_is_an_exact_three_plane_split(m):
     check(L.dr_gemm_x6_split_x(m, 15, ptr(x), ptr(img), torch.cuda.current_stream().cuda_stream))
     torch.cuda.synchronize()
     rec = img.cpu().numpy().reshape(m // 32, -1)
-    assert rec.shape[1] == 3136 and not rec[:, :64].any()          # zero header
-    planes = rec[:, 64:].view(np.uint16).reshape(m // 32, 3, 2, 2, 16, 8)   # p, j, fh, f, e
-    val = sum(_bf16_to_f64(planes[:, p]) for p in range(3))           # (g, j, fh, f, e)
+    assert rec.shape[1] == 3072
+    planes = rec.view(np.uint16).reshape(m // 32, 3, 4, 16, 8)       # p, q, f, e
+    val = sum(_bf16_to_f64(planes[:, p]) for p in range(3))           # (g, q, f, e)
     e = np.arange(8)
-    rows = (16 * np.arange(2)[:, None, None] + 4 * np.arange(2)[None, :, None] +
-            (e & 3)[None, None, :] + 8 * (e >> 2)[None, None, :])      # (j, fh, e)
+    rows = np.where(e[None, :] < 4, 4 * np.arange(4)[:, None] + e[None, :],
+                    16 + 4 * np.arange(4)[:, None] + e[None, :] - 4)  # (q, e)
     xs = x.double().cpu().numpy().reshape(m // 32, 32, 15)
-    ref = np.ones((m // 32, 2, 2, 16, 8))
+    ref = np.ones((m // 32, 4, 16, 8))
     for f in range(15):
-        ref[:, :, :, f, :] = xs[:, rows, f]
+        ref[:, :, f, :] = xs[:, rows, f]
     assert np.array_equal(val, ref)
 
 

@@ -23,11 +23,12 @@ import pytest
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 SRC = os.path.join(ROOT, "drone_rl_amd", "csrc", "gemm_x6.hip")
 # the weight-stationary GEMM and (round 5) its first-layer-backward form
-# (round 6: the 16x16x32 forms, the fused one compiled with X6_MFMA16=1)
-KERNELS = (("gemm_x6_ws_kernel", 0), ("gemm_x6_fl_kernel", 0), ("gemm_x6_ws16_kernel", 0),
-           ("gemm_x6_fl16_kernel", 1))
-# XDL (v_mfma_f32_32x32x16_bf16, 8 passes on gfx950) write VGPR -> VALU, VMEM
-# or LDS access of it: 11 wait states on gfx940-class parts; checked with margin
+# the weight-stationary forward and its first-layer-backward form (round 6:
+# both on v_mfma_f32_16x16x32_bf16)
+KERNELS = ("gemm_x6_ws16_kernel", "gemm_x6_fl16_kernel")
+# XDL write VGPR -> VALU, VMEM or LDS access of it: 11 wait states for an
+# 8-pass XDL op on gfx940-class parts (v_mfma_f32_16x16x32_bf16 has fewer
+# passes); checked with margin
 WAIT = 18
 # VALU (or v_accvgpr_write) write of a VGPR / AGPR -> an MFMA reading it as
 # SrcA / SrcB / SrcC: 2 wait states on gfx940-class parts (the CDNA3/4 ISA
@@ -57,10 +58,10 @@ def _any_regs(text):
 _ASM = {}
 
 
-def _kernel_asm(kernel, m16=0):
-    if m16 not in _ASM:
-        _ASM[m16] = _compile(m16)
-    s = _ASM[m16]
+def _kernel_asm(kernel):
+    if "s" not in _ASM:
+        _ASM["s"] = _compile()
+    s = _ASM["s"]
     name = next(l.split(":")[0] for l in s.splitlines()
                 if kernel in l.split(":")[0] and re.match(r"^[_A-Za-z0-9]+:", l))
     a = s.index(name + ":")
@@ -68,7 +69,7 @@ def _kernel_asm(kernel, m16=0):
     return s[a:b].splitlines()
 
 
-def _compile(m16=0):
+def _compile():
     hipcc = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
     if not os.path.exists(hipcc):
         pytest.skip("hipcc not available")
@@ -77,7 +78,6 @@ def _compile(m16=0):
         out = subprocess.run(
             [hipcc, "-O3", "-std=c++17", "-fPIC", "--offload-arch=gfx950", "-ffp-contract=off",
              "-fno-fast-math", "-fno-slp-vectorize", "-I", os.path.join(ROOT, "include"),
-             f"-DX6_MFMA16={m16}",
              "--cuda-device-only", "-S", SRC, "-o", asm],
             capture_output=True, text=True, timeout=300)
         assert out.returncode == 0, out.stderr[-2000:]
@@ -181,8 +181,8 @@ def test_scanner_flags_an_operand_written_right_before_an_asm_mfma():
     assert any("reads v178" in b for b in bad) and any("reads a77" in b for b in bad)
 
 
-@pytest.mark.parametrize("kernel,m16", KERNELS)
-def test_no_compiler_access_to_asm_mfma_results_without_wait_states(kernel, m16):
-    n_mfma, bad = _scan(_kernel_asm(kernel, m16))
+@pytest.mark.parametrize("kernel", KERNELS)
+def test_no_compiler_access_to_asm_mfma_results_without_wait_states(kernel):
+    n_mfma, bad = _scan(_kernel_asm(kernel))
     assert n_mfma >= 192, f"expected the kernel's asm MFMAs, found {n_mfma}"
     assert not bad, "\n".join(bad[:20])
