@@ -30,9 +30,9 @@ res = {"workload": "scripts/micro/gemm_x6_bench.py --reps 10 (both nets, 65,536 
                    "and input-gradient forms of dr_gemm_x6 and the 64-chunk weight gradient; cold "
                    "inputs), rocprofv3 --pmc, two passes (scripts/micro/gemm_x6_pmc.sh); "
                    "per-dispatch averages per kernel"}
-for key, pat in (("gemm_x6_ws_kernel", r"gemm_x6_ws_kernel"),
-                 ("gemm_x6_wgrad_kernel", r"gemm_x6_wgrad_kernel"),
-                 ("gemm_x6_fl_kernel", r"gemm_x6_fl_kernel"),
+for key, pat in (("gemm_x6_ws16_kernel", r"gemm_x6_ws16_kernel"),
+                 ("gemm_x6_wgrad16_kernel", r"gemm_x6_wgrad16_kernel"),
+                 ("gemm_x6_fl16_kernel", r"gemm_x6_fl16_kernel"),
                  ("ppo_head_kernel", r"ppo_head_kernel")):
     acc = collections.defaultdict(list)
     for f in glob.glob(out + "/p*/run_counter_collection.csv"):

@@ -1,7 +1,7 @@
 # round 6: the 16x16x32-only library -- new x6 digests, the GPU suite, a bench
 set -o pipefail
 mkdir -p gpurun_out/r6e
-for a in "384 1" "65536 64"; do timeout -k 10 120 python tests/x6_forms_worker.py $a || exit 1; done
+for a in "384 1" "65536 64"; do PYTHONPATH=$PWD timeout -k 10 120 python tests/x6_forms_worker.py $a || exit 1; done
 timeout -k 10 900 python -u -m pytest tests -m gpu -q --timeout 300 --timeout-method thread > gpurun_out/r6e/gpu_tests.log 2>&1
 echo "tests rc=$?"; grep -E "passed|failed|FAILED|Error" gpurun_out/r6e/gpu_tests.log | tail -15
 grep -q "Memory access fault\|core dumped" gpurun_out/r6e/gpu_tests.log && exit 1
