@@ -131,6 +131,63 @@ __device__ inline void mfma16_first(f32x4_t &d, const bf16x8_t &x, const bf16x8_
     asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, 0" : "=&v"(d) : "v"(x), "a"(w));
 }
 
+// The split of one staged half-unit (a, b, c, d -> the h, m, l planes of the
+// pairs (a, b), (c, d)) as 12 pieces of at most two VALU instructions, each
+// issued as its own asm statement right behind one of a k32 step's MFMAs, so
+// that it runs in that MFMA's issue shadow (an MFMA holds the SIMD's vector
+// issue for 8 of its 16 cycles; two 4-cycle VALU fit the rest,
+// MI355X_MICROARCH.md cycle constants) instead of as one block between MFMA
+// groups.  Bitwise the C++ split (pk_bf16 = v_cvt_pk_bf16_f32, lo_f / hi_f
+// = shift / mask, plain f32 subtractions).
+#ifndef X6_SPLIT_ASM
+#define X6_SPLIT_ASM 1
+#endif
+#ifndef X6_MEM_SPREAD
+#define X6_MEM_SPREAD 1
+#endif
+struct SplitHU {
+    float a, b, c, d;
+    uint32_t h0, h1, m0, m1, l0, l1;
+};
+__device__ inline void sp_cvt(uint32_t &o, float i0, float i1) {
+    asm volatile("v_cvt_pk_bf16_f32 %0, %1, %2" : "=v"(o) : "v"(i0), "v"(i1));
+}
+__device__ inline void sp_cvt2(uint32_t &o0, uint32_t &o1, float i0, float i1, float i2,
+                               float i3) {
+    asm volatile("v_cvt_pk_bf16_f32 %0, %2, %3\n\tv_cvt_pk_bf16_f32 %1, %4, %5"
+                 : "=&v"(o0), "=v"(o1)
+                 : "v"(i0), "v"(i1), "v"(i2), "v"(i3));
+}
+__device__ inline void sp_sublo(float &r, uint32_t h) {     // r -= lo_f(h)
+    uint32_t t;
+    asm volatile("v_lshlrev_b32 %1, 16, %2\n\tv_sub_f32 %0, %0, %1"
+                 : "+v"(r), "=&v"(t)
+                 : "v"(h));
+}
+__device__ inline void sp_subhi(float &r, uint32_t h) {     // r -= hi_f(h)
+    uint32_t t;
+    asm volatile("v_and_b32 %1, 0xffff0000, %2\n\tv_sub_f32 %0, %0, %1"
+                 : "+v"(r), "=&v"(t)
+                 : "v"(h));
+}
+__device__ inline void split_piece(SplitHU &u, int i) {
+    switch (i) {
+    case 0: sp_cvt(u.h0, u.a, u.b); break;
+    case 1: sp_cvt(u.h1, u.c, u.d); break;
+    case 2: sp_sublo(u.a, u.h0); break;
+    case 3: sp_subhi(u.b, u.h0); break;
+    case 4: sp_sublo(u.c, u.h1); break;
+    case 5: sp_subhi(u.d, u.h1); break;
+    case 6: sp_cvt2(u.m0, u.m1, u.a, u.b, u.c, u.d); break;
+    case 7: sp_sublo(u.a, u.m0); break;
+    case 8: sp_subhi(u.b, u.m0); break;
+    case 9: sp_sublo(u.c, u.m1); break;
+    case 10: sp_subhi(u.d, u.m1); break;
+    case 11: sp_cvt2(u.l0, u.l1, u.a, u.b, u.c, u.d); break;
+    default: break;
+    }
+}
+
 __global__ __launch_bounds__(WS_THREADS, 1) void gemm_x6_ws16_kernel(
     const float *__restrict__ A, const uint8_t *__restrict__ img, float *__restrict__ C,
     int64_t m, int batch) {
@@ -217,6 +274,10 @@ __global__ __launch_bounds__(WS_THREADS, 1) void gemm_x6_ws16_kernel(
 #pragma unroll
         for (int p = 0; p < 3; ++p) f[p] = *reinterpret_cast<const bf16x8_t *>(src + p * WS_PLANE);
     };
+    auto read_frag_plane = [&](int k, int g, AFrag &f, int p) {
+        const uint8_t *src = sh + (k & 1) * WS_PSTAGE + fr_base + (g >> 3) * 256 + (g & 7) * 2048;
+        f[p] = *reinterpret_cast<const bf16x8_t *>(src + p * WS_PLANE);
+    };
     // accumulators [row tile][column tile]: hi (h.h) and lo (the five small
     // products)
     f32x4_t acc_h[2][4], acc_l[2][4];
@@ -248,25 +309,42 @@ __global__ __launch_bounds__(WS_THREADS, 1) void gemm_x6_ws16_kernel(
     // the six products of row tile t, k32 step s, for the four column tiles
     // (h += xh.wh; l += xh.wm, xm.wh, xh.wl, xl.wh, xm.wm: per output the
     // order of every x6 kernel), interleaved over the column tiles
-    auto mfma_group = [&](bool first, int t, int s, const AFrag &x) {
+    // extra(i) runs behind MFMA i of the 24 (the split pieces and, with
+    // X6_MEM_SPREAD, the step's fragment reads and stores)
+    auto mfma_group = [&](bool first, int t, int s, const AFrag &x, auto &&extra) {
+        auto piece = [&](int i) { extra(i); };
 #pragma unroll
         for (int ct = 0; ct < 4; ++ct) {
             if (first) mfma16_first(acc_h[t][ct], x[0], Wa[ct][s][0]);
             else mfma16_a(acc_h[t][ct], x[0], Wa[ct][s][0]);
+            piece(ct);
         }
 #pragma unroll
         for (int ct = 0; ct < 4; ++ct) {
             if (first) mfma16_first(acc_l[t][ct], x[0], Wa[ct][s][1]);
             else mfma16_a(acc_l[t][ct], x[0], Wa[ct][s][1]);
+            piece(4 + ct);
         }
 #pragma unroll
-        for (int ct = 0; ct < 4; ++ct) mfma16_a(acc_l[t][ct], x[1], Wa[ct][s][0]);
+        for (int ct = 0; ct < 4; ++ct) {
+            mfma16_a(acc_l[t][ct], x[1], Wa[ct][s][0]);
+            piece(8 + ct);
+        }
 #pragma unroll
-        for (int ct = 0; ct < 4; ++ct) mfma16_v(acc_l[t][ct], x[0], Wv[ct][s]);
+        for (int ct = 0; ct < 4; ++ct) {
+            mfma16_v(acc_l[t][ct], x[0], Wv[ct][s]);
+            piece(12 + ct);
+        }
 #pragma unroll
-        for (int ct = 0; ct < 4; ++ct) mfma16_a(acc_l[t][ct], x[2], Wa[ct][s][0]);
+        for (int ct = 0; ct < 4; ++ct) {
+            mfma16_a(acc_l[t][ct], x[2], Wa[ct][s][0]);
+            piece(16 + ct);
+        }
 #pragma unroll
-        for (int ct = 0; ct < 4; ++ct) mfma16_a(acc_l[t][ct], x[1], Wa[ct][s][1]);
+        for (int ct = 0; ct < 4; ++ct) {
+            mfma16_a(acc_l[t][ct], x[1], Wa[ct][s][1]);
+            piece(20 + ct);
+        }
     };
 
     if (R > 0) issue_rows(0);
@@ -313,22 +391,45 @@ __global__ __launch_bounds__(WS_THREADS, 1) void gemm_x6_ws16_kernel(
             for (int s = 0; s < 8; ++s) {
                 const int g = 8 * t + s;
                 constexpr int D = WS_NF - 1;
-                if (g + D < 16) read_frag(k, g + D, fb[(g + D) % WS_NF]);
                 const int q = 4 * t + (s >> 1);
-                if ((s & 1) == 0) split_read(k + 1, q >> 1, q & 1, v);
-                mfma_group(s == 0, t, s, fb[g % WS_NF]);
-                store_one(ko, 1 - t, 2 * s);
-                store_one(ko, 1 - t, 2 * s + 1);
+                if (!X6_MEM_SPREAD) {
+                    if (g + D < 16) read_frag(k, g + D, fb[(g + D) % WS_NF]);
+                    if ((s & 1) == 0) split_read(k + 1, q >> 1, q & 1, v);
+                }
+                SplitHU u{v.x, v.y, v.z, v.w, 0u, 0u, 0u, 0u, 0u, 0u};
+                // behind the odd MFMAs the split pieces (odd s), behind the
+                // even ones (X6_MEM_SPREAD) one memory instruction each,
+                // pinned by scheduling barriers: the three fragment reads of
+                // k32 step g + D, the two output stores, the staging read
+                auto extra = [&](int i) {
+                    if (X6_SPLIT_ASM && (s & 1) && (i & 1)) split_piece(u, i >> 1);
+                    if (X6_MEM_SPREAD && !(i & 1)) {
+                        const int j = i >> 1;
+                        __builtin_amdgcn_sched_barrier(0);
+                        if (j < 3 && g + D < 16) read_frag_plane(k, g + D, fb[(g + D) % WS_NF], j);
+                        if (j == 3) store_one(ko, 1 - t, 2 * s);
+                        if (j == 4) store_one(ko, 1 - t, 2 * s + 1);
+                        if (j == 5 && (s & 1) == 0) split_read(k + 1, q >> 1, q & 1, v);
+                        __builtin_amdgcn_sched_barrier(0);
+                    }
+                };
+                mfma_group(s == 0, t, s, fb[g % WS_NF], extra);
+                if (!X6_MEM_SPREAD) {
+                    store_one(ko, 1 - t, 2 * s);
+                    store_one(ko, 1 - t, 2 * s + 1);
+                }
                 if ((s & 1) == 1) {
-                    const uint32_t h0 = pk_bf16(v.x, v.y);
-                    float ra = v.x - lo_f(h0), rb = v.y - hi_f(h0);
-                    const uint32_t m0 = pk_bf16(ra, rb);
-                    const uint32_t l0 = pk_bf16(ra - lo_f(m0), rb - hi_f(m0));
-                    const uint32_t h1 = pk_bf16(v.z, v.w);
-                    ra = v.z - lo_f(h1), rb = v.w - hi_f(h1);
-                    const uint32_t m1 = pk_bf16(ra, rb);
-                    const uint32_t l1 = pk_bf16(ra - lo_f(m1), rb - hi_f(m1));
-                    split_store(k + 1, q >> 1, q & 1, h0, h1, m0, m1, l0, l1);
+                    if (!X6_SPLIT_ASM) {
+                        u.h0 = pk_bf16(v.x, v.y);
+                        float ra = v.x - lo_f(u.h0), rb = v.y - hi_f(u.h0);
+                        u.m0 = pk_bf16(ra, rb);
+                        u.l0 = pk_bf16(ra - lo_f(u.m0), rb - hi_f(u.m0));
+                        u.h1 = pk_bf16(v.z, v.w);
+                        ra = v.z - lo_f(u.h1), rb = v.w - hi_f(u.h1);
+                        u.m1 = pk_bf16(ra, rb);
+                        u.l1 = pk_bf16(ra - lo_f(u.m1), rb - hi_f(u.m1));
+                    }
+                    split_store(k + 1, q >> 1, q & 1, u.h0, u.h1, u.m0, u.m1, u.l0, u.l1);
                     if (q & 1) {
                         // unit q >> 1's staging pieces consumed: refill them
                         // with step k + 3 (clamped: such rows are never split)
