@@ -781,6 +781,17 @@ __global__ __launch_bounds__(WS_THREADS, 1) void gemm_x6_fl16_kernel(
             for (int p = 0; p < 3; ++p)
                 f[rt][p] = *reinterpret_cast<const bf16x8_t *>(src + rt * 256 + p * WS_PLANE);
     };
+    auto read_frag_one = [&](int k, int s, AFrag &f, int rt, int p) {
+        const uint8_t *src = sh + (k & 1) * WS_PSTAGE + fr_base + s * 2048;
+        f[rt][p] = *reinterpret_cast<const bf16x8_t *>(src + rt * 256 + p * WS_PLANE);
+    };
+    auto split_store_u = [&](int k, int q, const SplitHU &u) {
+        uint8_t *dst = sh + (k & 1) * WS_PSTAGE + wr_half[q & 1] + (q >> 1) * 8 * 512;
+        typedef uint32_t u32x2_t __attribute__((ext_vector_type(2)));
+        *reinterpret_cast<u32x2_t *>(dst) = (u32x2_t){u.h0, u.h1};
+        *reinterpret_cast<u32x2_t *>(dst + WS_PLANE) = (u32x2_t){u.m0, u.m1};
+        *reinterpret_cast<u32x2_t *>(dst + 2 * WS_PLANE) = (u32x2_t){u.l0, u.l1};
+    };
     // accumulators [phase][row tile][column tile of the phase]
     f32x4_t acc_h[2][2][2], acc_l[2][2][2];
 #pragma unroll
@@ -801,14 +812,17 @@ __global__ __launch_bounds__(WS_THREADS, 1) void gemm_x6_fl16_kernel(
     };
     // the six products of k32 step s for phase t's 2 x 2 tiles, interleaved
     // over the tiles (per output gemm_x6_ws16_kernel's order)
+    // extra(i) runs behind MFMA i of the 24 (split pieces, memory ops)
     auto mfma_group = [&](bool first, int t, int s, const AFrag &x, const bf16x8_t &wl0,
-                          const bf16x8_t &wl1) {
+                          const bf16x8_t &wl1, auto &&extra) {
+        int i = 0;
 #pragma unroll
         for (int rt = 0; rt < 2; ++rt)
 #pragma unroll
             for (int j = 0; j < 2; ++j) {
                 if (first) mfma16_first(acc_h[t][rt][j], x[rt][0], Wa[2 * t + j][s][0]);
                 else mfma16_a(acc_h[t][rt][j], x[rt][0], Wa[2 * t + j][s][0]);
+                extra(i++);
             }
 #pragma unroll
         for (int rt = 0; rt < 2; ++rt)
@@ -816,23 +830,36 @@ __global__ __launch_bounds__(WS_THREADS, 1) void gemm_x6_fl16_kernel(
             for (int j = 0; j < 2; ++j) {
                 if (first) mfma16_first(acc_l[t][rt][j], x[rt][0], Wa[2 * t + j][s][1]);
                 else mfma16_a(acc_l[t][rt][j], x[rt][0], Wa[2 * t + j][s][1]);
+                extra(i++);
             }
 #pragma unroll
         for (int rt = 0; rt < 2; ++rt)
 #pragma unroll
-            for (int j = 0; j < 2; ++j) mfma16_a(acc_l[t][rt][j], x[rt][1], Wa[2 * t + j][s][0]);
+            for (int j = 0; j < 2; ++j) {
+                mfma16_a(acc_l[t][rt][j], x[rt][1], Wa[2 * t + j][s][0]);
+                extra(i++);
+            }
 #pragma unroll
         for (int rt = 0; rt < 2; ++rt)
 #pragma unroll
-            for (int j = 0; j < 2; ++j) mfma16_v(acc_l[t][rt][j], x[rt][0], j ? wl1 : wl0);
+            for (int j = 0; j < 2; ++j) {
+                mfma16_v(acc_l[t][rt][j], x[rt][0], j ? wl1 : wl0);
+                extra(i++);
+            }
 #pragma unroll
         for (int rt = 0; rt < 2; ++rt)
 #pragma unroll
-            for (int j = 0; j < 2; ++j) mfma16_a(acc_l[t][rt][j], x[rt][2], Wa[2 * t + j][s][0]);
+            for (int j = 0; j < 2; ++j) {
+                mfma16_a(acc_l[t][rt][j], x[rt][2], Wa[2 * t + j][s][0]);
+                extra(i++);
+            }
 #pragma unroll
         for (int rt = 0; rt < 2; ++rt)
 #pragma unroll
-            for (int j = 0; j < 2; ++j) mfma16_a(acc_l[t][rt][j], x[rt][1], Wa[2 * t + j][s][1]);
+            for (int j = 0; j < 2; ++j) {
+                mfma16_a(acc_l[t][rt][j], x[rt][1], Wa[2 * t + j][s][1]);
+                extra(i++);
+            }
     };
 
     // ---- the epilogue: grad_z1 of phase tt's tiles of row step kk into D2
@@ -921,22 +948,50 @@ __global__ __launch_bounds__(WS_THREADS, 1) void gemm_x6_fl16_kernel(
 #pragma unroll
             for (int s = 0; s < 8; ++s) {
                 const int g = 8 * t + s;
-                if (g + 1 < 16) read_frag(k, (g + 1) & 7, fb[(g + 1) & 1]);
-                wl[(2 * g + WLA) % WLR] = wl_load(2 * g + WLA);
-                wl[(2 * g + 1 + WLA) % WLR] = wl_load(2 * g + 1 + WLA);
-                mfma_group(s == 0, t, s, fb[g & 1], wl[(2 * g) % WLR], wl[(2 * g + 1) % WLR]);
-                if (s < 4) {
-#pragma unroll
-                    for (int i = 0; i < 4; ++i) h_load(kk, tt, 4 * s + i);
-                }
-                if (s == 1) x_frag(kk, xf);
+                const int q = 4 * t + (s >> 1);
+                // the step's memory instructions, one per MFMA slot (pinned
+                // between scheduling barriers): 6 A-fragment reads of k32
+                // step g + 1, 2 l-plane loads, 4 h1 loads (s < 4), the X
+                // fragment's 3 loads (s = 2; D2 at s = 5, 7), the staging
+                // load behind odd steps' split
+                auto mem_op = [&](int op) {
+                    if (op < 6) {
+                        if (g + 1 < 16) read_frag_one(k, (g + 1) & 7, fb[(g + 1) & 1], op / 3, op % 3);
+                    } else if (op < 8) {
+                        const int u = 2 * g + (op - 6) + WLA;
+                        wl[u % WLR] = wl_load(u);
+                    } else if (op < 12) {
+                        if (s < 4) h_load(kk, tt, 4 * s + (op - 8));
+                    } else if (op == 12 && (s & 1)) {
+                        stg[q & 3] = stage_load(q + 4 < 8 ? k + 1 : k + 2, (q + 4) & 7);
+                    } else if (op >= 12 && op < 15 && s == 2) {
+                        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+                            (void *)(ximg + (int64_t)(j0 + kk * per) * XREC), 0, XREC,
+                            kBufFlags);
+                        xf[op - 12] = __builtin_bit_cast(
+                            bf16x8_t,
+                            __builtin_amdgcn_raw_buffer_load_b128(rs, xoff, (op - 12) * 1024, 0));
+                    }
+                };
+                SplitHU u{stg[q & 3].x, stg[q & 3].y, stg[q & 3].z, stg[q & 3].w,
+                          0u, 0u, 0u, 0u, 0u, 0u};
+                auto extra = [&](int i) {
+                    if ((s & 1) && (i & 1)) split_piece(u, i >> 1);
+                    int op = -1;
+                    if (!(i & 1)) op = i >> 1;
+                    else if (!(s & 1)) op = 12 + (i >> 1);
+                    else if (i == 23) op = 12;
+                    if (op >= 0) {
+                        __builtin_amdgcn_sched_barrier(0);
+                        mem_op(op);
+                        __builtin_amdgcn_sched_barrier(0);
+                    }
+                };
+                mfma_group(s == 0, t, s, fb[g & 1], wl[(2 * g) % WLR], wl[(2 * g + 1) % WLR],
+                           extra);
                 if (s == 5) d2_tile(tt, 0, xf);
                 if (s == 7) d2_tile(tt, 1, xf);
-                if (s & 1) {
-                    const int q = 4 * t + (s >> 1);
-                    split_store(k + 1, q, stg[q & 3]);
-                    stg[q & 3] = stage_load(q + 4 < 8 ? k + 1 : k + 2, (q + 4) & 7);
-                }
+                if (s & 1) split_store_u(k + 1, q, u);
             }
         }
         asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
