@@ -138,13 +138,10 @@ __device__ inline void mfma16_first(f32x4_t &d, const bf16x8_t &x, const bf16x8_
 // issue for 8 of its 16 cycles; two 4-cycle VALU fit the rest,
 // MI355X_MICROARCH.md cycle constants) instead of as one block between MFMA
 // groups.  Bitwise the C++ split (pk_bf16 = v_cvt_pk_bf16_f32, lo_f / hi_f
-// = shift / mask, plain f32 subtractions).
-#ifndef X6_SPLIT_ASM
-#define X6_SPLIT_ASM 1
-#endif
-#ifndef X6_MEM_SPREAD
-#define X6_MEM_SPREAD 1
-#endif
+// = shift / mask, plain f32 subtractions).  Round 6, with the memory
+// instructions likewise spread one per MFMA slot: forward 85.7 -> 81.7 us,
+// the fused kernel 113.7-116.4 -> 103.8-107.8 us (alternating A/Bs, the
+// same output bytes).
 struct SplitHU {
     float a, b, c, d;
     uint32_t h0, h1, m0, m1, l0, l1;
@@ -309,8 +306,8 @@ __global__ __launch_bounds__(WS_THREADS, 1) void gemm_x6_ws16_kernel(
     // the six products of row tile t, k32 step s, for the four column tiles
     // (h += xh.wh; l += xh.wm, xm.wh, xh.wl, xl.wh, xm.wm: per output the
     // order of every x6 kernel), interleaved over the column tiles
-    // extra(i) runs behind MFMA i of the 24 (the split pieces and, with
-    // X6_MEM_SPREAD, the step's fragment reads and stores)
+    // extra(i) runs behind MFMA i of the 24 (the split pieces, the step's
+    // fragment reads and stores)
     auto mfma_group = [&](bool first, int t, int s, const AFrag &x, auto &&extra) {
         auto piece = [&](int i) { extra(i); };
 #pragma unroll
@@ -392,18 +389,14 @@ __global__ __launch_bounds__(WS_THREADS, 1) void gemm_x6_ws16_kernel(
                 const int g = 8 * t + s;
                 constexpr int D = WS_NF - 1;
                 const int q = 4 * t + (s >> 1);
-                if (!X6_MEM_SPREAD) {
-                    if (g + D < 16) read_frag(k, g + D, fb[(g + D) % WS_NF]);
-                    if ((s & 1) == 0) split_read(k + 1, q >> 1, q & 1, v);
-                }
                 SplitHU u{v.x, v.y, v.z, v.w, 0u, 0u, 0u, 0u, 0u, 0u};
                 // behind the odd MFMAs the split pieces (odd s), behind the
-                // even ones (X6_MEM_SPREAD) one memory instruction each,
-                // pinned by scheduling barriers: the three fragment reads of
-                // k32 step g + D, the two output stores, the staging read
+                // even ones one memory instruction each, pinned by
+                // scheduling barriers: the three fragment reads of k32 step
+                // g + D, the two output stores, the staging read
                 auto extra = [&](int i) {
-                    if (X6_SPLIT_ASM && (s & 1) && (i & 1)) split_piece(u, i >> 1);
-                    if (X6_MEM_SPREAD && !(i & 1)) {
+                    if ((s & 1) && (i & 1)) split_piece(u, i >> 1);
+                    if (!(i & 1)) {
                         const int j = i >> 1;
                         __builtin_amdgcn_sched_barrier(0);
                         if (j < 3 && g + D < 16) read_frag_plane(k, g + D, fb[(g + D) % WS_NF], j);
@@ -414,21 +407,7 @@ __global__ __launch_bounds__(WS_THREADS, 1) void gemm_x6_ws16_kernel(
                     }
                 };
                 mfma_group(s == 0, t, s, fb[g % WS_NF], extra);
-                if (!X6_MEM_SPREAD) {
-                    store_one(ko, 1 - t, 2 * s);
-                    store_one(ko, 1 - t, 2 * s + 1);
-                }
                 if ((s & 1) == 1) {
-                    if (!X6_SPLIT_ASM) {
-                        u.h0 = pk_bf16(v.x, v.y);
-                        float ra = v.x - lo_f(u.h0), rb = v.y - hi_f(u.h0);
-                        u.m0 = pk_bf16(ra, rb);
-                        u.l0 = pk_bf16(ra - lo_f(u.m0), rb - hi_f(u.m0));
-                        u.h1 = pk_bf16(v.z, v.w);
-                        ra = v.z - lo_f(u.h1), rb = v.w - hi_f(u.h1);
-                        u.m1 = pk_bf16(ra, rb);
-                        u.l1 = pk_bf16(ra - lo_f(u.m1), rb - hi_f(u.m1));
-                    }
                     split_store(k + 1, q >> 1, q & 1, u.h0, u.h1, u.m0, u.m1, u.l0, u.l1);
                     if (q & 1) {
                         // unit q >> 1's staging pieces consumed: refill them
