@@ -373,29 +373,55 @@ __global__ __launch_bounds__(WS_THREADS, 1) void gemm_x6_ws16_kernel(
     // buffer.  Branches would also risk the compiler copying an accumulator
     // between asm MFMA groups, a VALU read inside an MFMA's wait states
     // (tests/test_x6_asm_hazards.py).
+    // unit u's staging pieces, consumed by the split of half-units 2 u and
+    // 2 u + 1, refilled with step k + 3 (clamped: such rows are never split)
+    auto dma_piece = [&](int k, int u, int i) {
+        const int k3 = k + 3 >= R ? R - 1 : k + 3;
+        const float *r0 = Ab + ((int64_t)(j0 + k3 * per) * WS_RS + 8 * w) * XK;
+        uint8_t *dst = sh + WS_LDS_F + ((k + 3) & 1) * WS_FSLOT + w * 8 * 1024;
+        glds16_s(r0 + 32 * (2 * u + i), voff_f, lds_addr(dst + (2 * u + i) * 1024));
+    };
+    auto split_store_plane = [&](int k, int u, int hf, int p, const SplitHU &x) {
+        uint8_t *dst = sh + (k & 1) * WS_PSTAGE + wr_half[hf] + u * 8 * 512 + p * WS_PLANE;
+        typedef uint32_t u32x2_t __attribute__((ext_vector_type(2)));
+        const uint32_t lo = p == 0 ? x.h0 : p == 1 ? x.m0 : x.l0;
+        const uint32_t hi = p == 0 ? x.h1 : p == 1 ? x.m1 : x.l1;
+        *reinterpret_cast<u32x2_t *>(dst) = (u32x2_t){lo, hi};
+    };
+    float4 v;
+    SplitHU pu{};           // the previous odd step's planes (pq >= 0)
+    int pq = -1;
     auto row_step = [&](int k) {
         // the staging of step k + 1 (issued in step k - 2): every vector
         // memory op of step k - 1 (32 stores + 8 DMA pieces) is younger;
         // for k = 0 the prologue waited
         __builtin_amdgcn_sched_barrier(0);
         asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+        pq = -1;            // (a compile-time value at every use below)
 #pragma unroll
         for (int t = 0; t < 2; ++t) {
             const int ko = t == 1 ? k : k - 1;
             finish_tile(1 - t);
-            float4 v;
 #pragma unroll
             for (int s = 0; s < 8; ++s) {
                 const int g = 8 * t + s;
                 constexpr int D = WS_NF - 1;
                 const int q = 4 * t + (s >> 1);
                 SplitHU u{v.x, v.y, v.z, v.w, 0u, 0u, 0u, 0u, 0u, 0u};
-                // behind the odd MFMAs the split pieces (odd s), behind the
-                // even ones one memory instruction each, pinned by
-                // scheduling barriers: the three fragment reads of k32 step
-                // g + D, the two output stores, the staging read
+                // behind the odd MFMAs the split pieces (odd s) or the
+                // previous odd step's plane stores and staging DMA (even
+                // s), behind the even ones one memory instruction each, all
+                // pinned by scheduling barriers: the three fragment reads
+                // of k32 step g + D, the two output stores, the staging read
                 auto extra = [&](int i) {
                     if ((s & 1) && (i & 1)) split_piece(u, i >> 1);
+                    if (!(s & 1) && (i & 1) && pq >= 0 && (i >> 1) < 5) {
+                        const int j = i >> 1;
+                        __builtin_amdgcn_sched_barrier(0);
+                        if (j < 3) split_store_plane(k + 1, pq >> 1, pq & 1, j, pu);
+                        else if (pq & 1) dma_piece(k, pq >> 1, j - 3);
+                        __builtin_amdgcn_sched_barrier(0);
+                    }
                     if (!(i & 1)) {
                         const int j = i >> 1;
                         __builtin_amdgcn_sched_barrier(0);
@@ -407,20 +433,16 @@ __global__ __launch_bounds__(WS_THREADS, 1) void gemm_x6_ws16_kernel(
                     }
                 };
                 mfma_group(s == 0, t, s, fb[g % WS_NF], extra);
-                if ((s & 1) == 1) {
+                if ((s & 1) == 0) {
+                    pq = -1;                    // stored in this step's slots
+                } else if (t == 1 && s == 7) {
+                    // the row step's last split: its planes before the barrier
                     split_store(k + 1, q >> 1, q & 1, u.h0, u.h1, u.m0, u.m1, u.l0, u.l1);
-                    if (q & 1) {
-                        // unit q >> 1's staging pieces consumed: refill them
-                        // with step k + 3 (clamped: such rows are never split)
-                        const int u = q >> 1;
-                        const int k3 = k + 3 >= R ? R - 1 : k + 3;
-                        const float *r0 =
-                            Ab + ((int64_t)(j0 + k3 * per) * WS_RS + 8 * w) * XK;
-                        uint8_t *dst = sh + WS_LDS_F + ((k + 3) & 1) * WS_FSLOT + w * 8 * 1024;
-                        glds16_s(r0 + 32 * (2 * u), voff_f, lds_addr(dst + (2 * u) * 1024));
-                        glds16_s(r0 + 32 * (2 * u + 1), voff_f,
-                                 lds_addr(dst + (2 * u + 1) * 1024));
-                    }
+                    dma_piece(k, q >> 1, 0);
+                    dma_piece(k, q >> 1, 1);
+                } else {
+                    pu = u;                     // stored in the next step's slots
+                    pq = q;
                 }
             }
         }
@@ -865,25 +887,14 @@ __global__ __launch_bounds__(WS_THREADS, 1) void gemm_x6_fl16_kernel(
             xf[p] = __builtin_bit_cast(bf16x8_t, __builtin_amdgcn_raw_buffer_load_b128(
                                                      rs, xoff, p * 1024, 0));
     };
-    // grad_z1 = grad_h1 (1 - h1^2) of phase tt's column tile j (both row
-    // tiles: the B fragment's 8 K values), split, and the six products
-    auto d2_tile = [&](int tt, int j, const bf16x8_t (&xf)[3]) {
-        float gz[8];
-#pragma unroll
-        for (int e = 0; e < 8; ++e) {
-            const float y = hb[e >> 2][j][e & 3];
-            gz[e] = acc_h[tt][e >> 2][j][e & 3] * (1.0f - y * y);
-        }
-        u32x4_t gh, gm, gl;
-        split8(gz, gh, gm, gl);
-        const bf16x8_t bh = __builtin_bit_cast(bf16x8_t, gh);
-        const bf16x8_t bm = __builtin_bit_cast(bf16x8_t, gm);
-        const bf16x8_t bl = __builtin_bit_cast(bf16x8_t, gl);
+    // the six D2 products of phase tt's column tile j: one asm statement,
+    // so D2 stays in VGPRs (the builtin's accumulator took AGPRs, evicting a
+    // weight fragment with a copy back before each use, round 5) and no
+    // compiler VALU lands between the MFMAs; s_nop 4 covers the VALU writes
+    // of bh, bm, bl -> SrcB reads
+    auto d2_mfma = [&](int tt, int j, const bf16x8_t (&xf)[3], const bf16x8_t &bh,
+                       const bf16x8_t &bm, const bf16x8_t &bl) {
         f32x4_t &d = d2[2 * tt + j];
-        // one asm statement: D2 stays in VGPRs (the builtin's accumulator
-        // took AGPRs, evicting a weight fragment with a copy back before each
-        // use, round 5) and no compiler VALU lands between the MFMAs; s_nop 4
-        // covers the VALU writes of bh, bm, bl -> SrcB reads
         asm volatile("s_nop 4\n\t"
                      "v_mfma_f32_16x16x32_bf16 %0, %1, %4, %0\n\t"
                      "v_mfma_f32_16x16x32_bf16 %0, %1, %5, %0\n\t"
@@ -894,7 +905,22 @@ __global__ __launch_bounds__(WS_THREADS, 1) void gemm_x6_fl16_kernel(
                      : "+v"(d)
                      : "v"(xf[0]), "v"(xf[1]), "v"(xf[2]), "v"(bh), "v"(bm), "v"(bl));
     };
-
+    // grad_z1 = grad_h1 (1 - h1^2) of phase tt's column tile j (both row
+    // tiles: the B fragment's 8 K values), split, and the six products.
+    // (Round 6: the same VALU as asm pieces spread over the MFMA slots of
+    // k32 steps 4 / 6 measured 128-131 vs 106-108 us per call; not taken.)
+    auto d2_tile = [&](int tt, int j, const bf16x8_t (&xf)[3]) {
+        float gz[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+            const float y = hb[e >> 2][j][e & 3];
+            gz[e] = acc_h[tt][e >> 2][j][e & 3] * (1.0f - y * y);
+        }
+        u32x4_t gh, gm, gl;
+        split8(gz, gh, gm, gl);
+        d2_mfma(tt, j, xf, __builtin_bit_cast(bf16x8_t, gh), __builtin_bit_cast(bf16x8_t, gm),
+                __builtin_bit_cast(bf16x8_t, gl));
+    };
     // ---- prologue: step 0's planes, the staging ring for step 1 ----
     {
         float4 v0[8];
