@@ -1,7 +1,8 @@
 """Time dr_ppo_head_loss_backward (both heads + PPO loss + backward through
 the heads and the top tanh) on one 65,536-row minibatch of pre-activations,
-rows drawn through a permutation of a 2,097,152-row rollout buffer (the
-trainer's shapes), deferred finish (defer=2), on the library DRONERL_LIB names;
+actions / aux rows contiguous as the trainer's record gather leaves them
+(ROWS=1: read through a permutation of a 2,097,152-row rollout buffer
+instead, the rounds-3-5 form), deferred finish (defer=2), on the library DRONERL_LIB names;
 digest of gz_pi / gz_vf and the per-block rows so variants that change
 results show it.
 
@@ -28,10 +29,12 @@ b_act = torch.zeros(4, device=dev)
 w_val = (torch.randn(1, HD, generator=g) * 0.06).to(dev)
 b_val = torch.zeros(1, device=dev)
 log_std = torch.zeros(4, device=dev)
-actions = (torch.randn(NBUF, 4, generator=g) * 0.5).to(dev)
-aux = torch.randn(NBUF, 3, generator=g).to(dev)
+ROWS = os.environ.get("ROWS", "0") == "1"
+NA = NBUF if ROWS else M
+actions = (torch.randn(NA, 4, generator=g) * 0.5).to(dev)
+aux = torch.randn(NA, 3, generator=g).to(dev)
 aux[:, 0] = -4.0
-rows = torch.randperm(NBUF, generator=g)[:M].to(torch.int32).to(dev)
+rows = torch.randperm(NBUF, generator=g)[:M].to(torch.int32).to(dev) if ROWS else None
 gz_pi, gz_vf = torch.empty_like(z_pi), torch.empty_like(z_vf)
 gw_act, gb_act = torch.empty_like(w_act), torch.empty(4, device=dev)
 gw_val, gb_val = torch.empty_like(w_val), torch.empty(1, device=dev)
