@@ -205,28 +205,4 @@ inline unsigned grid_for(int64_t n, int per_block = kBlock) {
     return (unsigned)((n + per_block - 1) / per_block);
 }
 
-// LDS DMA by inline asm.  glds16_s: global_load_lds_dwordx4 in the saddr
-// form (a wave-uniform 64-bit base in SGPRs and a 32-bit per-lane byte
-// offset, so a loop of these keeps one offset VGPR): lane l's 16 bytes land at
-// LDS byte lds_base + 16 l.  glds4_v: global_load_lds_dword from a per-lane
-// 64-bit address: lane l's 4 bytes land at lds_base + 4 l.  Issued by hand
-// because hipcc's waitcnt pass drains every pending LDS DMA (vmcnt(0)) before
-// any ds_read it cannot prove disjoint from it (and, with a DMA in flight, at
-// the next use of any ordinary load); the callers count their waits by hand.
-// Both clobber m0 (reserved: the compiler sets it before each own use).
-#pragma clang diagnostic ignored "-Winline-asm"
-__device__ inline void glds16_s(const void *sbase, uint32_t voff, uint32_t lds_base) {
-    asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, %1"
-                 ::"v"(voff), "s"(sbase), "s"(lds_base)
-                 : "memory", "m0");
-}
-__device__ inline void glds4_v(const void *src, uint32_t lds_base) {
-    asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dword %0, off"
-                 ::"v"(src), "s"(lds_base)
-                 : "memory", "m0");
-}
-__device__ inline uint32_t lds_addr(const uint8_t *p) {
-    return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) uint8_t *)p;
-}
-
 }  // namespace dr

@@ -46,6 +46,8 @@
 #include "x6_split.h"
 
 #pragma clang fp contract(off)
+// glds16_s clobbers m0 (reserved: the compiler sets it before each own use)
+#pragma clang diagnostic ignored "-Winline-asm"
 
 namespace dr {
 namespace {
@@ -62,7 +64,20 @@ __global__ __launch_bounds__(256) void split_weights_kernel(const float *__restr
     split_weights_item(w, transpose, batch, img, blockIdx.x * 256 + threadIdx.x, blockIdx.y);
 }
 
-// glds16_s / lds_addr: common.h (shared with ppo_head_kernel's row pipeline)
+// global_load_lds_dwordx4 by inline asm (the saddr form: a wave-uniform
+// 64-bit base in SGPRs and a 32-bit per-lane byte offset, so a loop of these
+// keeps one offset VGPR): lane l's 16 bytes land at LDS byte lds_base + 16 l.
+// Issued by hand because hipcc's waitcnt pass drains every pending LDS DMA
+// (vmcnt(0)) before any ds_read it cannot prove disjoint from it; the waits
+// are counted by hand.
+__device__ inline void glds16_s(const void *sbase, uint32_t voff, uint32_t lds_base) {
+    asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, %1"
+                 ::"v"(voff), "s"(sbase), "s"(lds_base)
+                 : "memory", "m0");
+}
+__device__ inline uint32_t lds_addr(const uint8_t *p) {
+    return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) uint8_t *)p;
+}
 
 // ---------------------------------------------------------------------------
 // dr_gemm_x6: weight-stationary.  A 256-thread block (one wave per SIMD, 512

@@ -973,63 +973,6 @@ __device__ inline float wave_allsum(float x) {
            __int_as_float(__builtin_amdgcn_readlane(__float_as_int(x), 32));
 }
 
-// Reduce-scatter form of wave_allsum for several values at once (wave_rs16: rs16_first on
-// value pairs, then wave_rs16_rest; wave_rs4): the same butterfly (same pairs, same operand order at every level, so each total is
-// bitwise wave_allsum's), but at every level a lane keeps only the half of
-// its values that its partner does not, so 16 values cost 8 + 4 + 2 + 1 DPP
-// adds instead of 16 x 4.  The kept half is chosen so that every later
-// partner holds the same values: after the DPP levels lane L (bits b0..b3 of
-// L & 15) holds value t = (b0^b2) + 2 (b0^b1) + 4 (b2^b3) + 8 b3 (16 values;
-// the first two bits only for 4), summed over its 32-lane half after the
-// xor-16 swizzle; the returned y = that + the other half's (lane L ^ 32) is
-// wave_allsum's total of value t in every lane that holds t.
-__device__ inline int rs_lane(int t) {      // a lane (0..15) holding value t
-    const int a1 = t & 1, a2 = (t >> 1) & 1, a3 = (t >> 2) & 1, b3 = (t >> 3) & 1;
-    const int b2 = a3 ^ b3, b0 = a1 ^ b2, b1 = a2 ^ b0;
-    return b0 | (b1 << 1) | (b2 << 2) | (b3 << 3);
-}
-template <int CTRL>
-__device__ inline float rs_level(float lo_v, float hi_v, bool hi) {
-    const float keep = hi ? hi_v : lo_v, send = hi ? lo_v : hi_v;
-    return keep + dpp_mov<CTRL>(send);
-}
-__device__ inline float rs_tail(float x) {  // levels 5 (xor 16) and 6 (lane ^ 32)
-    x = x + __int_as_float(__builtin_amdgcn_ds_swizzle(__float_as_int(x), 0x401F));
-    const int lane = __lane_id();
-    return x + __int_as_float(__builtin_amdgcn_ds_bpermute((lane ^ 32) << 2, __float_as_int(x)));
-}
-// the first level of wave_rs16 on the pair (v[2 p], v[2 p + 1]), so a
-// caller can reduce values as it produces them (fewer live registers)
-__device__ inline float rs16_first(float v0, float v1) {
-    const int l = __lane_id();
-    return rs_level<0xB1>(v0, v1, (l ^ (l >> 2)) & 1);
-}
-// wave_rs16 after its first level: h[p] = rs16_first(v[2 p], v[2 p + 1])
-__device__ inline float wave_rs16_rest(const float h[8]) {
-    const int l = __lane_id();
-    const bool b0 = l & 1, b1 = (l >> 1) & 1, b2 = (l >> 2) & 1, b3 = (l >> 3) & 1;
-    float q[4], e[2];
-#pragma unroll
-    for (int p = 0; p < 4; ++p) q[p] = rs_level<0x4E>(h[2 * p], h[2 * p + 1], b0 ^ b1);
-#pragma unroll
-    for (int p = 0; p < 2; ++p) e[p] = rs_level<0x141>(q[2 * p], q[2 * p + 1], b2 ^ b3);
-    return rs_tail(rs_level<0x140>(e[0], e[1], b3));
-}
-__device__ inline float wave_rs4(const float v[4]) {
-    const int l = __lane_id();
-    const bool b0 = l & 1, b1 = (l >> 1) & 1, b2 = (l >> 2) & 1;
-    const float h0 = rs_level<0xB1>(v[0], v[1], b0 ^ b2);
-    const float h1 = rs_level<0xB1>(v[2], v[3], b0 ^ b2);
-    float x = rs_level<0x4E>(h0, h1, b0 ^ b1);
-    x = x + dpp_mov<0x141>(x);
-    x = x + dpp_mov<0x140>(x);
-    return rs_tail(x);
-}
-// value t's total from the lane that holds it (wave_rs16 / wave_rs4's y)
-__device__ inline float rs_get(float y, int t) {
-    return __int_as_float(__builtin_amdgcn_ds_bpermute(rs_lane(t) << 2, __float_as_int(y)));
-}
-
 // tanh_fast: common.h (shared with the first-layer-fused GEMM, gemm_x6.hip)
 
 __device__ inline float4 ld4(const float *p) { return *reinterpret_cast<const float4 *>(p); }
@@ -1288,87 +1231,14 @@ struct HeadArgs {
 #define DR_HEAD_TILE 4
 #endif
 constexpr int kHeadTile = DR_HEAD_TILE;
-// 1: the tile's head dot products by one reduce-scatter (wave_rs16 /
-// wave_rs4, bitwise the per-dot wave_allsum's totals) -- round-6 A/B
-#ifndef DR_HEAD_RS
-#define DR_HEAD_RS 0
-#endif
-static_assert(!DR_HEAD_RS || kHeadTile == 4, "the reduce-scatter covers 4-row tiles");
 // (round 3 A/B, removed in round 4: the next tile's activation rows loaded
-// to registers while this tile computes, +16 VGPRs per wave, slower; round 6:
-// the same prefetch through LDS by DMA, below)
-
-// ---- the row pipeline (round 6) ----
-// With rows == nullptr (the trainer: its record gather leaves the
-// minibatch's actions / aux rows contiguous) a wave's tiles come through LDS
-// by DMA, one tile ahead, so the next tile's HBM reads overlap this tile's
-// VALU work (the plain-load form waited for every tile's rows and then
-// computed: 55-57 us per 65,536-row minibatch, its VALU issue ~35).  Per wave
-// two slots, each one tile: its 4 activation rows (lane l's 16 B of row i at
-// i * 1024 + 16 l) and its loss inputs (the 4 action rows at kHeadLossOff,
-// the 4 (old log-prob, advantage, return) rows 64 B further).  Every vector
-// memory instruction of the loop is issued by hand -- the DMA (4 row + 1
-// loss-input instructions per tile) and the gz stores (4 per tile) -- so the
-// wait for tile k is a counted s_waitcnt vmcnt(4 + 5): all but tile k-1's
-// stores and tile k+1's DMA (vector memory counts in issue order,
-// MI355X_MICROARCH.md "s_waitcnt vmcnt(N)").  The loop must not spill: a
-// scratch access would be an uncounted vector memory instruction
-// (tests/test_x6_asm_hazards.py checks the kernel's scratch size).
-#ifndef DR_HEAD_PIPE
-#define DR_HEAD_PIPE 0
-#endif
-constexpr int kHeadRowB = 1024;                       // 256 f32 activations
-constexpr int kHeadLossOff = kHeadTile * kHeadRowB;   // 4 x 16 B actions, then 4 x 12 B aux
-constexpr int kHeadSlot = kHeadLossOff + 128;
-constexpr int kHeadWaveLds = 2 * kHeadSlot;
-constexpr int kHeadDmaOps = kHeadTile + 1, kHeadStoreOps = kHeadTile;
-
-// tile r0's DMA into the LDS slot at `slot`: rows past the end are clamped
-// to the last row (loaded, never used), so every tile issues kHeadDmaOps
-__device__ inline void head_issue(const float *h, const float *act, const float *aux,
-                                  int64_t m, int hd, int64_t r0, uint32_t slot, int lane,
-                                  bool act_lane) {
-#pragma unroll
-    for (int i = 0; i < kHeadTile; ++i) {
-        const int64_t row = min(r0 + i, m - 1);
-        if (act_lane) glds16_s(h + row * hd, 16 * lane, slot + i * kHeadRowB);
-    }
-    if (lane < 28) {   // lanes 0-15: the action rows' floats, 16-27: the aux rows'
-        const float *src =
-            lane < 16 ? act + min(r0 + (lane >> 2), m - 1) * 4 + (lane & 3)
-                      : aux + min(r0 + (lane - 16) / 3, m - 1) * 3 + (lane - 16) % 3;
-        glds4_v(src, slot + kHeadLossOff);
-    }
-}
-// the wait for the tile whose DMA was issued last-but-one: all but the
-// previous tile's stores (when there was one) and the next tile's DMA (when
-// issued) done
-__device__ inline void head_wait(bool stores_before, bool next_issued) {
-    static_assert(kHeadDmaOps == 5 && kHeadStoreOps == 4, "counts below");
-    if (stores_before) {
-        if (next_issued) asm volatile("s_waitcnt vmcnt(9)" ::: "memory");
-        else asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-    } else {
-        if (next_issued) asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
-        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-}
-__device__ inline void head_st4(float *p, float4 x, bool by_asm) {
-    if (by_asm) {
-        typedef float f32x4v __attribute__((ext_vector_type(4)));
-        const f32x4v v = {x.x, x.y, x.z, x.w};
-        asm volatile("global_store_dwordx4 %0, %1, off" ::"v"(p), "v"(v) : "memory");
-    } else {
-        st4(p, x);
-    }
-}
+// while this tile computes, +16 VGPRs per wave, slower)
 
 // policy waves: accumulate u[0], u[2..7] (loss terms), u[9..12] (d b_act),
 // and per lane d b_pi (4 columns) and d W_act (4 x 4)
-template <bool kPipe>
 __device__ inline void head_policy_wave(const HeadArgs &a, const RowLossConst &c, int lane,
-                                        int64_t tile0, int64_t tstride, uint8_t *wl,
-                                        float u[kHeadFixed], float sb[4], float sw[4][4]) {
+                                        int64_t tile0, int64_t tstride, float u[kHeadFixed],
+                                        float sb[4], float sw[4][4]) {
     const int hd = a.hd, c0 = 4 * lane;
     const bool act = c0 < hd;
     const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -1377,63 +1247,24 @@ __device__ inline void head_policy_wave(const HeadArgs &a, const RowLossConst &c
     for (int j = 0; j < 4; ++j) wa[j] = act ? ld4(a.w_act + j * hd + c0) : z4;
     const float4 zb = (act && a.zb_pi) ? ld4(a.zb_pi + c0) : z4;
     const float ba[4] = {a.b_act[0], a.b_act[1], a.b_act[2], a.b_act[3]};
-    const float *act_rows = reinterpret_cast<const float *>(a.actions);
-    if (kPipe && tile0 * kHeadTile < a.m)
-        head_issue(a.h_pi, act_rows, a.aux, a.m, hd, tile0 * kHeadTile, lds_addr(wl), lane, act);
-    int it = 0;
-    for (int64_t tile = tile0; tile * kHeadTile < a.m; tile += tstride, ++it) {
+    for (int64_t tile = tile0; tile * kHeadTile < a.m; tile += tstride) {
         const int64_t r0 = tile * kHeadTile;
         const int nr = (int)min((int64_t)kHeadTile, a.m - r0);
-        const bool own = lane < nr;
         float4 h[kHeadTile];
-        float4 ac4;
-        float lp_old, A;
-        if constexpr (kPipe) {
-            const bool nxt = (tile + tstride) * kHeadTile < a.m;
-            const uint8_t *sl = wl + (it & 1) * kHeadSlot;
-            if (nxt)
-                head_issue(a.h_pi, act_rows, a.aux, a.m, hd, (tile + tstride) * kHeadTile,
-                           lds_addr(wl + ((it + 1) & 1) * kHeadSlot), lane, act);
-            head_wait(it > 0, nxt);
 #pragma unroll
-            for (int i = 0; i < kHeadTile; ++i)
-                h[i] = (act && i < nr)
-                           ? *reinterpret_cast<const float4 *>(sl + i * kHeadRowB + 16 * lane)
-                           : z4;
-            const uint8_t *li = sl + kHeadLossOff;
-            ac4 = *reinterpret_cast<const float4 *>(li + 16 * (lane & 3));
-            lp_old = *reinterpret_cast<const float *>(li + 64 + 12 * (lane & 3));
-            A = *reinterpret_cast<const float *>(li + 64 + 12 * (lane & 3) + 4);
-        } else {
-#pragma unroll
-            for (int i = 0; i < kHeadTile; ++i)
-                h[i] = (act && i < nr) ? ld4(a.h_pi + (r0 + i) * hd + c0) : z4;
-            // this lane's row (lane < nr): its loss inputs, loaded while the dots run
-            const int64_t rr = r0 + (own ? lane : 0);
-            const int64_t ro = a.rows ? (int64_t)a.rows[rr] : rr;
-            ac4 = a.actions[ro];
-            lp_old = a.aux[3 * ro];
-            A = a.aux[3 * ro + 1];
-        }
+        for (int i = 0; i < kHeadTile; ++i)
+            h[i] = (act && i < nr) ? ld4(a.h_pi + (r0 + i) * hd + c0) : z4;
+        // this lane's row (lane < nr): its loss inputs, loaded while the dots run
+        const bool own = lane < nr;
+        const int64_t rr = r0 + (own ? lane : 0);
+        const int64_t ro = a.rows ? (int64_t)a.rows[rr] : rr;
+        const float4 ac4 = a.actions[ro];
+        const float lp_old = a.aux[3 * ro], A = a.aux[3 * ro + 1];
         if (a.preact) {
 #pragma unroll
             for (int i = 0; i < kHeadTile; ++i)
                 h[i] = tanh4(add4(h[i], zb));
         }
-#if DR_HEAD_RS
-        // the tile's 16 dot products reduced at once; row lane & 3's four in
-        // this lane (bitwise wave_allsum's totals)
-        float hv[8];
-#pragma unroll
-        for (int i = 0; i < kHeadTile; ++i) {
-            hv[2 * i] = rs16_first(dot4(h[i], wa[0]), dot4(h[i], wa[1]));
-            hv[2 * i + 1] = rs16_first(dot4(h[i], wa[2]), dot4(h[i], wa[3]));
-        }
-        const float y = wave_rs16_rest(hv);
-        float mu[4];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) mu[j] = rs_get(y, j + 4 * (lane & 3)) + ba[j];
-#else
         float mu[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int i = 0; i < kHeadTile; ++i) {
@@ -1444,7 +1275,6 @@ __device__ inline void head_policy_wave(const HeadArgs &a, const RowLossConst &c
                 mu[j] = me ? mj : mu[j];
             }
         }
-#endif
         float gm[4] = {0.f, 0.f, 0.f, 0.f};
         if (own) {
             const float ac[4] = {ac4.x, ac4.y, ac4.z, ac4.w};
@@ -1476,18 +1306,16 @@ __device__ inline void head_policy_wave(const HeadArgs &a, const RowLossConst &c
                 for (int j = 0; j < 4; ++j) sw[j][q] = fmaf(g[j], hq[q], sw[j][q]);
             }
             if (act && i < nr)
-                head_st4(a.gz_pi + (r0 + i) * hd + c0, make_float4(gz[0], gz[1], gz[2], gz[3]),
-                         kPipe);
+                st4(a.gz_pi + (r0 + i) * hd + c0, make_float4(gz[0], gz[1], gz[2], gz[3]));
         }
     }
 }
 
 // value waves: accumulate u[1] (value-loss term), u[13] (d b_val), and per
 // lane d b_vf (4 columns) and d W_val (4)
-template <bool kPipe>
 __device__ inline void head_value_wave(const HeadArgs &a, const RowLossConst &c, int lane,
-                                       int64_t tile0, int64_t tstride, uint8_t *wl,
-                                       float u[kHeadFixed], float sb[4], float sw[4]) {
+                                       int64_t tile0, int64_t tstride, float u[kHeadFixed],
+                                       float sb[4], float sw[4]) {
     const int hd = a.hd, c0 = 4 * lane;
     const bool act = c0 < hd;
     const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -1495,55 +1323,28 @@ __device__ inline void head_value_wave(const HeadArgs &a, const RowLossConst &c,
     const float4 zb = (act && a.zb_vf) ? ld4(a.zb_vf + c0) : z4;
     const float bv = a.b_val[0];
     const float wvq[4] = {wv.x, wv.y, wv.z, wv.w};
-    const float *act_rows = reinterpret_cast<const float *>(a.actions);
-    if (kPipe && tile0 * kHeadTile < a.m)
-        head_issue(a.h_vf, act_rows, a.aux, a.m, hd, tile0 * kHeadTile, lds_addr(wl), lane, act);
-    int it = 0;
-    for (int64_t tile = tile0; tile * kHeadTile < a.m; tile += tstride, ++it) {
+    for (int64_t tile = tile0; tile * kHeadTile < a.m; tile += tstride) {
         const int64_t r0 = tile * kHeadTile;
         const int nr = (int)min((int64_t)kHeadTile, a.m - r0);
-        const bool own = lane < nr;
         float4 h[kHeadTile];
-        float R;
-        if constexpr (kPipe) {
-            const bool nxt = (tile + tstride) * kHeadTile < a.m;
-            const uint8_t *sl = wl + (it & 1) * kHeadSlot;
-            if (nxt)
-                head_issue(a.h_vf, act_rows, a.aux, a.m, hd, (tile + tstride) * kHeadTile,
-                           lds_addr(wl + ((it + 1) & 1) * kHeadSlot), lane, act);
-            head_wait(it > 0, nxt);
 #pragma unroll
-            for (int i = 0; i < kHeadTile; ++i)
-                h[i] = (act && i < nr)
-                           ? *reinterpret_cast<const float4 *>(sl + i * kHeadRowB + 16 * lane)
-                           : z4;
-            R = *reinterpret_cast<const float *>(sl + kHeadLossOff + 64 + 12 * (lane & 3) + 8);
-        } else {
-#pragma unroll
-            for (int i = 0; i < kHeadTile; ++i)
-                h[i] = (act && i < nr) ? ld4(a.h_vf + (r0 + i) * hd + c0) : z4;
-            const int64_t rr = r0 + (own ? lane : 0);
-            const int64_t ro = a.rows ? (int64_t)a.rows[rr] : rr;
-            R = a.aux[3 * ro + 2];
-        }
+        for (int i = 0; i < kHeadTile; ++i)
+            h[i] = (act && i < nr) ? ld4(a.h_vf + (r0 + i) * hd + c0) : z4;
+        const bool own = lane < nr;
+        const int64_t rr = r0 + (own ? lane : 0);
+        const int64_t ro = a.rows ? (int64_t)a.rows[rr] : rr;
+        const float R = a.aux[3 * ro + 2];
         if (a.preact) {
 #pragma unroll
             for (int i = 0; i < kHeadTile; ++i)
                 h[i] = tanh4(add4(h[i], zb));
         }
-#if DR_HEAD_RS
-        float dv[kHeadTile];
-#pragma unroll
-        for (int i = 0; i < kHeadTile; ++i) dv[i] = dot4(h[i], wv);
-        const float v = rs_get(wave_rs4(dv), lane & 3) + bv;
-#else
         float v = 0.f;
 #pragma unroll
         for (int i = 0; i < kHeadTile; ++i) {
             const float vv = wave_allsum(dot4(h[i], wv)) + bv;
             v = lane == i ? vv : v;
         }
-#endif
         float gv = 0.f;
         if (own) {
             ppo_row_value(c, R, v, gv, u);
@@ -1561,30 +1362,14 @@ __device__ inline void head_value_wave(const HeadArgs &a, const RowLossConst &c,
                 sw[q] = fmaf(gvi, hq[q], sw[q]);
             }
             if (act && i < nr)
-                head_st4(a.gz_vf + (r0 + i) * hd + c0, make_float4(gz[0], gz[1], gz[2], gz[3]),
-                         kPipe);
+                st4(a.gz_vf + (r0 + i) * hd + c0, make_float4(gz[0], gz[1], gz[2], gz[3]));
         }
     }
 }
 
-// dynamic LDS of ppo_head_kernel: the row pipeline's slots, reused for the
-// block's partial rows at the end
-inline size_t head_lds_bytes(int P) {
-    const size_t part = sizeof(float) * 4 * (size_t)P, pipe = 4 * (size_t)kHeadWaveLds;
-    return part > pipe ? part : pipe;
-}
-
-#ifndef DR_HEAD_WPE
-#define DR_HEAD_WPE 0
-#endif
-__global__ __launch_bounds__(kBlock)
-#if DR_HEAD_WPE
-__attribute__((amdgpu_waves_per_eu(4)))
-#endif
-void ppo_head_kernel(HeadArgs a) {
-    extern __shared__ float sh_part[];  // head_lds_bytes(P)
-    // wid wave-uniform for the compiler too (the DMA's SGPR operands derive from it)
-    const int lane = threadIdx.x & 63, wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+__global__ __launch_bounds__(kBlock) void ppo_head_kernel(HeadArgs a) {
+    extern __shared__ float sh_part[];  // 4 * P
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     const int hd = a.hd, c0 = 4 * lane;
     const bool act = c0 < hd;
     float amean = 0.f, astd = 1.f;
@@ -1601,27 +1386,15 @@ void ppo_head_kernel(HeadArgs a) {
     for (int k = 0; k < kHeadFixed; ++k) u[k] = 0.f;
     float sb[4] = {0.f, 0.f, 0.f, 0.f};
     float sw[4][4] = {};
-    // (round 6: the dispatcher already spreads a block's four waves over the
-    // CU's four SIMDs, each SIMD two policy and two value waves of the four
-    // blocks it hosts -- scripts/micro/wave_simd_probe.hip; swapping the roles
-    // on alternate blocks changed nothing)
     const bool policy = wid < 2;
     const int64_t tile0 = (int64_t)blockIdx.x * 2 + (wid & 1), tstride = (int64_t)gridDim.x * 2;
-    uint8_t *wl = reinterpret_cast<uint8_t *>(sh_part) + wid * kHeadWaveLds;
-    const bool pipe = DR_HEAD_PIPE && (DR_HEAD_PIPE == 2 || !a.rows);
-    if (policy) {
-        if (pipe) head_policy_wave<true>(a, c, lane, tile0, tstride, wl, u, sb, sw);
-        else head_policy_wave<false>(a, c, lane, tile0, tstride, wl, u, sb, sw);
-    } else {
-        if (pipe) head_value_wave<true>(a, c, lane, tile0, tstride, wl, u, sb, sw[0]);
-        else head_value_wave<false>(a, c, lane, tile0, tstride, wl, u, sb, sw[0]);
-    }
+    if (policy)
+        head_policy_wave(a, c, lane, tile0, tstride, u, sb, sw);
+    else
+        head_value_wave(a, c, lane, tile0, tstride, u, sb, sw[0]);
     // the lane-partial scalars to wave totals (fixed butterfly order)
 #pragma unroll
     for (int k = 0; k < kHeadFixed; ++k) u[k] = wave_allsum(u[k]);
-    // every wave's slots are read (its last tile waited for) before any wave
-    // overwrites them with partial rows
-    __syncthreads();
     float *mine = sh_part + wid * a.P;
     if (lane == 0) {
 #pragma unroll
@@ -2014,12 +1787,9 @@ inline int head_blocks(int64_t m) {
 }
 
 // ppo_head_kernel: 2 row tiles per block and round (one per wave of a role)
-#ifndef DR_HEAD_NB
-#define DR_HEAD_NB 1024
-#endif
 inline int loss_head_blocks(int64_t m) {
     const int64_t b = (m + 2 * kHeadTile - 1) / (2 * kHeadTile);
-    return (int)(b < DR_HEAD_NB ? b : DR_HEAD_NB);
+    return (int)(b < 1024 ? b : 1024);
 }
 
 // ---------------------------------------------------------------------------
@@ -2785,7 +2555,7 @@ int dr_ppo_head_loss_backward(int64_t m, int64_t hd, int preact, const float *h_
     HeadArgs a{m, (int)hd, preact, h_pi, h_vf, zb_pi, zb_vf, w_act, b_act, w_val, b_val, log_std,
                reinterpret_cast<const float4 *>(actions), aux, rows, clip_range, ent_coef,
                vf_coef, norm, adv_part, anb, gz_pi, gz_vf, part, P};
-    hipLaunchKernelGGL(ppo_head_kernel, dim3(nb), dim3(kBlock), head_lds_bytes(P), st, a);
+    hipLaunchKernelGGL(ppo_head_kernel, dim3(nb), dim3(kBlock), sizeof(float) * 4 * P, st, a);
     int rc = check_launch("dr_ppo_head_loss_backward");
     if (rc) return rc;
     // defer 2: the per-block rows are summed by the finish (head_direct)
