@@ -6,8 +6,10 @@
 cd "$(dirname "$0")/../.."
 if [ "${HEAD:-0}" = 1 ]; then
   OUT=$PWD/gpurun_out/pmc_head; PROG="$PWD/scripts/micro/head_bench.py"; export REPS=10
+  export PMC_WORKLOAD="scripts/micro/head_bench.py (REPS=10; ppo_head_kernel, 65,536-row minibatch, the trainer's contiguous actions / aux rows), rocprofv3 --pmc, four passes (HEAD=1 scripts/micro/gemm_x6_pmc.sh)"
 elif [ "${FL:-0}" = 1 ]; then
   OUT=$PWD/gpurun_out/pmc_fl; PROG="$PWD/scripts/micro/fl_bench.py"; export REPS=10
+  export PMC_WORKLOAD="scripts/micro/fl_bench.py (REPS=10; the fused input-gradient GEMM + first-layer backward beside the forward), rocprofv3 --pmc, four passes (FL=1 scripts/micro/gemm_x6_pmc.sh)"
 else
   OUT=$PWD/gpurun_out/pmc_gx6; PROG="$PWD/scripts/micro/gemm_x6_bench.py --reps 10"
 fi
@@ -26,10 +28,12 @@ done
 python3 - "$OUT" <<'PY'
 import csv, glob, json, re, sys, collections
 out = sys.argv[1]
-res = {"workload": "scripts/micro/gemm_x6_bench.py --reps 10 (both nets, 65,536 rows: the forward "
-                   "and input-gradient forms of dr_gemm_x6 and the 64-chunk weight gradient; cold "
-                   "inputs), rocprofv3 --pmc, two passes (scripts/micro/gemm_x6_pmc.sh); "
-                   "per-dispatch averages per kernel"}
+import os
+res = {"workload": os.environ.get("PMC_WORKLOAD",
+                                  "scripts/micro/gemm_x6_bench.py --reps 10 (both nets, 65,536 rows: "
+                                  "the forward and input-gradient forms of dr_gemm_x6 and the 64-chunk "
+                                  "weight gradient; cold inputs), rocprofv3 --pmc, four passes "
+                                  "(scripts/micro/gemm_x6_pmc.sh); per-dispatch averages per kernel")}
 for key, pat in (("gemm_x6_ws16_kernel", r"gemm_x6_ws16_kernel"),
                  ("gemm_x6_wgrad16_kernel", r"gemm_x6_wgrad16_kernel"),
                  ("gemm_x6_fl16_kernel", r"gemm_x6_fl16_kernel"),
