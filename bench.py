@@ -187,14 +187,14 @@ def parse():
                     help="steps per launch of the K-step rollout kernel line (0 = skip)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"))
     ap.add_argument("--kernel-stats",
-                    default=os.path.join(ROOT, "profiles", "r05_kernel_stats.csv"),
+                    default=os.path.join(ROOT, "profiles", "r06_kernel_stats.csv"),
                     help="rocprofv3 --stats csv whose kernel averages the ppo block reports")
     ap.add_argument("--rollout-grid-stats",
-                    default=os.path.join(ROOT, "profiles", "r05_rollout_grid_stats.json"),
+                    default=os.path.join(ROOT, "profiles", "r06_rollout_grid_stats.json"),
                     help="scripts/kernel_grid_stats.py output: the headline kernel's rocprof "
                          "durations at K = 32 on 65,536 envs")
     ap.add_argument("--pmc-rollout",
-                    default=os.path.join(ROOT, "profiles", "r05_pmc_rollout.json"),
+                    default=os.path.join(ROOT, "profiles", "r06_pmc_rollout.json"),
                     help="scripts/pmc_summary.py output of the K = 32 rollout kernel (its "
                          "VALU-active fractions are reported when it matches the tree)")
     ap.add_argument("--headline", choices=["rollout", "step"], default="rollout",
@@ -784,7 +784,7 @@ def rollout_rocprof_k32(path, n, state_dtype):
 
 def rocprof_averages(path):
     """{kernel name: average us} from a committed rocprofv3 --stats csv
-    (profiles/r05_kernel_stats.csv: scripts/r05_artifacts.sh's `kstats`
+    (profiles/r06_kernel_stats.csv: scripts/final_artifacts.sh's `kstats`
     run of this bench), or {} when absent."""
     import csv
     out = {}

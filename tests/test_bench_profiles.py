@@ -36,7 +36,27 @@ def test_committed_kernel_stats_cover_every_ppo_kernel():
     r5 = bench.rocprof_averages(os.path.join(ROOT, "profiles", "r05_kernel_stats.csv"))
     for k in set(bench.PPO_KERNEL_NAMES.values()) - fused_away - newer:
         assert k in r5 and r5[k] > 0, k
+    # round 6's summary (the bench's default --kernel-stats): every kernel the
+    # default step launches
+    r6 = bench.rocprof_averages(os.path.join(ROOT, "profiles", "r06_kernel_stats.csv"))
+    for k in set(bench.PPO_KERNEL_NAMES.values()) - fused_away:
+        assert k in r6 and r6[k] > 0, k
     assert bench.rocprof_averages(os.path.join(ROOT, "profiles", "no_such.csv")) == {}
+
+
+def test_round6_dominant_kernel_is_the_fused_input_gradient_gemm():
+    """The committed round-6 summary picks the kernel with the largest time
+    per optimizer step (the fused input-gradient GEMM, ~99 us) as the PPO
+    block's dominant kernel."""
+    class Cfg:
+        batch_size, num_envs, n_steps, n_epochs = 65536, 65536, 32, 10
+    rp = bench.rocprof_averages(os.path.join(ROOT, "profiles", "r06_kernel_stats.csv"))
+    ks = {n: 1.0 for n in bench.PPO_KERNEL_NAMES}
+    out = bench.ppo_roofline(Cfg, 0.13, ks, rp, {}, "profiles/r06_kernel_stats.csv")
+    d = out["dominant_kernel"]
+    assert d["kernel"] == "gemm_x6_fl16_kernel", d
+    assert d["us"] == max(e["rocprof_us"] for e in out["kernels_per_minibatch"].values()
+                          if "rocprof_us" in e and "bound" in e)
 
 
 def test_ppo_roofline_carries_rocprof_durations_and_fractions():
@@ -157,7 +177,7 @@ def test_grid_stats_split_the_probe_from_the_headline_launches(tmp_path):
 
 
 def test_pmc_valu_active_read_from_the_committed_summary():
-    p = os.path.join(ROOT, "profiles", "r05_pmc_rollout.json")
+    p = os.path.join(ROOT, "profiles", "r06_pmc_rollout.json")
     d = json.load(open(p))
     v = bench.pmc_rollout_valu_active(p)
     assert v["actions_from_hbm"] == d["actions_from_hbm"]["valu_active_frac_of_wave_cycles"]
