@@ -618,6 +618,12 @@ __global__ __launch_bounds__(XTHREADS) void gemm_x6_wgrad16_kernel(
                 load(g + 2 < G_ ? g + 2 : G_ - 1);
             }
         }
+        // the scheduler's MFMA / LDS-read interleave (iglp_opt(0)): 100-103
+        // vs 105-107 us per call, bitwise the same partials (alternating
+        // A/B, scripts/micro/r6m.sh, r6n.sh; a hand-written
+        // sched_group_barrier pipeline and the two waves of a SIMD splitting
+        // at different points of the stage measured equal or slower)
+        __builtin_amdgcn_iglp_opt(0);
         asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
     }
     // D[n][k] of tile (i, j): column k = 16 j + (lane & 15), row n =
