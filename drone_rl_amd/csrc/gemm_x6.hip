@@ -620,7 +620,7 @@ __global__ __launch_bounds__(XTHREADS) void gemm_x6_wgrad16_kernel(
         }
         // the scheduler's MFMA / LDS-read interleave (iglp_opt(0)): 100-103
         // vs 105-107 us per call, bitwise the same partials (alternating
-        // A/B, scripts/micro/r6m.sh, r6n.sh; a hand-written
+        // A/B, scripts/micro/r6_sessions.sh m, r6_sessions.sh n; a hand-written
         // sched_group_barrier pipeline and the two waves of a SIMD splitting
         // at different points of the stage measured equal or slower)
         __builtin_amdgcn_iglp_opt(0);
