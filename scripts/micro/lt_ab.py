@@ -37,14 +37,23 @@ s = torch.cuda.current_stream().cuda_stream
 xg = x[rows.long()].contiguous()       # the trainer's form: a gathered minibatch
 out = {"lib": os.path.basename(os.path.dirname(_lib.LIB_PATH)) + "/" +
        os.path.basename(_lib.LIB_PATH)}
-for mode, xx, rr in (("rows", x, ptr(rows)), ("dense", xg, None)):
+w256 = (torch.randn(2, 256, 256, generator=g) * 0.06).to(dev)
+img = torch.empty(2 * L.dr_gemm_x6_weights_bytes(2), dtype=torch.uint8, device=dev)
+ximg = torch.empty(L.dr_gemm_x6_x_bytes(a.m), dtype=torch.uint8, device=dev)
+for mode, xx, rr in (("rows", x, ptr(rows)), ("dense", xg, None), ("x6", xg, None)):
     def call():
-        check(L.dr_linear_tanh2(a.m, K, N, ptr(xx), rr, ptr(w[0]), ptr(b[0]), ptr(h[0]),
-                                ptr(w[1]), ptr(b[1]), ptr(h[1]), s))
+        if mode == "x6":   # the trainer's form: + both weight images and the obs image
+            check(L.dr_linear_tanh2_x6(a.m, K, N, ptr(xx), rr, ptr(w[0]), ptr(b[0]), ptr(h[0]),
+                                       ptr(w[1]), ptr(b[1]), ptr(h[1]), ptr(w256), ptr(img),
+                                       ptr(ximg), s))
+        else:
+            check(L.dr_linear_tanh2(a.m, K, N, ptr(xx), rr, ptr(w[0]), ptr(b[0]), ptr(h[0]),
+                                    ptr(w[1]), ptr(b[1]), ptr(h[1]), s))
     call()
     torch.cuda.synchronize()
-    sha = hashlib.sha256(h[0].cpu().numpy().tobytes() +
-                         h[1].cpu().numpy().tobytes()).hexdigest()[:16]
+    sha = hashlib.sha256(h[0].cpu().numpy().tobytes() + h[1].cpu().numpy().tobytes() +
+                         (img.cpu().numpy().tobytes() + ximg.cpu().numpy().tobytes()
+                          if mode == "x6" else b"")).hexdigest()[:16]
     ref = torch.tanh(xg.double() @ w[0].double().T + b[0].double())
     err = (h[0].double() - ref).abs().max().item()
     st, en = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)

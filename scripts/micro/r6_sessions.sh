@@ -125,5 +125,18 @@ o)
   for i in 1 2 3; do for v in wg0 wgnew; do DRONERL_LIB=scripts/micro/build/lib_$v.so timeout -k 10 200 python bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-companion > gpurun_out/r6o/b_${v}_$i.log 2>&1 || exit 1; python3 -c "import json,sys; d=json.loads([l for l in open(sys.argv[1]) if l.startswith('{')][-1]); print(sys.argv[2], d['ppo']['updates_per_s'], d['ppo']['roofline']['kernels_per_minibatch']['gemm_x6_wgrad'].get('isolated_us'))" gpurun_out/r6o/b_${v}_$i.log $v; done; done
   timeout -k 10 400 python -u -m pytest tests/test_gemm_x6_gpu.py tests/test_gemm_x6_fl_gpu.py tests/test_ppo_flagship_parity_gpu.py -q -x --timeout 200 --timeout-method thread 2>&1 | tail -3
   ;;
+p)
+  # the first-layer forward (dr_linear_tanh2_x6, the trainer's form, and the
+  # plain dr_linear_tanh2) under launch shapes: lt0 = HEAD (64 rows per
+  # block, <= 1,024 blocks per net); ltb512 = <= 512 blocks; ltb2k = 32 rows
+  # per block, <= 2,048; ltr128 = 128 rows, <= 512
+  for i in 1 2 3; do for v in lt0 ltb512 ltb2k ltr128; do DRONERL_LIB=scripts/micro/build/lib_$v.so timeout -k 10 120 python scripts/micro/lt_ab.py || exit 1; done; done
+  ;;
+q)
+  # the first-layer forward with its input rows loaded 1 (HEAD) / 2 / 3 / 4
+  # rows ahead (DR_LT_PF; scalar loads; the knob is not kept); lth / lthpf2: two waves per row
+  # (DR_LT_HALF: 50 VGPRs, 8 waves per SIMD), with PF 1 / 2
+  for i in 1 2 3; do for v in ltpf1 ltpf2 ltpf3 ltpf4 lth lthpf2; do DRONERL_LIB=scripts/micro/build/lib_$v.so timeout -k 10 120 python scripts/micro/lt_ab.py || exit 1; done; done
+  ;;
 *) echo "usage: $0 b|c|...|o"; exit 2 ;;
 esac
