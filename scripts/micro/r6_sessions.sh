@@ -138,5 +138,10 @@ q)
   # (DR_LT_HALF: 50 VGPRs, 8 waves per SIMD), with PF 1 / 2
   for i in 1 2 3; do for v in ltpf1 ltpf2 ltpf3 ltpf4 lth lthpf2; do DRONERL_LIB=scripts/micro/build/lib_$v.so timeout -k 10 120 python scripts/micro/lt_ab.py || exit 1; done; done
   ;;
+r)
+  # the record gather with the block's records loaded cooperatively into LDS
+  # (gc1: eight threads per 128-B record) against HEAD (gc0)
+  for i in 1 2 3; do for v in gc0 gc1; do DRONERL_LIB=scripts/micro/build/lib_$v.so timeout -k 10 120 python scripts/micro/gather_bench.py || exit 1; done; done
+  ;;
 *) echo "usage: $0 b|c|...|o"; exit 2 ;;
 esac
