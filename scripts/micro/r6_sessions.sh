@@ -143,5 +143,10 @@ r)
   # (gc1: eight threads per 128-B record) against HEAD (gc0)
   for i in 1 2 3; do for v in gc0 gc1; do DRONERL_LIB=scripts/micro/build/lib_$v.so timeout -k 10 120 python scripts/micro/gather_bench.py || exit 1; done; done
   ;;
+s)
+  # the weight gradient's stage-start reads: H tile 0 and G tile 0 issued
+  # first (wgo1, with iglp_opt(0); wgo1n without) against the product (wgc)
+  for i in 1 2 3; do for v in wgc wgo1 wgo1n; do DRONERL_LIB=scripts/micro/build/lib_$v.so timeout -k 10 120 python scripts/micro/wgrad_ab.py || exit 1; done; done
+  ;;
 *) echo "usage: $0 b|c|...|o"; exit 2 ;;
 esac
