@@ -17,6 +17,7 @@ Then stamp them: python scripts/provenance.py record <the files listed>.
 
 Usage: python scripts/make_profiles.py r06
 """
+import json
 import os
 import shutil
 import subprocess
@@ -45,7 +46,22 @@ def main():
     done = []
     for s, d in pairs:
         if os.path.exists(s) and os.path.getsize(s) > 0:
-            shutil.copy(s, os.path.join(out, d))
+            dst = os.path.join(out, d)
+            keep = {}
+            if d.endswith(".json") and os.path.exists(dst):
+                # blocks added to a committed summary by hand (an A/B record
+                # beside the counters) survive a re-copy of the counters
+                try:
+                    old, new = json.load(open(dst)), json.load(open(s))
+                    if isinstance(old, dict) and isinstance(new, dict):
+                        keep = {k: v for k, v in old.items() if k not in new and k.endswith("_ab")}
+                except ValueError:
+                    keep = {}
+            shutil.copy(s, dst)
+            if keep:
+                merged = json.load(open(dst))
+                merged.update(keep)
+                json.dump(merged, open(dst, "w"), indent=1)
             done.append(os.path.join("profiles", d))
     rt = os.path.join(src, "pmc_rollout_traffic")            # scripts/rollout_traffic.sh
     if os.path.isdir(rt):
