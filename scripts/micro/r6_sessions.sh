@@ -148,5 +148,23 @@ s)
   # first (wgo1, with iglp_opt(0); wgo1n without) against the product (wgc)
   for i in 1 2 3; do for v in wgc wgo1 wgo1n; do DRONERL_LIB=scripts/micro/build/lib_$v.so timeout -k 10 120 python scripts/micro/wgrad_ab.py || exit 1; done; done
   ;;
+t)
+  # the driver's multi-rank command form on the one-GPU box, both ranks on the
+  # card over gloo (RCCL refuses two ranks per device), then a second seed of
+  # the staged-curriculum convergence run on the final kernels
+  DRONERL_DIST_BACKEND=gloo timeout -k 10 600 python -m torch.distributed.run --nnodes=1 \
+    --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 \
+    --steps 20 --warmup 5 > gpurun_out/r06_n2_gloo.log 2>&1 || exit 1
+  grep '^{' gpurun_out/r06_n2_gloo.log | tail -1 > gpurun_out/r06_n2_gloo.json
+  ENT=0.01 TAG=r06_ppo_c3_staged_ent01 SEEDS=1 bash scripts/c3_staged.sh > gpurun_out/r06_c3_s1.log 2>&1
+  ;;
+u)
+  # the first layer's dot products on the x6 MFMA path (lm1: 512 blocks per
+  # net, 4-byte column stores; lm2 / lm2b: the transposed product with 16-byte
+  # row stores, 512 / 1,024 blocks) against the FMA-chain kernel (lm0); then the
+  # first-layer, x6 and PPO tests on lm2
+  for i in 1 2 3; do for v in lm0 lm1 lm2 lm2b; do DRONERL_LIB=scripts/micro/build/lib_$v.so timeout -k 10 120 python scripts/micro/lt_ab.py || exit 1; done; done
+  DRONERL_LIB=scripts/micro/build/lib_lm2.so timeout -k 10 600 python -u -m pytest tests/test_ppo_kernels_gpu.py tests/test_gemm_x6_fl_gpu.py tests/test_trainer_knobs_gpu.py tests/test_ppo_flagship_parity_gpu.py tests/test_ppo_gpu.py -q -x --timeout 200 --timeout-method thread 2>&1 | tail -15
+  ;;
 *) echo "usage: $0 b|c|...|o"; exit 2 ;;
 esac
