@@ -108,7 +108,7 @@ STAGED = ["r03_ppo_c3_staged_ent01_s0", "r03_ppo_c3_staged_ent01_s1",
           # round 5's kernels (fused first-layer backward, direct finishes)
           "r05_ppo_c3_staged_ent01_s0", "r05_ppo_c3_staged_ent01_s1",
           # round 6's kernels (16x16x32 x6 GEMMs, record gather)
-          "r06_ppo_c3_staged_ent01_s0"]
+          "r06_ppo_c3_staged_ent01_s0", "r06_ppo_c3_staged_ent01_s1"]
 
 
 def _eval(name):
